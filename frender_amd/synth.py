@@ -1,0 +1,247 @@
+"""SYN-v1: the seeded synthetic Illumina-style FASTQ generator.
+
+Every record is a pure function of (seed, global record index r), built from a
+counter-based hash, so the host generator here and the device generator kernel
+(`fr_synth_records` in csrc/fr_synth.hip) produce byte-identical streams, and a
+file split is just a range of r.  Records have a fixed length:
+
+    @SYN:1:FCX:1:{tile:04d}:{x:05d}:{y:05d} 1:N:0:{i1}+{i2}\\n   (36+L1+1+L2+1 B)
+    {seq: R bases}\\n+\\n{qual: R chars '!'..'J'}\\n               (2R+4 B)
+
+8+8 indexes, R=8 -> 74 B/record (the headline size); R=150 -> 358 B.
+
+Per read (hash fields k):  k=0 sample; k=1,2 index hop (2 %, idx2 of a random
+sample); k=3,4 fully random idx1+idx2 (1 %); k=8+j per index base j: 0.5 %
+substitution, 0.2 % 'N'; k=80.. sequence bases; k=100.. quality bytes.
+
+The sample sheets are generated with numpy's seeded PCG64 (seed 42 by default);
+indexes are drawn with a pairwise Hamming distance >= 3 within each index list,
+as real index kits are.
+"""
+from __future__ import annotations
+
+import csv
+import gzip
+import io
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+M64 = (1 << 64) - 1
+GOLDEN = 0x9E3779B97F4A7C15
+BASES = np.frombuffer(b"ACGT", dtype=np.uint8)
+RC_TABLE = bytes.maketrans(b"ATGCNatgcn", b"TACGNtacgn")
+
+# per-10000 rates of SYN-v1
+HOP_PER_10K = 200
+JUNK_PER_10K = 100
+SUB_PER_10K = 50
+N_PER_10K = 20
+
+
+def mix64_int(x: int) -> int:
+    """splitmix64 finalizer on a python int (mod 2^64)."""
+    x &= M64
+    x ^= x >> 30
+    x = (x * 0xBF58476D1CE4E5B9) & M64
+    x ^= x >> 27
+    x = (x * 0x94D049BB133111EB) & M64
+    x ^= x >> 31
+    return x
+
+
+def _mix64(x: np.ndarray) -> np.ndarray:
+    x = x.copy()
+    x ^= x >> np.uint64(30)
+    x *= np.uint64(0xBF58476D1CE4E5B9)
+    x ^= x >> np.uint64(27)
+    x *= np.uint64(0x94D049BB133111EB)
+    x ^= x >> np.uint64(31)
+    return x
+
+
+def seed_base(seed: int) -> int:
+    return mix64_int(seed + GOLDEN)
+
+
+def _h(base: int, r: np.ndarray, k: int) -> np.ndarray:
+    return _mix64(((r << np.uint64(8)) | np.uint64(k)) ^ np.uint64(base))
+
+
+@dataclass
+class Sheet:
+    ids: list
+    idx1: list
+    idx2: list
+
+    @property
+    def S(self) -> int:
+        return len(self.ids)
+
+    def write_csv(self, path: str, illumina: bool = False) -> None:
+        with open(path, "w", newline="") as f:
+            if illumina:
+                f.write("[Header]\nIEMFileVersion,4\nInvestigator Name,syn\n[Reads]\n151\n[Data]\n")
+            w = csv.writer(f, lineterminator="\n")
+            w.writerow(["Sample_ID", "Sample_Name", "index", "index2"])
+            for i, a, b in zip(self.ids, self.idx1, self.idx2):
+                w.writerow([i, i, a, b])
+
+
+def _draw_indexes(rng: np.random.Generator, count: int, length: int, min_dist: int = 3) -> list:
+    out: list = []
+    arr = np.zeros((0, length), dtype=np.uint8)
+    while len(out) < count:
+        cand = rng.integers(0, 4, size=length, dtype=np.uint8)
+        if arr.shape[0] and int(((arr != cand).sum(axis=1)).min()) < min_dist:
+            continue
+        arr = np.vstack([arr, cand[None, :]])
+        out.append(BASES[cand].tobytes().decode())
+    return out
+
+
+def make_sheet(S: int = 96, L1: int = 8, L2: int = 8, seed: int = 42,
+               combinatorial: tuple | None = None, prefix: str = "Sample_") -> Sheet:
+    """Unique-dual (default) or combinatorial (n1 x n2 grid) sample sheet."""
+    rng = np.random.default_rng(seed)
+    if combinatorial:
+        n1, n2 = combinatorial
+        i1 = _draw_indexes(rng, n1, L1)
+        i2 = _draw_indexes(rng, n2, L2)
+        pairs = [(a, b) for a in i1 for b in i2][:S]
+        idx1 = [p[0] for p in pairs]
+        idx2 = [p[1] for p in pairs]
+    else:
+        idx1 = _draw_indexes(rng, S, L1)
+        idx2 = _draw_indexes(rng, S, L2)
+    ids = [f"{prefix}{i + 1:03d}" for i in range(len(idx1))]
+    return Sheet(ids, idx1, idx2)
+
+
+def record_length(L1: int, L2: int, R: int) -> int:
+    return 36 + L1 + 1 + L2 + 1 + 2 * R + 4
+
+
+def _digits(v: np.ndarray, width: int) -> np.ndarray:
+    out = np.empty((v.shape[0], width), dtype=np.uint8)
+    v = v.copy()
+    for i in range(width - 1, -1, -1):
+        out[:, i] = (v % np.uint64(10)).astype(np.uint8) + ord("0")
+        v //= np.uint64(10)
+    return out
+
+
+def generate_records(sheet: Sheet, r0: int, n: int, R: int = 8, seed: int = 1,
+                     rc_names: set | None = None) -> np.ndarray:
+    """Records r0 .. r0+n-1 as an (n, reclen) uint8 array.
+
+    rc_names: samples whose reads carry the reverse complement of the sheet's
+    idx2 (to exercise -rc; the sheet itself is unchanged)."""
+    L1 = len(sheet.idx1[0])
+    L2 = len(sheet.idx2[0])
+    assert all(len(x) == L1 for x in sheet.idx1) and all(len(x) == L2 for x in sheet.idx2)
+    assert L1 + L2 <= 32 and R <= 256
+    S = sheet.S
+    base = seed_base(seed)
+    r = np.arange(r0, r0 + n, dtype=np.uint64)
+    reclen = record_length(L1, L2, R)
+    out = np.empty((n, reclen), dtype=np.uint8)
+
+    lut1 = np.frombuffer("".join(sheet.idx1).encode(), dtype=np.uint8).reshape(S, L1)
+    idx2_eff = [
+        (x.encode().translate(RC_TABLE)[::-1].decode() if rc_names and sheet.ids[i] in rc_names else x)
+        for i, x in enumerate(sheet.idx2)
+    ]
+    lut2 = np.frombuffer("".join(idx2_eff).encode(), dtype=np.uint8).reshape(S, L2)
+    code_of = np.zeros(256, dtype=np.uint8)
+    for c, v in zip(b"ACGT", range(4)):
+        code_of[c] = v
+
+    s = (_h(base, r, 0) % np.uint64(S)).astype(np.int64)
+    idx = np.concatenate([lut1[s], lut2[s]], axis=1)  # (n, L1+L2) ascii
+    hop = (_h(base, r, 1) % np.uint64(10000)) < np.uint64(HOP_PER_10K)
+    s2 = (_h(base, r, 2) % np.uint64(S)).astype(np.int64)
+    idx[hop, L1:] = lut2[s2[hop]]
+    junk = (_h(base, r, 3) % np.uint64(10000)) < np.uint64(JUNK_PER_10K)
+    if junk.any():
+        hj = _h(base, r[junk], 4)
+        jb = np.stack([((hj >> np.uint64(2 * j)) & np.uint64(3)).astype(np.uint8) for j in range(L1 + L2)], axis=1)
+        idx[junk] = BASES[jb]
+    for j in range(L1 + L2):
+        v = _h(base, r, 8 + j)
+        p = v % np.uint64(10000)
+        sub = p < np.uint64(SUB_PER_10K)
+        nn = (p >= np.uint64(SUB_PER_10K)) & (p < np.uint64(SUB_PER_10K + N_PER_10K))
+        if sub.any():
+            orig = code_of[idx[sub, j]]
+            new = (orig.astype(np.uint64) + np.uint64(1) + (v[sub] >> np.uint64(32)) % np.uint64(3)) % np.uint64(4)
+            idx[sub, j] = BASES[new.astype(np.int64)]
+        idx[nn, j] = ord("N")
+
+    pos = 0
+
+    def put(b: bytes):
+        nonlocal pos
+        out[:, pos:pos + len(b)] = np.frombuffer(b, dtype=np.uint8)
+        pos += len(b)
+
+    put(b"@SYN:1:FCX:1:")
+    out[:, pos:pos + 4] = _digits((r // np.uint64(10**10)) % np.uint64(10**4), 4); pos += 4
+    put(b":")
+    out[:, pos:pos + 5] = _digits((r // np.uint64(10**5)) % np.uint64(10**5), 5); pos += 5
+    put(b":")
+    out[:, pos:pos + 5] = _digits(r % np.uint64(10**5), 5); pos += 5
+    put(b" 1:N:0:")
+    out[:, pos:pos + L1] = idx[:, :L1]; pos += L1
+    put(b"+")
+    out[:, pos:pos + L2] = idx[:, L1:]; pos += L2
+    put(b"\n")
+    for w in range((R + 31) // 32):
+        hv = _h(base, r, 80 + w)
+        for j in range(32 * w, min(R, 32 * w + 32)):
+            out[:, pos + j] = BASES[((hv >> np.uint64(2 * (j - 32 * w))) & np.uint64(3)).astype(np.int64)]
+    pos += R
+    put(b"\n+\n")
+    for w in range((R + 7) // 8):
+        hv = _h(base, r, 100 + w)
+        for j in range(8 * w, min(R, 8 * w + 8)):
+            out[:, pos + j] = (((hv >> np.uint64(8 * (j - 8 * w))) & np.uint64(0xFF)) % np.uint64(42)).astype(np.uint8) + 33
+    pos += R
+    put(b"\n")
+    assert pos == reclen
+    return out
+
+
+def generate_bytes(sheet: Sheet, r0: int, n: int, R: int = 8, seed: int = 1, rc_names=None,
+                   block: int = 1 << 20) -> bytes:
+    parts = []
+    for a in range(r0, r0 + n, block):
+        b = min(block, r0 + n - a)
+        parts.append(generate_records(sheet, a, b, R=R, seed=seed, rc_names=rc_names).tobytes())
+    return b"".join(parts)
+
+
+def write_fastq_gz(path: str, data: bytes, level: int = 1, members: int = 1) -> None:
+    """Write decoded FASTQ bytes as gzip; members>1 writes a multi-member file
+    (split at arbitrary byte points, which Python's gzip reader concatenates)."""
+    with open(path, "wb") as f:
+        if members <= 1:
+            f.write(gzip.compress(data, compresslevel=level))
+        else:
+            cuts = np.linspace(0, len(data), members + 1).astype(np.int64)
+            for a, b in zip(cuts[:-1], cuts[1:]):
+                f.write(gzip.compress(data[a:b], compresslevel=level))
+
+
+def make_dataset(outdir: str, sheet: Sheet, n_reads: int, n_files: int = 1, R: int = 8, seed: int = 1,
+                 rc_names=None, name_fmt: str = "syn_L{f:03d}_R1_001.fastq.gz", level: int = 1) -> list:
+    """Split records [0, n_reads) into n_files gz files; return their paths."""
+    os.makedirs(outdir, exist_ok=True)
+    cuts = np.linspace(0, n_reads, n_files + 1).astype(np.int64)
+    paths = []
+    for f, (a, b) in enumerate(zip(cuts[:-1], cuts[1:])):
+        p = os.path.join(outdir, name_fmt.format(f=f + 1))
+        write_fastq_gz(p, generate_bytes(sheet, int(a), int(b - a), R=R, seed=seed, rc_names=rc_names), level=level)
+        paths.append(p)
+    return paths

@@ -1,0 +1,302 @@
+"""ctypes binding of libfrender_hip.so (include/frender_amd.h).
+
+There is no fallback: if the HIP library is missing or does not load, importing
+this module raises.  Build it with `python -c "import __graft_entry__ as g; g.build()"`.
+
+PyTorch (when importable) is imported first so that this process holds a single
+HIP runtime: torch ships its own libamdhip64.so.7 and our library's NEEDED entry
+then binds to that same copy, which lets torch.distributed (RCCL) move buffers
+that this library wrote.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+try:  # one HIP runtime per process (see module doc)
+    import torch  # noqa: F401
+except Exception:  # pragma: no cover - torch is plumbing only
+    torch = None
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("FRENDER_HIP_LIB", os.path.join(HERE, "libfrender_hip.so"))
+
+FR_OK = 0
+FR_SAMPLE_DONE = 5
+FR_SCAN_OK, FR_SCAN_NO_SPACE, FR_SCAN_UTF8 = 0, 1, 2
+CLASS_NAMES = ("undetermined", "index_hop", "demuxable", "ambiguous")
+
+
+class FrenderError(RuntimeError):
+    pass
+
+
+class FileStats(C.Structure):
+    _fields_ = [("records", C.c_uint64), ("lines", C.c_uint64), ("new_keys", C.c_uint64),
+                ("exotic", C.c_uint64), ("error", C.c_int32), ("pad", C.c_int32),
+                ("error_offset", C.c_uint64)]
+
+
+class Timing(C.Structure):
+    _fields_ = [("scan_launches", C.c_uint64), ("scan_bytes", C.c_uint64), ("scan_ms", C.c_double),
+                ("last_scan_ms", C.c_double), ("classify_ms", C.c_double), ("finalize_ms", C.c_double)]
+
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(f"frender_amd: HIP library {LIB_PATH} is not built (run __graft_entry__.build())")
+lib = C.CDLL(LIB_PATH)
+
+P = C.c_void_p
+u64p = C.POINTER(C.c_uint64)
+_SIGS = {
+    "fr_create": (P, [C.c_int, C.c_uint64, C.c_uint64]),
+    "fr_destroy": (None, [P]),
+    "fr_last_error": (C.c_char_p, [P]),
+    "fr_get_timing": (C.c_int, [P, C.POINTER(Timing)]),
+    "fr_sync": (C.c_int, [P]),
+    "fr_set_sheet": (C.c_int, [P, C.c_int, P, P, P, P, P, P, C.c_int, P, P, P, C.c_int]),
+    "fr_reset": (C.c_int, [P]),
+    "fr_begin_file": (C.c_int, [P, C.c_int64]),
+    "fr_feed": (C.c_int, [P, P, C.c_uint64]),
+    "fr_feed_device": (C.c_int, [P, P, C.c_uint64]),
+    "fr_end_file": (C.c_int, [P, C.POINTER(FileStats)]),
+    "fr_finalize": (C.c_int, [P, u64p, u64p, u64p]),
+    "fr_get_unique": (C.c_int, [P, P, P, P]),
+    "fr_get_presence": (C.c_int, [P, P, P]),
+    "fr_get_exotic": (C.c_int, [P, P, P, P, P, C.c_uint64]),
+    "fr_classify": (C.c_int, [P, C.c_int, C.c_int, P, P, P, P, P, P, P, P, P]),
+    "fr_rc_counts": (C.c_int, [P, P, P]),
+    "fr_classify_cp": (C.c_int, [P, C.c_int, P, P, P, P, C.c_int, C.c_int, C.c_int, P, P, P, P, P, P, P, P]),
+    "fr_export_unique_device": (C.c_int, [P, P, P, P, C.c_uint64]),
+    "fr_merge_unique_device": (C.c_int, [P, P, P, P, C.c_uint64]),
+    "fr_device_alloc": (P, [P, C.c_uint64]),
+    "fr_device_free": (C.c_int, [P, P]),
+    "fr_copy_to_host": (C.c_int, [P, P, P, C.c_uint64]),
+    "fr_copy_to_device": (C.c_int, [P, P, P, C.c_uint64]),
+    "fr_synth_device": (C.c_int, [P, P, C.c_uint64, C.c_uint64, C.c_int, C.c_uint64, C.c_char_p, C.c_char_p,
+                                  C.c_int, C.c_int, C.c_int]),
+}
+for _name, (_res, _args) in _SIGS.items():
+    _f = getattr(lib, _name)
+    _f.restype = _res
+    _f.argtypes = _args
+
+EXPORTED = tuple(_SIGS)
+
+
+def _ptr(a: np.ndarray | None):
+    return None if a is None else a.ctypes.data_as(P)
+
+
+M21 = np.arange(21, dtype=np.uint64) * np.uint64(3)
+SYM_LUT = np.frombuffer(b"\0ACGTN+\0", dtype=np.uint8)
+
+
+def decode_keys(keys: np.ndarray) -> list:
+    """3-bit packed fast keys -> code strings (char i at bits [3i, 3i+3))."""
+    if keys.size == 0:
+        return []
+    syms = ((keys[:, None] >> M21[None, :]) & np.uint64(7)).astype(np.uint8)
+    raw = np.ascontiguousarray(SYM_LUT[syms]).view("S21").ravel()
+    return [b.decode("ascii") for b in raw.tolist()]
+
+
+def pack_lower(s: str) -> int:
+    """Sheet entry -> 3-bit packed case-folded chars (a1 c2 g3 t4 n5 other 7); 0 if > 21 chars."""
+    if len(s) > 21:
+        return 0
+    v = 0
+    for i, ch in enumerate(s):
+        v |= {"a": 1, "c": 2, "g": 3, "t": 4, "n": 5}.get(ch, 7) << (3 * i)
+    return v
+
+
+class Context:
+    """One GPU's scan state (fr_ctx)."""
+
+    def __init__(self, device: int = 0, chunk_bytes: int = 256 << 20, table_slots: int = 1 << 20):
+        self.h = lib.fr_create(device, chunk_bytes, table_slots)
+        if not self.h:
+            raise FrenderError("fr_create returned NULL")
+        err = lib.fr_last_error(self.h)
+        if err:
+            raise FrenderError(f"fr_create: {err.decode()}")
+        self.n_names = 0
+
+    def close(self):
+        if self.h:
+            lib.fr_destroy(self.h)
+            self.h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _ck(self, rc: int, what: str) -> int:
+        if rc not in (FR_OK, FR_SAMPLE_DONE):
+            raise FrenderError(f"{what} failed ({rc}): {lib.fr_last_error(self.h).decode()}")
+        return rc
+
+    # ---- sheet ----------------------------------------------------------------------
+    def set_sheet(self, idx1: list, idx2: list, idx2rc: list, name_id: list, n_names: int):
+        S = len(idx1)
+        l1 = [s.lower() for s in idx1]
+        l2 = [s.lower() for s in idx2]
+        l2rc = [s.lower() for s in idx2rc]
+        p1 = np.array([pack_lower(s) for s in l1], dtype=np.uint64)
+        p2 = np.array([pack_lower(s) for s in l2], dtype=np.uint64)
+        p2rc = np.array([pack_lower(s) for s in l2rc], dtype=np.uint64)
+        len1 = np.array([len(s) for s in l1], dtype=np.int32)
+        len2 = np.array([len(s) for s in l2], dtype=np.int32)
+        nid = np.array(name_id, dtype=np.int32)
+        stride = max([1] + [len(s) for s in l1 + l2])
+        self.cp_stride = stride
+        cp = [np.zeros((S, stride), dtype=np.uint32) for _ in range(3)]
+        for arr, strs in zip(cp, (l1, l2, l2rc)):
+            for i, s in enumerate(strs):
+                arr[i, :len(s)] = [ord(ch) for ch in s]
+        self._sheet_keep = (p1, p2, p2rc, len1, len2, nid, cp)
+        self.n_names = n_names
+        self._ck(lib.fr_set_sheet(self.h, S, _ptr(p1), _ptr(len1), _ptr(p2), _ptr(len2), _ptr(p2rc), _ptr(nid),
+                                  n_names, _ptr(cp[0]), _ptr(cp[1]), _ptr(cp[2]), stride), "fr_set_sheet")
+
+    # ---- tally ----------------------------------------------------------------------
+    def reset(self):
+        self._ck(lib.fr_reset(self.h), "fr_reset")
+
+    def begin_file(self, max_records: int | None):
+        self._ck(lib.fr_begin_file(self.h, int(max_records or 0)), "fr_begin_file")
+
+    def feed(self, data) -> bool:
+        """Feed decoded bytes; returns True once the -s sample limit is reached."""
+        buf = C.c_char_p(data) if isinstance(data, bytes) else None
+        if buf is not None:
+            rc = lib.fr_feed(self.h, C.cast(buf, P), len(data))
+        else:
+            a = np.frombuffer(data, dtype=np.uint8)
+            rc = lib.fr_feed(self.h, _ptr(a), a.size)
+        return self._ck(rc, "fr_feed") == FR_SAMPLE_DONE
+
+    def feed_device(self, dev_ptr: int, nbytes: int):
+        self._ck(lib.fr_feed_device(self.h, P(dev_ptr), nbytes), "fr_feed_device")
+
+    def end_file(self) -> FileStats:
+        st = FileStats()
+        self._ck(lib.fr_end_file(self.h, C.byref(st)), "fr_end_file")
+        return st
+
+    # ---- unique table ---------------------------------------------------------------
+    def finalize(self):
+        u, p, e = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        self._ck(lib.fr_finalize(self.h, C.byref(u), C.byref(p), C.byref(e)), "fr_finalize")
+        self.U, self.NP, self.NE = u.value, p.value, e.value
+        return self.U, self.NP, self.NE
+
+    def unique(self):
+        keys = np.empty(self.U, dtype=np.uint64)
+        counts = np.empty(self.U, dtype=np.uint64)
+        first = np.empty(self.U, dtype=np.uint64)
+        self._ck(lib.fr_get_unique(self.h, _ptr(keys), _ptr(counts), _ptr(first)), "fr_get_unique")
+        return keys, counts, first
+
+    def presence(self):
+        u = np.empty(self.NP, dtype=np.uint32)
+        f = np.empty(self.NP, dtype=np.uint32)
+        self._ck(lib.fr_get_presence(self.h, _ptr(u), _ptr(f)), "fr_get_presence")
+        return u, f
+
+    def exotic(self):
+        n = self.NE
+        ords = np.empty(n, dtype=np.uint64)
+        lens = np.empty(n, dtype=np.uint32)
+        offs = np.empty(n, dtype=np.uint64)
+        self._ck(lib.fr_get_exotic(self.h, _ptr(ords), _ptr(lens), _ptr(offs), None, 0), "fr_get_exotic")
+        pool_bytes = int((offs + lens).max()) if n else 0
+        pool = np.empty(max(pool_bytes, 1), dtype=np.uint8)
+        self._ck(lib.fr_get_exotic(self.h, _ptr(ords), _ptr(lens), _ptr(offs), _ptr(pool), pool_bytes),
+                 "fr_get_exotic")
+        return ords, lens, offs, pool
+
+    # ---- classify -------------------------------------------------------------------
+    def classify(self, num_subs: int, rc: bool, to_host: bool = True):
+        """Classify the finalized table on the GPU; to_host=False leaves the results in HBM."""
+        n = self.U if to_host else 0
+        out = {k: (np.empty(n, dtype=np.int16) if to_host else None) for k in ("m1", "m2", "row", "rc_m2", "rc_row")}
+        out["cls"] = np.empty(n, dtype=np.uint8) if to_host else None
+        out["rc_cls"] = np.empty(n, dtype=np.uint8) if to_host else None
+        eu, ew = C.c_int64(), C.c_int32()
+        self._ck(lib.fr_classify(self.h, num_subs, 1 if rc else 0, _ptr(out["m1"]), _ptr(out["m2"]),
+                                 _ptr(out["cls"]), _ptr(out["row"]), _ptr(out["rc_m2"]), _ptr(out["rc_cls"]),
+                                 _ptr(out["rc_row"]), C.byref(eu), C.byref(ew)), "fr_classify")
+        out["err_unique"], out["err_which"] = eu.value, ew.value
+        return out
+
+    def rc_counts(self):
+        f = np.zeros(max(self.n_names, 1), dtype=np.uint64)
+        r = np.zeros(max(self.n_names, 1), dtype=np.uint64)
+        self._ck(lib.fr_rc_counts(self.h, _ptr(f), _ptr(r)), "fr_rc_counts")
+        return f[:self.n_names], r[:self.n_names]
+
+    def classify_cp(self, q1: list, q2: list, num_subs: int, rc: bool):
+        n = len(q1)
+        stride = self.cp_stride
+        a1 = np.zeros((n, stride), dtype=np.uint32)
+        a2 = np.zeros((n, stride), dtype=np.uint32)
+        for i, (x, y) in enumerate(zip(q1, q2)):
+            a1[i, :min(len(x), stride)] = [ord(c) for c in x[:stride]]
+            a2[i, :min(len(y), stride)] = [ord(c) for c in y[:stride]]
+        l1 = np.array([len(x) for x in q1], dtype=np.int32)
+        l2 = np.array([len(y) for y in q2], dtype=np.int32)
+        out = {k: np.empty(n, dtype=np.int16) for k in ("m1", "m2", "row", "rc_m2", "rc_row")}
+        out["cls"] = np.empty(n, dtype=np.uint8)
+        out["rc_cls"] = np.empty(n, dtype=np.uint8)
+        out["err"] = np.zeros(n, dtype=np.int32)
+        self._ck(lib.fr_classify_cp(self.h, n, _ptr(a1), _ptr(l1), _ptr(a2), _ptr(l2), stride, num_subs,
+                                    1 if rc else 0, _ptr(out["m1"]), _ptr(out["m2"]), _ptr(out["cls"]),
+                                    _ptr(out["row"]), _ptr(out["rc_m2"]), _ptr(out["rc_cls"]), _ptr(out["rc_row"]),
+                                    _ptr(out["err"])), "fr_classify_cp")
+        return out
+
+    # ---- device memory / synthetic data / timing --------------------------------------
+    def device_alloc(self, nbytes: int) -> int:
+        p = lib.fr_device_alloc(self.h, nbytes)
+        if not p:
+            raise FrenderError(f"fr_device_alloc({nbytes}) failed")
+        return p
+
+    def device_free(self, p: int):
+        self._ck(lib.fr_device_free(self.h, P(p)), "fr_device_free")
+
+    def copy_to_host(self, dev_ptr: int, nbytes: int) -> bytes:
+        out = np.empty(nbytes, dtype=np.uint8)
+        self._ck(lib.fr_copy_to_host(self.h, _ptr(out), P(dev_ptr), nbytes), "fr_copy_to_host")
+        return out.tobytes()
+
+    def copy_to_device(self, dev_ptr: int, data: bytes):
+        a = np.frombuffer(data, dtype=np.uint8)
+        self._ck(lib.fr_copy_to_device(self.h, P(dev_ptr), _ptr(a), a.size), "fr_copy_to_device")
+
+    def synth_device(self, dev_ptr: int, r0: int, n: int, R: int, seed: int, idx1: list, idx2: list):
+        L1, L2 = len(idx1[0]), len(idx2[0])
+        self._ck(lib.fr_synth_device(self.h, P(dev_ptr), r0, n, R, seed, "".join(idx1).encode(),
+                                     "".join(idx2).encode(), len(idx1), L1, L2), "fr_synth_device")
+
+    def timing(self) -> Timing:
+        t = Timing()
+        self._ck(lib.fr_get_timing(self.h, C.byref(t)), "fr_get_timing")
+        return t
+
+    def sync(self):
+        self._ck(lib.fr_sync(self.h), "fr_sync")
+
+    def export_unique_device(self, keys_ptr: int, counts_ptr: int, first_ptr: int, cap: int):
+        self._ck(lib.fr_export_unique_device(self.h, P(keys_ptr), P(counts_ptr), P(first_ptr), cap),
+                 "fr_export_unique_device")
+
+    def merge_unique_device(self, keys_ptr: int, counts_ptr: int, first_ptr: int, n: int):
+        self._ck(lib.fr_merge_unique_device(self.h, P(keys_ptr), P(counts_ptr), P(first_ptr), n),
+                 "fr_merge_unique_device")

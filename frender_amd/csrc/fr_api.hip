@@ -1,0 +1,877 @@
+// fr_api.hip — the C ABI of libfrender_hip.so (declared in include/frender_amd.h).
+//
+// Host-side owner of one GPU's scan state: the pinned ring for host feeds, the HBM hash
+// table (grown between launches, never during one: the overflow list absorbs in-flight
+// growth), the look-back descriptors, the sheet image, and the finalized unique table.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/frender_amd.h"
+#include "fr_internal.h"
+
+using namespace fr;
+
+struct fr_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;  // tally / classify / table kernels
+    hipStream_t copy = nullptr;    // H2D of host feeds
+    std::string err;
+    int grid = 0;
+
+    DevState* st = nullptr;
+    DevState* h_st = nullptr;      // pinned snapshot
+    hipEvent_t st_ev = nullptr;
+    bool st_pending = false;
+    u64* tiles = nullptr;
+    u64 tiles_cap = 0;
+    u32 epoch = 0;
+    u32 par = 0;
+
+    Table tab{};
+    u64 nslots = 0;
+
+    // host feed ring
+    u64 chunk_bytes = 0;
+    u8* pin[2] = {nullptr, nullptr};
+    u8* dbuf[2] = {nullptr, nullptr};
+    hipEvent_t copied[2] = {nullptr, nullptr};
+    hipEvent_t consumed[2] = {nullptr, nullptr};
+    bool used[2] = {false, false};
+    int cur = 0;
+    std::vector<u8> carry;
+
+    // current file
+    bool scanning = false;
+    bool file_open = false;
+    u32 file_tag = 0;
+    u64 file_offset = 0;
+    i64 max_records = 0;
+    int last_byte = -1;
+    u64 pres_before = 0;
+    u64 exo_before = 0;
+    bool sample_done = false;
+
+    // sheet
+    int S = -1;
+    int n_names = 0;
+    int L1u = -1, L2u = -1;
+    u64 *d_i1 = nullptr, *d_i2 = nullptr, *d_i2rc = nullptr;
+    int32_t* d_name = nullptr;
+    u32 *d_cp1 = nullptr, *d_cp2 = nullptr, *d_cp2rc = nullptr;
+    int32_t *d_cpl1 = nullptr, *d_cpl2 = nullptr;
+    int cp_stride = 0;
+
+    // finalized table
+    u64 U = 0;
+    u64 ucap = 0;
+    u64 *d_keys = nullptr, *d_counts = nullptr, *d_first = nullptr;
+    u64 *d_keys_s = nullptr, *d_counts_s = nullptr, *d_first_s = nullptr;
+    u32 *d_pos = nullptr, *d_perm = nullptr, *d_rank = nullptr;
+    u64* d_counter = nullptr;
+    void* d_temp = nullptr;
+    size_t temp_bytes = 0;
+    u64 n_pres = 0;
+    u64 pmap_cap = 0;
+    u32 *d_pres_u = nullptr, *d_pres_f = nullptr;
+    u64 n_exo = 0;
+
+    // classify scratch
+    u64 ccap = 0;
+    int16_t *d_m1 = nullptr, *d_m2 = nullptr, *d_row = nullptr, *d_rm2 = nullptr, *d_rrow = nullptr;
+    u8 *d_cls = nullptr, *d_rcls = nullptr;
+    int32_t* d_errw = nullptr;
+    u64* d_errf = nullptr;
+    u64 *d_rcf = nullptr, *d_rcr = nullptr;
+    int rc_names_cap = 0;
+
+    // timing
+    std::vector<hipEvent_t> ev_a, ev_b;
+    size_t ev_used = 0;
+    u64 scan_launches = 0, scan_bytes = 0;
+    double classify_ms = 0, finalize_ms = 0;
+};
+
+#define CK(x)                                                                                  \
+    do {                                                                                       \
+        hipError_t e_ = (x);                                                                   \
+        if (e_ != hipSuccess) {                                                                \
+            ctx->err = std::string(#x) + ": " + hipGetErrorString(e_);                         \
+            return FR_ERR_HIP;                                                                 \
+        }                                                                                      \
+    } while (0)
+
+static int fail(fr_ctx* ctx, int code, const std::string& msg) {
+    ctx->err = msg;
+    return code;
+}
+
+template <class T>
+static hipError_t dalloc(T** p, u64 n) {
+    return hipMalloc((void**)p, std::max<u64>(n, 1) * sizeof(T));
+}
+
+static u64 pow2_at_least(u64 x) {
+    u64 p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+static int state_reset_counts(fr_ctx* ctx) {
+    DevState z;
+    std::memset(&z, 0, sizeof(z));
+    z.err_nospace = ~0ull;
+    CK(hipStreamSynchronize(ctx->stream));
+    *ctx->h_st = z;
+    CK(hipMemcpyAsync(ctx->st, ctx->h_st, sizeof(DevState), hipMemcpyHostToDevice, ctx->stream));
+    CK(hipStreamSynchronize(ctx->stream));
+    return FR_OK;
+}
+
+static int read_state(fr_ctx* ctx) {  // synchronous exact snapshot
+    CK(hipMemcpyAsync(ctx->h_st, ctx->st, sizeof(DevState), hipMemcpyDeviceToHost, ctx->stream));
+    CK(hipStreamSynchronize(ctx->stream));
+    ctx->st_pending = false;
+    return FR_OK;
+}
+
+// grow the table (x4) and/or re-insert overflow entries; stream-ordered between launches
+static int grow_table(fr_ctx* ctx, bool force_bigger) {
+    int rc = read_state(ctx);
+    if (rc) return rc;
+    const u64 nkeys = ctx->h_st->n_keys;
+    const u64 novf = std::min<u64>(ctx->h_st->n_overflow, ctx->tab.ovf_cap);
+    if (force_bigger || (nkeys + novf) * 2 > ctx->nslots) {
+        u64 ns = ctx->nslots;
+        while ((nkeys + novf) * 4 > ns) ns <<= 1;
+        if (ns == ctx->nslots) ns <<= 1;
+        GSlot* ns_slots = nullptr;
+        CK(dalloc(&ns_slots, ns));
+        CK(launch_table_init(ns_slots, ns, ctx->stream));
+        Table t = ctx->tab;
+        t.slots = ns_slots;
+        t.mask = ns - 1;
+        CK(launch_rehash(t, ctx->st, ctx->tab.slots, ctx->nslots, ctx->stream));
+        CK(hipStreamSynchronize(ctx->stream));
+        CK(hipFree(ctx->tab.slots));
+        ctx->tab = t;
+        ctx->nslots = ns;
+    }
+    if (novf) {
+        Overflow* old = ctx->tab.ovf;
+        Overflow* fresh = nullptr;
+        CK(dalloc(&fresh, ctx->tab.ovf_cap));
+        ctx->tab.ovf = fresh;
+        CK(hipMemsetAsync(&ctx->st->n_overflow, 0, sizeof(u64), ctx->stream));
+        CK(launch_reinsert_overflow(ctx->tab, ctx->st, old, novf, ctx->stream));
+        CK(hipStreamSynchronize(ctx->stream));
+        CK(hipFree(old));
+    }
+    // presence list: keep at least half free
+    rc = read_state(ctx);
+    if (rc) return rc;
+    if (ctx->h_st->n_presence * 2 > ctx->tab.pres_cap) {
+        const u64 ncap = ctx->tab.pres_cap * 4;
+        Presence* np = nullptr;
+        CK(dalloc(&np, ncap));
+        CK(hipMemcpyAsync(np, ctx->tab.pres, std::min(ctx->h_st->n_presence, ctx->tab.pres_cap) * sizeof(Presence),
+                          hipMemcpyDeviceToDevice, ctx->stream));
+        CK(hipStreamSynchronize(ctx->stream));
+        CK(hipFree(ctx->tab.pres));
+        ctx->tab.pres = np;
+        ctx->tab.pres_cap = ncap;
+    }
+    return FR_OK;
+}
+
+// called before each tally launch: act on the latest asynchronous snapshot, if ready
+static int maybe_grow(fr_ctx* ctx) {
+    if (!ctx->st_pending) return FR_OK;
+    if (hipEventQuery(ctx->st_ev) != hipSuccess) return FR_OK;
+    ctx->st_pending = false;
+    const DevState& s = *ctx->h_st;
+    if (s.n_overflow || s.n_keys * 2 > ctx->nslots || s.n_presence * 2 > ctx->tab.pres_cap) return grow_table(ctx, false);
+    return FR_OK;
+}
+
+static int snapshot_async(fr_ctx* ctx) {
+    CK(hipMemcpyAsync(ctx->h_st, ctx->st, sizeof(DevState), hipMemcpyDeviceToHost, ctx->stream));
+    CK(hipEventRecord(ctx->st_ev, ctx->stream));
+    ctx->st_pending = true;
+    return FR_OK;
+}
+
+static int launch_range(fr_ctx* ctx, const u8* dptr, u64 len, u64 avail, int own_start, int own_end, int pre_valid) {
+    if (len == 0) return FR_OK;
+    int rc = maybe_grow(ctx);
+    if (rc) return rc;
+    ScanArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.buf = dptr;
+    a.len = len;
+    a.avail = avail;
+    a.file_offset = ctx->file_offset;
+    a.file_tag = ctx->file_tag;
+    a.par = ctx->par;
+    a.epoch = ++ctx->epoch;
+    a.num_tiles = (u32)((len + TILE - 1) / TILE);
+    a.own_start = own_start;
+    a.own_end = own_end;
+    a.pre_valid = pre_valid;
+    a.max_records = ctx->max_records;
+    a.st = ctx->st;
+    a.tiles = ctx->tiles;
+    a.tab = ctx->tab;
+    if (a.num_tiles > ctx->tiles_cap) return fail(ctx, FR_ERR_INVALID, "range larger than the look-back array");
+    if (ctx->epoch >= 0x7FFFFFFFu) {  // tag wrap: restart epochs on a cleared descriptor array
+        CK(hipMemsetAsync(ctx->tiles, 0, ctx->tiles_cap * sizeof(u64), ctx->stream));
+        ctx->epoch = 1;
+        a.epoch = 1;
+    }
+    CK(hipMemsetAsync(&ctx->st->ticket, 0, sizeof(u32), ctx->stream));
+    if (ctx->ev_used == ctx->ev_a.size()) {
+        hipEvent_t e1, e2;
+        CK(hipEventCreate(&e1));
+        CK(hipEventCreate(&e2));
+        ctx->ev_a.push_back(e1);
+        ctx->ev_b.push_back(e2);
+    }
+    CK(hipEventRecord(ctx->ev_a[ctx->ev_used], ctx->stream));
+    const int grid = (int)std::min<u64>((u64)ctx->grid, a.num_tiles);
+    CK(launch_scan(a, grid, ctx->stream));
+    CK(hipEventRecord(ctx->ev_b[ctx->ev_used], ctx->stream));
+    ctx->ev_used++;
+    ctx->scan_launches++;
+    ctx->scan_bytes += len;
+    ctx->par ^= 1u;
+    ctx->file_offset += len;
+    return snapshot_async(ctx);
+}
+
+extern "C" {
+
+fr_ctx* fr_create(int device, uint64_t chunk_bytes, uint64_t table_slots) {
+    fr_ctx* ctx = new fr_ctx();
+    ctx->device = device;
+    auto bad = [&](const char* what, hipError_t e) {
+        ctx->err = std::string(what) + ": " + hipGetErrorString(e);
+        return ctx;  // caller inspects fr_last_error; the context is unusable
+    };
+    hipError_t e;
+    if ((e = hipSetDevice(device)) != hipSuccess) return bad("hipSetDevice", e);
+    if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess) return bad("stream", e);
+    if ((e = hipStreamCreateWithFlags(&ctx->copy, hipStreamNonBlocking)) != hipSuccess) return bad("stream", e);
+    hipDeviceProp_t prop;
+    if ((e = hipGetDeviceProperties(&prop, device)) != hipSuccess) return bad("props", e);
+    const int per_cu = 2;  // LDS-bound: ~58 KB per workgroup -> 2 per CU
+    ctx->grid = prop.multiProcessorCount * per_cu;
+
+    ctx->chunk_bytes = chunk_bytes ? ((chunk_bytes + TILE - 1) / TILE) * TILE : (256ull << 20);
+    if (ctx->chunk_bytes > RANGE_MAX) ctx->chunk_bytes = RANGE_MAX;
+    ctx->tiles_cap = RANGE_MAX / TILE + 2;
+    ctx->nslots = pow2_at_least(std::max<u64>(table_slots, 1024));
+    if ((e = hipMalloc((void**)&ctx->st, sizeof(DevState))) != hipSuccess) return bad("state", e);
+    if ((e = hipHostMalloc((void**)&ctx->h_st, sizeof(DevState), hipHostMallocDefault)) != hipSuccess)
+        return bad("pinned state", e);
+    if ((e = hipEventCreateWithFlags(&ctx->st_ev, hipEventDisableTiming)) != hipSuccess) return bad("event", e);
+    if ((e = dalloc(&ctx->tiles, ctx->tiles_cap)) != hipSuccess) return bad("tiles", e);
+    if ((e = hipMemset(ctx->tiles, 0, ctx->tiles_cap * sizeof(u64))) != hipSuccess) return bad("tiles", e);
+    if ((e = dalloc(&ctx->tab.slots, ctx->nslots)) != hipSuccess) return bad("table", e);
+    ctx->tab.mask = ctx->nslots - 1;
+    ctx->tab.ovf_cap = 1ull << 22;
+    ctx->tab.pres_cap = 1ull << 22;
+    ctx->tab.exo_cap = 1ull << 20;
+    ctx->tab.exo_pool_cap = 64ull << 20;
+    if ((e = dalloc(&ctx->tab.ovf, ctx->tab.ovf_cap)) != hipSuccess) return bad("overflow", e);
+    if ((e = dalloc(&ctx->tab.pres, ctx->tab.pres_cap)) != hipSuccess) return bad("presence", e);
+    if ((e = dalloc(&ctx->tab.exo_ord, ctx->tab.exo_cap)) != hipSuccess) return bad("exotic", e);
+    if ((e = dalloc(&ctx->tab.exo_off, ctx->tab.exo_cap)) != hipSuccess) return bad("exotic", e);
+    if ((e = dalloc(&ctx->tab.exo_len, ctx->tab.exo_cap)) != hipSuccess) return bad("exotic", e);
+    if ((e = dalloc(&ctx->tab.exo_pool, ctx->tab.exo_pool_cap)) != hipSuccess) return bad("exotic", e);
+    for (int i = 0; i < 2; ++i) {
+        if ((e = hipHostMalloc((void**)&ctx->pin[i], ctx->chunk_bytes, hipHostMallocDefault)) != hipSuccess)
+            return bad("pinned ring", e);
+        if ((e = dalloc(&ctx->dbuf[i], ctx->chunk_bytes + 64)) != hipSuccess) return bad("device ring", e);
+        if ((e = hipEventCreateWithFlags(&ctx->copied[i], hipEventDisableTiming)) != hipSuccess) return bad("event", e);
+        if ((e = hipEventCreateWithFlags(&ctx->consumed[i], hipEventDisableTiming)) != hipSuccess)
+            return bad("event", e);
+        if ((e = hipEventRecord(ctx->consumed[i], ctx->stream)) != hipSuccess) return bad("event", e);
+    }
+    if ((e = dalloc(&ctx->d_counter, 1)) != hipSuccess) return bad("counter", e);
+    if (fr_reset(ctx) != FR_OK) return ctx;
+    ctx->err.clear();
+    return ctx;
+}
+
+void fr_destroy(fr_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->copy) (void)hipStreamSynchronize(ctx->copy);
+    void* dev[] = {ctx->st, ctx->tiles, ctx->tab.slots, ctx->tab.ovf, ctx->tab.pres, ctx->tab.exo_ord,
+                   ctx->tab.exo_off, ctx->tab.exo_len, ctx->tab.exo_pool, ctx->dbuf[0], ctx->dbuf[1], ctx->d_i1,
+                   ctx->d_i2, ctx->d_i2rc, ctx->d_name, ctx->d_cp1, ctx->d_cp2, ctx->d_cp2rc, ctx->d_cpl1,
+                   ctx->d_cpl2, ctx->d_keys, ctx->d_counts, ctx->d_first, ctx->d_keys_s, ctx->d_counts_s,
+                   ctx->d_first_s, ctx->d_pos, ctx->d_perm, ctx->d_rank, ctx->d_counter, ctx->d_temp, ctx->d_pres_u,
+                   ctx->d_pres_f, ctx->d_m1, ctx->d_m2, ctx->d_row, ctx->d_rm2, ctx->d_rrow, ctx->d_cls, ctx->d_rcls,
+                   ctx->d_errw, ctx->d_errf, ctx->d_rcf, ctx->d_rcr};
+    for (void* p : dev)
+        if (p) (void)hipFree(p);
+    if (ctx->h_st) (void)hipHostFree(ctx->h_st);
+    for (int i = 0; i < 2; ++i) {
+        if (ctx->pin[i]) (void)hipHostFree(ctx->pin[i]);
+        if (ctx->copied[i]) (void)hipEventDestroy(ctx->copied[i]);
+        if (ctx->consumed[i]) (void)hipEventDestroy(ctx->consumed[i]);
+    }
+    for (auto e : ctx->ev_a) (void)hipEventDestroy(e);
+    for (auto e : ctx->ev_b) (void)hipEventDestroy(e);
+    if (ctx->st_ev) (void)hipEventDestroy(ctx->st_ev);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    if (ctx->copy) (void)hipStreamDestroy(ctx->copy);
+    delete ctx;
+}
+
+const char* fr_last_error(const fr_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int fr_sync(fr_ctx* ctx) {
+    CK(hipStreamSynchronize(ctx->stream));
+    CK(hipStreamSynchronize(ctx->copy));
+    return FR_OK;
+}
+
+int fr_get_timing(fr_ctx* ctx, fr_timing* out) {
+    CK(hipStreamSynchronize(ctx->stream));
+    double tot = 0, last = 0;
+    for (size_t i = 0; i < ctx->ev_used; ++i) {
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, ctx->ev_a[i], ctx->ev_b[i]));
+        tot += ms;
+        last = ms;
+    }
+    out->scan_launches = ctx->scan_launches;
+    out->scan_bytes = ctx->scan_bytes;
+    out->scan_ms = tot;
+    out->last_scan_ms = last;
+    out->classify_ms = ctx->classify_ms;
+    out->finalize_ms = ctx->finalize_ms;
+    return FR_OK;
+}
+
+int fr_set_sheet(fr_ctx* ctx, int S, const uint64_t* idx1_packed, const int32_t* idx1_len,
+                 const uint64_t* idx2_packed, const int32_t* idx2_len, const uint64_t* idx2rc_packed,
+                 const int32_t* name_id, int n_names, const uint32_t* idx1_cp, const uint32_t* idx2_cp,
+                 const uint32_t* idx2rc_cp, int cp_stride) {
+    if (S < 0 || S > 32767) return fail(ctx, FR_ERR_INVALID, "sheet rows must be in [0, 32767]");
+    CK(hipStreamSynchronize(ctx->stream));
+    void* old[] = {ctx->d_i1, ctx->d_i2, ctx->d_i2rc, ctx->d_name, ctx->d_cp1, ctx->d_cp2, ctx->d_cp2rc,
+                   ctx->d_cpl1, ctx->d_cpl2};
+    for (void* p : old)
+        if (p) CK(hipFree(p));
+    ctx->d_cp1 = ctx->d_cp2 = ctx->d_cp2rc = nullptr;
+    ctx->d_cpl1 = ctx->d_cpl2 = nullptr;
+    CK(dalloc(&ctx->d_i1, S));
+    CK(dalloc(&ctx->d_i2, S));
+    CK(dalloc(&ctx->d_i2rc, S));
+    CK(dalloc(&ctx->d_name, S));
+    if (S) {
+        CK(hipMemcpy(ctx->d_i1, idx1_packed, S * sizeof(u64), hipMemcpyHostToDevice));
+        CK(hipMemcpy(ctx->d_i2, idx2_packed, S * sizeof(u64), hipMemcpyHostToDevice));
+        CK(hipMemcpy(ctx->d_i2rc, idx2rc_packed, S * sizeof(u64), hipMemcpyHostToDevice));
+        CK(hipMemcpy(ctx->d_name, name_id, S * sizeof(int32_t), hipMemcpyHostToDevice));
+    }
+    ctx->S = S;
+    ctx->n_names = n_names;
+    auto common = [&](const int32_t* l) {
+        if (S == 0) return -1;
+        for (int i = 1; i < S; ++i)
+            if (l[i] != l[0]) return -2;
+        return (int)l[0];
+    };
+    ctx->L1u = common(idx1_len);
+    ctx->L2u = common(idx2_len);
+    if (idx1_cp && idx2_cp && idx2rc_cp && cp_stride > 0 && S > 0) {
+        const u64 n = (u64)S * cp_stride;
+        CK(dalloc(&ctx->d_cp1, n));
+        CK(dalloc(&ctx->d_cp2, n));
+        CK(dalloc(&ctx->d_cp2rc, n));
+        CK(dalloc(&ctx->d_cpl1, S));
+        CK(dalloc(&ctx->d_cpl2, S));
+        CK(hipMemcpy(ctx->d_cp1, idx1_cp, n * 4, hipMemcpyHostToDevice));
+        CK(hipMemcpy(ctx->d_cp2, idx2_cp, n * 4, hipMemcpyHostToDevice));
+        CK(hipMemcpy(ctx->d_cp2rc, idx2rc_cp, n * 4, hipMemcpyHostToDevice));
+        CK(hipMemcpy(ctx->d_cpl1, idx1_len, S * 4, hipMemcpyHostToDevice));
+        CK(hipMemcpy(ctx->d_cpl2, idx2_len, S * 4, hipMemcpyHostToDevice));
+        ctx->cp_stride = cp_stride;
+    } else {
+        ctx->cp_stride = 0;
+    }
+    return FR_OK;
+}
+
+int fr_reset(fr_ctx* ctx) {
+    CK(hipSetDevice(ctx->device));
+    CK(hipStreamSynchronize(ctx->copy));
+    CK(launch_table_init(ctx->tab.slots, ctx->nslots, ctx->stream));
+    int rc = state_reset_counts(ctx);
+    if (rc) return rc;
+    ctx->scanning = true;
+    ctx->file_open = false;
+    ctx->file_tag = 0;
+    ctx->par = 0;
+    ctx->U = 0;
+    ctx->n_pres = 0;
+    ctx->n_exo = 0;
+    ctx->ev_used = 0;
+    ctx->scan_launches = ctx->scan_bytes = 0;
+    ctx->classify_ms = ctx->finalize_ms = 0;
+    ctx->st_pending = false;
+    return FR_OK;
+}
+
+int fr_begin_file(fr_ctx* ctx, int64_t max_records) {
+    if (ctx->file_open) return fail(ctx, FR_ERR_INVALID, "fr_begin_file: a file is already open");
+    if (ctx->file_tag + 1 >= (1u << 19)) return fail(ctx, FR_ERR_INVALID, "too many files in one scan");
+    int rc = read_state(ctx);
+    if (rc) return rc;
+    ctx->pres_before = ctx->h_st->n_presence;
+    ctx->exo_before = ctx->h_st->n_exotic;
+    // per-file device flags + line carry
+    CK(hipMemsetAsync(&ctx->st->lines[0], 0, 2 * sizeof(u64), ctx->stream));
+    CK(hipMemsetAsync(&ctx->st->err_nospace, 0xFF, sizeof(u64), ctx->stream));
+    CK(hipMemsetAsync(&ctx->st->nonascii, 0, 2 * sizeof(u32), ctx->stream));
+    ctx->file_tag++;
+    ctx->file_offset = 0;
+    ctx->max_records = max_records > 0 ? max_records : 0;
+    ctx->last_byte = -1;
+    ctx->carry.clear();
+    ctx->sample_done = false;
+    ctx->par = 0;
+    ctx->file_open = true;
+    return FR_OK;
+}
+
+static int check_sample(fr_ctx* ctx) {
+    if (ctx->max_records <= 0) return FR_OK;
+    int rc = read_state(ctx);
+    if (rc) return rc;
+    const u64 lines = ctx->h_st->lines[ctx->par];
+    if (lines + 3 >= 4ull * (u64)ctx->max_records) ctx->sample_done = true;
+    return FR_OK;
+}
+
+// launch [0, n) of ring slot `slot` (already filled in pin[slot])
+static int ship_slot(fr_ctx* ctx, int slot, u64 n) {
+    CK(hipStreamWaitEvent(ctx->copy, ctx->consumed[slot], 0));
+    CK(hipMemcpyAsync(ctx->dbuf[slot], ctx->pin[slot], n, hipMemcpyHostToDevice, ctx->copy));
+    CK(hipEventRecord(ctx->copied[slot], ctx->copy));
+    CK(hipStreamWaitEvent(ctx->stream, ctx->copied[slot], 0));
+    int rc = launch_range(ctx, ctx->dbuf[slot], n, n, 1, 0, 0);
+    if (rc) return rc;
+    CK(hipEventRecord(ctx->consumed[slot], ctx->stream));
+    ctx->used[slot] = true;
+    return FR_OK;
+}
+
+int fr_feed(fr_ctx* ctx, const uint8_t* data, uint64_t len) {
+    if (!ctx->file_open) return fail(ctx, FR_ERR_INVALID, "fr_feed: no open file");
+    if (ctx->sample_done) return FR_SAMPLE_DONE;
+    if (len) ctx->last_byte = data[len - 1];
+    u64 done = 0;
+    while (done < len) {
+        const int slot = ctx->cur;
+        if (ctx->used[slot]) CK(hipEventSynchronize(ctx->copied[slot]));  // pinned slot free again
+        u8* pin = ctx->pin[slot];
+        const u64 nc = ctx->carry.size();
+        if (nc >= ctx->chunk_bytes) return fail(ctx, FR_ERR_CAPACITY, "a line is longer than the chunk size");
+        if (nc) std::memcpy(pin, ctx->carry.data(), nc);
+        const u64 take = std::min<u64>(len - done, ctx->chunk_bytes - nc);
+        std::memcpy(pin + nc, data + done, take);
+        done += take;
+        const u64 n = nc + take;
+        // cut after the last '\n' so no header crosses a launch (R1 line phase is carried on device)
+        u64 cut = n;
+        while (cut > 0 && pin[cut - 1] != '\n') --cut;
+        if (cut == 0) {
+            ctx->carry.assign(pin, pin + n);
+            continue;
+        }
+        ctx->carry.assign(pin + cut, pin + n);
+        int rc = ship_slot(ctx, slot, cut);
+        if (rc) return rc;
+        ctx->cur ^= 1;
+        rc = check_sample(ctx);
+        if (rc) return rc;
+        if (ctx->sample_done) return FR_SAMPLE_DONE;
+    }
+    return FR_OK;
+}
+
+int fr_feed_device(fr_ctx* ctx, const uint8_t* dev_data, uint64_t len) {
+    if (!ctx->file_open) return fail(ctx, FR_ERR_INVALID, "fr_feed_device: no open file");
+    if (ctx->file_offset != 0 || !ctx->carry.empty())
+        return fail(ctx, FR_ERR_INVALID, "fr_feed_device takes a whole file (no prior fr_feed)");
+    if (((uintptr_t)dev_data & 15u) != 0) return fail(ctx, FR_ERR_INVALID, "device data must be 16-byte aligned");
+    for (u64 off = 0; off < len; off += ctx->chunk_bytes) {
+        const u64 n = std::min<u64>(ctx->chunk_bytes, len - off);
+        int rc = launch_range(ctx, dev_data + off, n, len - off, off == 0 ? 1 : 0, 1, off ? 1 : 0);
+        if (rc) return rc;
+    }
+    if (len) {
+        u8 b = 0;
+        CK(hipMemcpyAsync(&b, dev_data + len - 1, 1, hipMemcpyDeviceToHost, ctx->stream));
+        CK(hipStreamSynchronize(ctx->stream));
+        ctx->last_byte = b;
+    }
+    ctx->carry.clear();
+    return FR_OK;
+}
+
+int fr_end_file(fr_ctx* ctx, fr_file_stats* out) {
+    if (!ctx->file_open) return fail(ctx, FR_ERR_INVALID, "fr_end_file: no open file");
+    if (!ctx->carry.empty() && !ctx->sample_done) {  // the last piece: no '\n' cut needed
+        const int slot = ctx->cur;
+        if (ctx->used[slot]) CK(hipEventSynchronize(ctx->copied[slot]));
+        std::memcpy(ctx->pin[slot], ctx->carry.data(), ctx->carry.size());
+        const u64 n = ctx->carry.size();
+        ctx->carry.clear();
+        int rc = ship_slot(ctx, slot, n);
+        if (rc) return rc;
+        ctx->cur ^= 1;
+    }
+    ctx->carry.clear();
+    CK(hipStreamSynchronize(ctx->copy));
+    int rc = grow_table(ctx, false);  // re-inserts any overflow; exact state afterwards
+    if (rc) return rc;
+    rc = read_state(ctx);
+    if (rc) return rc;
+    const DevState& s = *ctx->h_st;
+    if (s.spin_fail) return fail(ctx, FR_ERR_DEVICE, "tally look-back exceeded its spin bound");
+    if (s.cap_flags) return fail(ctx, FR_ERR_CAPACITY, "a device list overflowed (flags " + std::to_string(s.cap_flags) + ")");
+    u64 lines = s.lines[ctx->par];
+    const bool ended = ctx->last_byte == '\n' || ctx->last_byte == '\r';
+    if (ctx->last_byte >= 0 && !ended && !ctx->sample_done) lines += 1;  // trailing line without terminator
+    u64 records = (lines + 3) / 4;
+    if (ctx->max_records > 0 && records > (u64)ctx->max_records) records = (u64)ctx->max_records;
+    std::memset(out, 0, sizeof(*out));
+    out->records = records;
+    out->lines = lines;
+    out->new_keys = s.n_presence - ctx->pres_before;
+    out->exotic = s.n_exotic - ctx->exo_before;
+    out->error = FR_SCAN_OK;
+    ctx->n_exo = std::min<u64>(s.n_exotic, ctx->tab.exo_cap);
+    if (s.utf8_bad) out->error = FR_SCAN_UTF8;
+    if (s.err_nospace != ~0ull) {
+        out->error = FR_SCAN_NO_SPACE;
+        out->error_offset = s.err_nospace;
+    }
+    ctx->file_open = false;
+    return FR_OK;
+}
+
+int fr_finalize(fr_ctx* ctx, uint64_t* n_unique, uint64_t* n_presence, uint64_t* n_exotic) {
+    if (ctx->file_open) return fail(ctx, FR_ERR_INVALID, "fr_finalize: a file is still open");
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    int rc = grow_table(ctx, false);
+    if (rc) return rc;
+    rc = read_state(ctx);
+    if (rc) return rc;
+    const u64 nk = ctx->h_st->n_keys;
+    if (nk > 0xFFFFFFFFull) return fail(ctx, FR_ERR_CAPACITY, "more than 2^32 unique codes");
+    if (nk > ctx->ucap) {
+        void* old[] = {ctx->d_keys, ctx->d_counts, ctx->d_first, ctx->d_keys_s, ctx->d_counts_s, ctx->d_first_s,
+                       ctx->d_pos, ctx->d_perm, ctx->d_rank, ctx->d_temp};
+        for (void* p : old)
+            if (p) CK(hipFree(p));
+        ctx->d_temp = nullptr;
+        ctx->temp_bytes = 0;
+        const u64 cap = std::max<u64>(nk + nk / 4, 1024);
+        CK(dalloc(&ctx->d_keys, cap));
+        CK(dalloc(&ctx->d_counts, cap));
+        CK(dalloc(&ctx->d_first, cap));
+        CK(dalloc(&ctx->d_keys_s, cap));
+        CK(dalloc(&ctx->d_counts_s, cap));
+        CK(dalloc(&ctx->d_first_s, cap));
+        CK(dalloc(&ctx->d_pos, cap));
+        CK(dalloc(&ctx->d_perm, cap));
+        CK(dalloc(&ctx->d_rank, cap));
+        ctx->ucap = cap;
+    }
+    CK(hipEventRecord(e0, ctx->stream));
+    CK(hipMemsetAsync(ctx->d_counter, 0, sizeof(u64), ctx->stream));
+    CK(launch_compact(ctx->tab.slots, ctx->nslots, ctx->d_keys, ctx->d_counts, ctx->d_first, ctx->d_pos,
+                      ctx->d_counter, ctx->stream));
+    size_t need = 0;
+    CK(launch_order(ctx->d_first, ctx->d_pos, nk, ctx->d_first_s, ctx->d_perm, nullptr, &need, ctx->stream));
+    if (need > ctx->temp_bytes) {
+        if (ctx->d_temp) CK(hipFree(ctx->d_temp));
+        CK(hipMalloc(&ctx->d_temp, need));
+        ctx->temp_bytes = need;
+    }
+    size_t tb = ctx->temp_bytes;
+    if (nk) CK(launch_order(ctx->d_first, ctx->d_pos, nk, ctx->d_first_s, ctx->d_perm, ctx->d_temp, &tb, ctx->stream));
+    CK(launch_gather(ctx->d_perm, nk, ctx->d_keys, ctx->d_counts, ctx->d_keys_s, ctx->d_counts_s, ctx->d_rank,
+                     ctx->stream));
+    CK(launch_set_uidx(ctx->tab.slots, ctx->tab.mask, ctx->d_keys_s, nk, ctx->d_rank, ctx->stream));
+    const u64 np = std::min<u64>(ctx->h_st->n_presence, ctx->tab.pres_cap);
+    if (np > ctx->pmap_cap) {
+        if (ctx->d_pres_u) CK(hipFree(ctx->d_pres_u));
+        if (ctx->d_pres_f) CK(hipFree(ctx->d_pres_f));
+        CK(dalloc(&ctx->d_pres_u, np));
+        CK(dalloc(&ctx->d_pres_f, np));
+        ctx->pmap_cap = np;
+    }
+    CK(launch_presence_map(ctx->tab.slots, ctx->tab.mask, ctx->tab.pres, np, ctx->d_pres_u, ctx->d_pres_f,
+                           ctx->stream));
+    CK(hipEventRecord(e1, ctx->stream));
+    u64 got = 0;
+    CK(hipMemcpyAsync(&got, ctx->d_counter, sizeof(u64), hipMemcpyDeviceToHost, ctx->stream));
+    CK(hipStreamSynchronize(ctx->stream));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    ctx->finalize_ms = ms;
+    CK(hipEventDestroy(e0));
+    CK(hipEventDestroy(e1));
+    if (got != nk) return fail(ctx, FR_ERR_DEVICE, "compaction count mismatch");
+    ctx->U = nk;
+    ctx->n_pres = np;
+    ctx->n_exo = std::min<u64>(ctx->h_st->n_exotic, ctx->tab.exo_cap);
+    if (n_unique) *n_unique = ctx->U;
+    if (n_presence) *n_presence = ctx->n_pres;
+    if (n_exotic) *n_exotic = ctx->n_exo;
+    return FR_OK;
+}
+
+int fr_get_unique(fr_ctx* ctx, uint64_t* keys, uint64_t* counts, uint64_t* first_ordinal) {
+    const u64 n = ctx->U;
+    if (!n) return FR_OK;
+    if (keys) CK(hipMemcpy(keys, ctx->d_keys_s, n * 8, hipMemcpyDeviceToHost));
+    if (counts) CK(hipMemcpy(counts, ctx->d_counts_s, n * 8, hipMemcpyDeviceToHost));
+    if (first_ordinal) CK(hipMemcpy(first_ordinal, ctx->d_first_s, n * 8, hipMemcpyDeviceToHost));
+    return FR_OK;
+}
+
+int fr_get_presence(fr_ctx* ctx, uint32_t* unique_idx, uint32_t* file_idx) {
+    const u64 n = ctx->n_pres;
+    if (!n) return FR_OK;
+    CK(hipMemcpy(unique_idx, ctx->d_pres_u, n * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(file_idx, ctx->d_pres_f, n * 4, hipMemcpyDeviceToHost));
+    return FR_OK;
+}
+
+int fr_get_exotic(fr_ctx* ctx, uint64_t* ordinal, uint32_t* length, uint64_t* pool_offset, uint8_t* pool,
+                  uint64_t pool_bytes) {
+    const u64 n = ctx->n_exo;
+    if (!n) return FR_OK;
+    CK(hipMemcpy(ordinal, ctx->tab.exo_ord, n * 8, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(length, ctx->tab.exo_len, n * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(pool_offset, ctx->tab.exo_off, n * 8, hipMemcpyDeviceToHost));
+    const u64 used = std::min<u64>(ctx->h_st->exo_pool_used, ctx->tab.exo_pool_cap);
+    if (pool && pool_bytes) CK(hipMemcpy(pool, ctx->tab.exo_pool, std::min(used, pool_bytes), hipMemcpyDeviceToHost));
+    return FR_OK;
+}
+
+static int ensure_class_scratch(fr_ctx* ctx, u64 n) {
+    if (n <= ctx->ccap && ctx->n_names <= ctx->rc_names_cap && ctx->d_errf) return FR_OK;
+    void* old[] = {ctx->d_m1, ctx->d_m2, ctx->d_row, ctx->d_rm2, ctx->d_rrow, ctx->d_cls, ctx->d_rcls, ctx->d_errw,
+                   ctx->d_errf, ctx->d_rcf, ctx->d_rcr};
+    for (void* p : old)
+        if (p) CK(hipFree(p));
+    const u64 cap = std::max<u64>(std::max(n, ctx->ccap), 1024);
+    CK(dalloc(&ctx->d_m1, cap));
+    CK(dalloc(&ctx->d_m2, cap));
+    CK(dalloc(&ctx->d_row, cap));
+    CK(dalloc(&ctx->d_rm2, cap));
+    CK(dalloc(&ctx->d_rrow, cap));
+    CK(dalloc(&ctx->d_cls, cap));
+    CK(dalloc(&ctx->d_rcls, cap));
+    CK(dalloc(&ctx->d_errw, cap));
+    CK(dalloc(&ctx->d_errf, 1));
+    const int names = std::max(ctx->n_names, 1);
+    CK(dalloc(&ctx->d_rcf, names));
+    CK(dalloc(&ctx->d_rcr, names));
+    ctx->ccap = cap;
+    ctx->rc_names_cap = names;
+    return FR_OK;
+}
+
+int fr_classify(fr_ctx* ctx, int num_subs, int rc_mode, int16_t* m1, int16_t* m2, uint8_t* cls, int16_t* row,
+                int16_t* rc_m2, uint8_t* rc_cls, int16_t* rc_row, int64_t* err_unique, int32_t* err_which) {
+    if (ctx->S < 0) return fail(ctx, FR_ERR_INVALID, "fr_classify: no sheet");
+    const u64 n = ctx->U;
+    int rc = ensure_class_scratch(ctx, n);
+    if (rc) return rc;
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    CK(hipMemsetAsync(ctx->d_errf, 0xFF, 8, ctx->stream));
+    CK(hipMemsetAsync(ctx->d_rcf, 0, std::max(ctx->n_names, 1) * 8, ctx->stream));
+    CK(hipMemsetAsync(ctx->d_rcr, 0, std::max(ctx->n_names, 1) * 8, ctx->stream));
+    SheetArgs sh{ctx->S, ctx->n_names, ctx->L1u, ctx->L2u, ctx->d_i1, ctx->d_i2, ctx->d_i2rc, ctx->d_name};
+    ClassOut o{ctx->d_m1, ctx->d_m2, ctx->d_cls, ctx->d_row, ctx->d_rm2, ctx->d_rcls, ctx->d_rrow,
+               ctx->d_rcf, ctx->d_rcr, ctx->d_errf, ctx->d_errw};
+    CK(hipEventRecord(e0, ctx->stream));
+    CK(launch_classify(ctx->d_keys_s, ctx->d_counts_s, n, sh, num_subs, rc_mode ? 1 : 0, o, ctx->stream));
+    CK(hipEventRecord(e1, ctx->stream));
+    u64 ef = ~0ull;
+    CK(hipMemcpyAsync(&ef, ctx->d_errf, 8, hipMemcpyDeviceToHost, ctx->stream));
+    CK(hipStreamSynchronize(ctx->stream));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    ctx->classify_ms = ms;
+    CK(hipEventDestroy(e0));
+    CK(hipEventDestroy(e1));
+    if (err_unique) *err_unique = ef == ~0ull ? -1 : (int64_t)ef;
+    if (err_which) {
+        *err_which = 0;
+        if (ef != ~0ull) CK(hipMemcpy(err_which, ctx->d_errw + ef, 4, hipMemcpyDeviceToHost));
+    }
+    if (n) {
+        if (m1) CK(hipMemcpy(m1, ctx->d_m1, n * 2, hipMemcpyDeviceToHost));
+        if (m2) CK(hipMemcpy(m2, ctx->d_m2, n * 2, hipMemcpyDeviceToHost));
+        if (cls) CK(hipMemcpy(cls, ctx->d_cls, n, hipMemcpyDeviceToHost));
+        if (row) CK(hipMemcpy(row, ctx->d_row, n * 2, hipMemcpyDeviceToHost));
+        if (rc_mode) {
+            if (rc_m2) CK(hipMemcpy(rc_m2, ctx->d_rm2, n * 2, hipMemcpyDeviceToHost));
+            if (rc_cls) CK(hipMemcpy(rc_cls, ctx->d_rcls, n, hipMemcpyDeviceToHost));
+            if (rc_row) CK(hipMemcpy(rc_row, ctx->d_rrow, n * 2, hipMemcpyDeviceToHost));
+        }
+    }
+    return FR_OK;
+}
+
+int fr_rc_counts(fr_ctx* ctx, uint64_t* reads_f, uint64_t* reads_rc) {
+    if (!ctx->d_rcf) return fail(ctx, FR_ERR_INVALID, "fr_rc_counts: no rc classify yet");
+    const int names = std::max(ctx->n_names, 1);
+    std::vector<u64> f(names), r(names);
+    CK(hipMemcpy(f.data(), ctx->d_rcf, names * 8, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(r.data(), ctx->d_rcr, names * 8, hipMemcpyDeviceToHost));
+    for (int i = 0; i < ctx->n_names; ++i) {
+        reads_f[i] = f[i];
+        reads_rc[i] = r[i];
+    }
+    return FR_OK;
+}
+
+int fr_classify_cp(fr_ctx* ctx, int n, const uint32_t* q1, const int32_t* q1len, const uint32_t* q2,
+                   const int32_t* q2len, int cp_stride, int num_subs, int rc_mode, int16_t* m1, int16_t* m2,
+                   uint8_t* cls, int16_t* row, int16_t* rc_m2, uint8_t* rc_cls, int16_t* rc_row,
+                   int32_t* err_which) {
+    if (n <= 0) return FR_OK;
+    if (ctx->S > 0 && (!ctx->d_cp1 || cp_stride != ctx->cp_stride))
+        return fail(ctx, FR_ERR_INVALID, "fr_classify_cp: sheet code points missing or stride mismatch");
+    u32 *dq1, *dq2;
+    int32_t *dl1, *dl2;
+    int16_t *o_m1, *o_m2, *o_row, *o_rm2, *o_rrow;
+    u8 *o_cls, *o_rcls;
+    int32_t* o_err;
+    const u64 qn = (u64)n * cp_stride;
+    CK(dalloc(&dq1, qn));
+    CK(dalloc(&dq2, qn));
+    CK(dalloc(&dl1, n));
+    CK(dalloc(&dl2, n));
+    CK(dalloc(&o_m1, n));
+    CK(dalloc(&o_m2, n));
+    CK(dalloc(&o_row, n));
+    CK(dalloc(&o_rm2, n));
+    CK(dalloc(&o_rrow, n));
+    CK(dalloc(&o_cls, n));
+    CK(dalloc(&o_rcls, n));
+    CK(dalloc(&o_err, n));
+    CK(hipMemcpy(dq1, q1, qn * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dq2, q2, qn * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dl1, q1len, n * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dl2, q2len, n * 4, hipMemcpyHostToDevice));
+    ClassOut o{o_m1, o_m2, o_cls, o_row, o_rm2, o_rcls, o_rrow, nullptr, nullptr, nullptr, o_err};
+    CK(launch_classify_cp(n, dq1, dl1, dq2, dl2, cp_stride, ctx->S > 0 ? ctx->S : 0, ctx->d_cp1, ctx->d_cpl1,
+                          ctx->d_cp2, ctx->d_cpl2, ctx->d_cp2rc, ctx->d_name, num_subs, rc_mode ? 1 : 0, o,
+                          ctx->stream));
+    CK(hipStreamSynchronize(ctx->stream));
+    CK(hipMemcpy(m1, o_m1, n * 2, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(m2, o_m2, n * 2, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(cls, o_cls, n, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(row, o_row, n * 2, hipMemcpyDeviceToHost));
+    if (err_which) CK(hipMemcpy(err_which, o_err, n * 4, hipMemcpyDeviceToHost));
+    if (rc_mode) {
+        CK(hipMemcpy(rc_m2, o_rm2, n * 2, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(rc_cls, o_rcls, n, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(rc_row, o_rrow, n * 2, hipMemcpyDeviceToHost));
+    }
+    void* tmp[] = {dq1, dq2, dl1, dl2, o_m1, o_m2, o_row, o_rm2, o_rrow, o_cls, o_rcls, o_err};
+    for (void* p : tmp) CK(hipFree(p));
+    return FR_OK;
+}
+
+int fr_export_unique_device(fr_ctx* ctx, void* dev_keys, void* dev_counts, void* dev_first, uint64_t cap) {
+    if (ctx->U > cap) return fail(ctx, FR_ERR_CAPACITY, "export buffer too small");
+    if (ctx->U) {
+        CK(hipMemcpyAsync(dev_keys, ctx->d_keys_s, ctx->U * 8, hipMemcpyDeviceToDevice, ctx->stream));
+        CK(hipMemcpyAsync(dev_counts, ctx->d_counts_s, ctx->U * 8, hipMemcpyDeviceToDevice, ctx->stream));
+        CK(hipMemcpyAsync(dev_first, ctx->d_first_s, ctx->U * 8, hipMemcpyDeviceToDevice, ctx->stream));
+    }
+    CK(hipStreamSynchronize(ctx->stream));
+    return FR_OK;
+}
+
+int fr_merge_unique_device(fr_ctx* ctx, const void* dev_keys, const void* dev_counts, const void* dev_first,
+                           uint64_t n) {
+    if (ctx->file_open) return fail(ctx, FR_ERR_INVALID, "fr_merge_unique_device: a file is open");
+    int rc = read_state(ctx);
+    if (rc) return rc;
+    if ((ctx->h_st->n_keys + n) * 2 > ctx->nslots) {
+        rc = grow_table(ctx, true);
+        if (rc) return rc;
+    }
+    CK(launch_merge(ctx->tab, ctx->st, (const u64*)dev_keys, (const u64*)dev_counts, (const u64*)dev_first, n,
+                    ctx->stream));
+    return grow_table(ctx, false);
+}
+
+void* fr_device_alloc(fr_ctx* ctx, uint64_t bytes) {
+    void* p = nullptr;
+    if (hipSetDevice(ctx->device) != hipSuccess || hipMalloc(&p, std::max<u64>(bytes, 1)) != hipSuccess) {
+        ctx->err = "fr_device_alloc failed";
+        return nullptr;
+    }
+    return p;
+}
+
+int fr_device_free(fr_ctx* ctx, void* ptr) {
+    CK(hipFree(ptr));
+    return FR_OK;
+}
+
+int fr_copy_to_host(fr_ctx* ctx, void* dst, const void* dev_src, uint64_t bytes) {
+    CK(hipStreamSynchronize(ctx->stream));
+    CK(hipMemcpy(dst, dev_src, bytes, hipMemcpyDeviceToHost));
+    return FR_OK;
+}
+
+int fr_copy_to_device(fr_ctx* ctx, void* dev_dst, const void* src, uint64_t bytes) {
+    CK(hipStreamSynchronize(ctx->stream));
+    CK(hipMemcpy(dev_dst, src, bytes, hipMemcpyHostToDevice));
+    return FR_OK;
+}
+
+int fr_synth_device(fr_ctx* ctx, uint8_t* dev_out, uint64_t r0, uint64_t n, int R, uint64_t seed,
+                    const char* idx1_ascii, const char* idx2_ascii, int S, int L1, int L2) {
+    if (S <= 0 || L1 <= 0 || L2 <= 0 || L1 + L2 > 32 || R < 0 || R > 256)
+        return fail(ctx, FR_ERR_INVALID, "fr_synth_device: bad shape");
+    u8 *d1, *d2;
+    CK(dalloc(&d1, (u64)S * L1));
+    CK(dalloc(&d2, (u64)S * L2));
+    CK(hipMemcpy(d1, idx1_ascii, (u64)S * L1, hipMemcpyHostToDevice));
+    CK(hipMemcpy(d2, idx2_ascii, (u64)S * L2, hipMemcpyHostToDevice));
+    CK(launch_synth(dev_out, r0, n, R, seed, d1, d2, S, L1, L2, ctx->stream));
+    CK(hipStreamSynchronize(ctx->stream));
+    CK(hipFree(d1));
+    CK(hipFree(d2));
+    return FR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,161 @@
+// fr_internal.h — device data layout shared by the kernels (fr_kernels.hip) and the
+// C-ABI context (fr_api.hip).  See DESIGN.md §3 for the HBM layout.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace fr {
+
+typedef uint8_t u8;
+typedef uint16_t u16;
+typedef uint32_t u32;
+typedef uint64_t u64;
+typedef int64_t i64;
+
+// ---- tally kernel geometry --------------------------------------------------------
+constexpr int WG = 256;              // 4 waves of 64
+constexpr int TILE = 16384;          // bytes per tile (one look-back unit)
+constexpr int SEG = TILE / WG;       // 64 contiguous bytes per thread
+constexpr int HALO = 512;            // bytes loaded past the tile for headers that cross it
+constexpr int LOG_NS = 11;
+constexpr int NS = 1 << LOG_NS;      // LDS hash slots per workgroup
+constexpr int LPROBE = 32;           // LDS probe bound before going to HBM directly
+constexpr int GPROBE = 256;          // HBM probe bound before the overflow list
+constexpr int MAXSYM = 21;           // fast key: <= 21 symbols of 3 bits
+constexpr u64 RANGE_MAX = 1ull << 30;  // bytes per tally launch (device feeds)
+constexpr u32 SPIN_MAX = 1u << 24;   // look-back spin bound (then FR_ERR_DEVICE)
+constexpr int ORD_SHIFT = 44;        // ordinal = file_tag << 44 | file byte offset
+
+// ---- HBM structures ---------------------------------------------------------------
+struct alignas(32) GSlot {           // open-addressing slot, one 32-B sector
+    u64 key;                         // 0 = empty
+    u64 count;
+    u64 first;                       // min ordinal, ~0 = none
+    u32 last_tag;                    // last file tag that inserted (presence detection)
+    u32 uidx;                        // compact index (set by fr_finalize)
+};
+
+struct alignas(16) Presence {
+    u64 key;
+    u32 tag;
+    u32 pad;
+};
+
+struct alignas(32) Overflow {
+    u64 key, count, first;
+    u32 tag, pad;
+};
+
+struct DevState {
+    u64 lines[2];        // terminators before the current range (launch parity)
+    u32 ticket;          // tile ticket, zeroed before every launch
+    u32 spin_fail;
+    u64 n_keys;
+    u64 n_overflow;
+    u64 n_presence;
+    u64 n_exotic;
+    u64 exo_pool_used;
+    u64 err_nospace;     // min file offset of a header without ' ' (~0 = none)
+    u32 nonascii;        // a byte >= 0x80 was seen in the current file
+    u32 utf8_bad;
+    u32 cap_flags;       // 1 presence, 2 overflow list, 4 exotic pool
+    u32 pad;
+};
+
+struct Table {
+    GSlot* slots;
+    u64 mask;
+    Overflow* ovf;
+    u64 ovf_cap;
+    Presence* pres;
+    u64 pres_cap;
+    u64* exo_ord;
+    u64* exo_off;
+    u32* exo_len;
+    u64 exo_cap;
+    u8* exo_pool;
+    u64 exo_pool_cap;
+};
+
+struct ScanArgs {
+    const u8* buf;       // range base (16-B aligned); bytes [0, len) are scanned
+    u64 len;
+    u64 avail;           // readable bytes from buf (headers may extend up to here)
+    u64 file_offset;     // file offset of buf[0]
+    u32 file_tag;        // file index + 1
+    u32 par;             // launch parity: read lines[par], write lines[par ^ 1]
+    u32 epoch;           // look-back tag of this launch (>= 1)
+    u32 num_tiles;
+    int own_start;       // position 0 is a line start handled by this launch
+    int own_end;         // a line start at position len is handled by this launch
+    int pre_valid;       // buf[-16..-1] readable (device-split ranges)
+    int pad;
+    i64 max_records;     // -s, <= 0: none
+    DevState* st;
+    u64* tiles;          // look-back descriptors
+    Table tab;
+};
+
+struct SheetArgs {
+    int S;
+    int n_names;
+    int L1u;             // common case-folded idx1 length, -1 empty sheet, -2 mixed
+    int L2u;
+    const u64* i1;
+    const u64* i2;
+    const u64* i2rc;
+    const int32_t* name;
+};
+
+struct ClassOut {
+    int16_t* m1;
+    int16_t* m2;
+    u8* cls;
+    int16_t* row;
+    int16_t* rc_m2;
+    u8* rc_cls;
+    int16_t* rc_row;
+    u64* rc_f;           // per name
+    u64* rc_r;
+    u64* err_first;      // min unique index with an error (~0 none)
+    int32_t* err_which;  // per unique (optional): 1 idx1 len, 2 idx2 len, 3 no '+'
+};
+
+enum { CLS_UNDET = 0, CLS_HOP = 1, CLS_DEMUX = 2, CLS_AMBIG = 3 };
+
+__host__ __device__ inline u64 mix64(u64 x) {
+    x ^= x >> 30;
+    x *= 0xBF58476D1CE4E5B9ull;
+    x ^= x >> 27;
+    x *= 0x94D049BB133111EBull;
+    x ^= x >> 31;
+    return x;
+}
+
+// ---- launchers (fr_kernels.hip) --------------------------------------------------
+hipError_t launch_table_init(GSlot* slots, u64 n, hipStream_t s);
+hipError_t launch_scan(const ScanArgs& a, int grid, hipStream_t s);
+hipError_t launch_reinsert_overflow(Table t, DevState* st, const Overflow* src, u64 n, hipStream_t s);
+hipError_t launch_rehash(Table dst, DevState* st, const GSlot* src, u64 nsrc, hipStream_t s);
+hipError_t launch_compact(const GSlot* slots, u64 nslots, u64* keys, u64* counts, u64* first, u32* pos,
+                          u64* counter, hipStream_t s);
+hipError_t launch_set_uidx(GSlot* slots, u64 mask, const u64* keys, u64 n, const u32* rank_of_pos,
+                           hipStream_t s);
+hipError_t launch_order(const u64* first_in, const u32* pos_in, u64 n, u64* first_out, u32* perm_out,
+                        void* temp, size_t* temp_bytes, hipStream_t s);
+hipError_t launch_gather(const u32* perm, u64 n, const u64* keys, const u64* counts, u64* keys_o,
+                         u64* counts_o, u32* rank, hipStream_t s);
+hipError_t launch_presence_map(const GSlot* slots, u64 mask, const Presence* pres, u64 n, u32* uidx,
+                               u32* file_idx, hipStream_t s);
+hipError_t launch_classify(const u64* keys, const u64* counts, u64 n, SheetArgs sh, int nsubs, int rc,
+                           ClassOut o, hipStream_t s);
+hipError_t launch_classify_cp(int n, const u32* q1, const int32_t* q1len, const u32* q2, const int32_t* q2len,
+                              int stride, int S, const u32* s1, const int32_t* s1len, const u32* s2,
+                              const int32_t* s2len, const u32* s2rc, const int32_t* name, int nsubs, int rc,
+                              ClassOut o, hipStream_t s);
+hipError_t launch_merge(Table t, DevState* st, const u64* keys, const u64* counts, const u64* first, u64 n,
+                        hipStream_t s);
+hipError_t launch_synth(u8* out, u64 r0, u64 n, int R, u64 seed, const u8* idx1, const u8* idx2, int S, int L1,
+                        int L2, hipStream_t s);
+
+}  // namespace fr

@@ -1,0 +1,919 @@
+// fr_kernels.hip — gfx950 kernels for frender's scan hot path.
+//
+//  tally (scan_kernel)  : frender.py:154-181 scan_file + :199-205 merge, one pass over the
+//                         decoded FASTQ bytes in HBM (R1-R4 of SURVEY.md §8.0)
+//  classify             : frender.py:214-234 (Hamming), :237-291 (classes), :294-351 (rc)
+//  table / order        : the first-occurrence-ordered merged table of :199-203
+//  synth                : SYN-v1 records (frender_amd/synth.py), device side
+//
+// Design notes: the tally is HBM-bound byte work.  A workgroup owns a
+// 16 KiB tile at a time (dynamic ticket), stages it in LDS with 16-B loads, computes
+// the line-terminator bitmap with SWAR compares, gets the tile's line prefix by a
+// decoupled look-back over 8-B {tag,value} granules (agent-scope relaxed atomics, no
+// fences: MI355X guide Guideline 16 R2), finds every 4th line, parses each header from
+// LDS (lane per header), packs the code 3 bits/char and counts it in an LDS-private
+// open-addressing table that is flushed to the HBM table with 64-bit atomics.
+#include <algorithm>
+#include <cstring>
+
+#include <rocprim/rocprim.hpp>
+
+#include "fr_internal.h"
+
+namespace fr {
+
+// ------------------------------------------------------------------------------------
+// small helpers
+// ------------------------------------------------------------------------------------
+
+// exact per-byte equality of w against the byte replicated in c -> 4-bit mask (byte i -> bit i)
+__device__ __forceinline__ u32 eq4(u32 w, u32 c) {
+    const u32 t = w ^ c;
+    const u32 z = ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;
+    return (((z >> 7) * 0x00204081u) >> 21) & 0xFu;
+}
+
+__device__ __forceinline__ u32 hi4(u32 w) {  // bytes >= 0x80
+    return ((((w & 0x80808080u) >> 7) * 0x00204081u) >> 21) & 0xFu;
+}
+
+// byte -> fast-key symbol (A1 C2 G3 T4 N5 +6), 0 if outside the fast alphabet
+__device__ __forceinline__ u32 sym_of(u32 c) {
+    const u32 i = (c >> 1) & 7u;
+    const u64 expect = 0x4E002B0047544341ull;  // idx: 0 A,1 C,2 T,3 G,4 -,5 +,6 -,7 N
+    const u32 symtab = 0x50603421u;
+    const bool ok = ((expect >> (8 * i)) & 0xFFu) == c;
+    return ok ? ((symtab >> (4 * i)) & 0xFu) : 0u;
+}
+
+__device__ __forceinline__ u64 agent_load(const u64* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void agent_store(u64* p, u64 v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ u64 wave_sum_u64(u64 v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+
+// ------------------------------------------------------------------------------------
+// HBM table insert (count add, first-occurrence min, per-file presence)
+// ------------------------------------------------------------------------------------
+__device__ void global_insert(const Table& T, DevState* st, u64 key, u64 cnt, u64 ord, u32 tag) {
+    u64 h = mix64(key) & T.mask;
+    for (int probe = 0; probe < GPROBE; ++probe) {
+        GSlot* s = &T.slots[h];
+        u64 k = agent_load(&s->key);
+        if (k == 0) {
+            const u64 old = atomicCAS((unsigned long long*)&s->key, 0ull, (unsigned long long)key);
+            if (old == 0) {
+                atomicAdd((unsigned long long*)&st->n_keys, 1ull);
+                k = key;
+            } else {
+                k = old;
+            }
+        }
+        if (k == key) {
+            atomicAdd((unsigned long long*)&s->count, (unsigned long long)cnt);
+            atomicMin((unsigned long long*)&s->first, (unsigned long long)ord);
+            const u32 prev = atomicMax(&s->last_tag, tag);
+            if (prev < tag) {
+                const u64 i = atomicAdd((unsigned long long*)&st->n_presence, 1ull);
+                if (i < T.pres_cap) {
+                    T.pres[i].key = key;
+                    T.pres[i].tag = tag;
+                } else {
+                    atomicOr(&st->cap_flags, 1u);
+                }
+            }
+            return;
+        }
+        h = (h + 1) & T.mask;
+    }
+    const u64 i = atomicAdd((unsigned long long*)&st->n_overflow, 1ull);
+    if (i < T.ovf_cap) {
+        Overflow o;
+        o.key = key;
+        o.count = cnt;
+        o.first = ord;
+        o.tag = tag;
+        o.pad = 0;
+        T.ovf[i] = o;
+    } else {
+        atomicOr(&st->cap_flags, 2u);
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// the tally kernel
+// ------------------------------------------------------------------------------------
+struct ScanShared {
+    u8 buf[16 + TILE + HALO];        // [0,16) = the 16 bytes before the tile (UTF-8 look-back)
+    u16 hdr[TILE / 4 + 4];
+    u64 key[NS];
+    u32 cnt[NS];
+    u32 mino[NS];
+    u32 wsum[WG / 64];
+    u64 tile_excl;
+    u32 tile;
+    u32 nhdr;
+    u32 nkeys;
+    u32 flags;
+};
+
+__device__ __forceinline__ u64 make_ord(const ScanArgs& a, u64 off_in_range) {
+    return ((u64)a.file_tag << ORD_SHIFT) | (a.file_offset + off_in_range);
+}
+
+__device__ void lds_flush(ScanShared& sh, const ScanArgs& a) {
+    for (int i = threadIdx.x; i < NS; i += WG) {
+        const u64 k = sh.key[i];
+        if (k) {
+            global_insert(a.tab, a.st, k, sh.cnt[i], make_ord(a, sh.mino[i]), a.file_tag);
+            sh.key[i] = 0;
+            sh.cnt[i] = 0;
+            sh.mino[i] = 0xFFFFFFFFu;
+        }
+    }
+}
+
+__device__ __forceinline__ void lds_insert(ScanShared& sh, const ScanArgs& a, u64 key, u32 off) {
+    u32 h = (u32)((key * 0x9E3779B97F4A7C15ull) >> (64 - LOG_NS));
+    for (int pr = 0; pr < LPROBE; ++pr) {
+        u64 k = *(volatile u64*)&sh.key[h];
+        if (k == 0) {
+            const u64 old = atomicCAS((unsigned long long*)&sh.key[h], 0ull, (unsigned long long)key);
+            if (old == 0) {
+                atomicAdd(&sh.nkeys, 1u);
+                k = key;
+            } else {
+                k = old;
+            }
+        }
+        if (k == key) {
+            atomicAdd(&sh.cnt[h], 1u);
+            atomicMin(&sh.mino[h], off);
+            return;
+        }
+        h = (h + 1) & (NS - 1);
+    }
+    global_insert(a.tab, a.st, key, 1, make_ord(a, off), a.file_tag);
+}
+
+// Decoupled look-back over the launch's tile descriptors: returns the number of line
+// terminators in tiles [0, t) of this range.  Descriptor = {tag = 2*epoch + inclusive, value}.
+__device__ u64 lookback(const ScanArgs& a, u32 t, u32 agg, int lane) {
+    const u64 tagA = (u64)(2u * a.epoch) << 32;
+    const u64 tagI = (u64)(2u * a.epoch + 1u) << 32;
+    if (t == 0) {
+        if (lane == 0) agent_store(&a.tiles[0], tagI | agg);
+        return 0;
+    }
+    if (lane == 0) agent_store(&a.tiles[t], tagA | agg);
+    u64 excl = 0;
+    i64 j = (i64)t - 1;
+    u32 spins = 0;
+    for (;;) {
+        const i64 idx = j - lane;
+        const u64 s = idx >= 0 ? agent_load(&a.tiles[idx]) : tagI;
+        const u32 tag = (u32)(s >> 32);
+        const bool ready = (tag >> 1) == a.epoch;
+        if (!__all(ready)) {
+            if (++spins > SPIN_MAX) {
+                if (lane == 0) atomicOr(&a.st->spin_fail, 1u);
+                return 0;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        const u64 inc = __ballot(tag & 1u);
+        const u32 v = (u32)s;
+        if (inc) {
+            const int first = __ffsll((long long)inc) - 1;
+            excl += wave_sum_u64(lane <= first ? (u64)v : 0ull);
+            break;
+        }
+        excl += wave_sum_u64((u64)v);
+        j -= 64;
+    }
+    if (lane == 0) agent_store(&a.tiles[t], tagI | (u64)(u32)(excl + agg));
+    return excl;
+}
+
+// validate UTF-8 for the bytes [s0, s0+n) of the tile (only called when a byte >= 0x80
+// is present).  Byte at tile position q is sh.buf[16 + q]; positions < 0 are the 16 bytes
+// before the tile (zero when not readable), positions >= nb are past the readable end.
+__device__ bool utf8_segment_ok(const ScanShared& sh, int s0, int n, int nb) {
+    auto byte_at = [&](int q) -> int { return (q < nb && q >= -16) ? (int)sh.buf[16 + q] : -1; };
+    for (int q = s0; q < s0 + n; ++q) {
+        const int b = byte_at(q);
+        if (b < 0x80) continue;
+        if (b >= 0x80 && b <= 0xBF) {  // continuation: must be claimed by a lead
+            bool claimed = false;
+            for (int j = 1; j <= 3; ++j) {
+                const int c = byte_at(q - j);
+                if (c < 0) break;
+                if (c >= 0x80 && c <= 0xBF) continue;
+                const int need = c >= 0xF0 ? 4 : c >= 0xE0 ? 3 : c >= 0xC0 ? 2 : 1;
+                claimed = need > j;
+                break;
+            }
+            if (!claimed) return false;
+            continue;
+        }
+        int need;
+        if (b >= 0xC2 && b <= 0xDF) need = 2;
+        else if (b >= 0xE0 && b <= 0xEF) need = 3;
+        else if (b >= 0xF0 && b <= 0xF4) need = 4;
+        else return false;
+        for (int j = 1; j < need; ++j) {
+            const int c = byte_at(q + j);
+            if (c < 0x80 || c > 0xBF) return false;
+            if (j == 1) {
+                if (b == 0xE0 && c < 0xA0) return false;
+                if (b == 0xED && c > 0x9F) return false;
+                if (b == 0xF0 && c < 0x90) return false;
+                if (b == 0xF4 && c > 0x8F) return false;
+            }
+        }
+    }
+    return true;
+}
+
+__device__ void process_header(ScanShared& sh, const ScanArgs& a, u64 tile0, u32 p, u32 nb) {
+    const u64 eof = a.avail - tile0;  // tile positions >= eof are past the end of the data
+    auto rd = [&](u64 q) -> u32 { return q < nb ? (u32)sh.buf[16 + q] : (u32)a.buf[tile0 + q]; };
+    u64 q = p;
+    // R2: the token after the first ' ' (frender.py:169 split(" ")[1]) ...
+    for (;;) {
+        if (q >= eof) goto nospace;
+        const u32 c = rd(q);
+        if (c == ' ') break;
+        if (c == '\n' || c == '\r') goto nospace;
+        ++q;
+    }
+    {
+        const u64 sp1 = q;
+        ++q;
+        i64 lc = -1;
+        for (;;) {
+            if (q >= eof) break;
+            const u32 c = rd(q);
+            if (c == ' ' || c == '\n' || c == '\r') break;
+            if (c == ':') lc = (i64)q;
+            ++q;
+        }
+        // ... and its suffix after the last ':' (.split(":")[-1])
+        const u64 start = (lc >= 0 ? (u64)lc : sp1) + 1;
+        const u64 n = q - start;
+        u64 key = 0;
+        bool fast = n >= 1 && n <= (u64)MAXSYM;
+        for (u64 i = 0; fast && i < n; ++i) {
+            const u32 s = sym_of(rd(start + i));
+            fast = s != 0;
+            key |= (u64)s << (3 * i);
+        }
+        if (fast) {
+            lds_insert(sh, a, key, (u32)(tile0 + p));
+        } else {  // exotic code: raw bytes to the exotic pool, merged by the host
+            const u64 i = atomicAdd((unsigned long long*)&a.st->n_exotic, 1ull);
+            const u64 po = atomicAdd((unsigned long long*)&a.st->exo_pool_used, (unsigned long long)n);
+            if (i < a.tab.exo_cap && po + n <= a.tab.exo_pool_cap) {
+                a.tab.exo_ord[i] = make_ord(a, tile0 + p);
+                a.tab.exo_off[i] = po;
+                a.tab.exo_len[i] = (u32)n;
+                for (u64 k = 0; k < n; ++k) a.tab.exo_pool[po + k] = (u8)rd(start + k);
+            } else {
+                atomicOr(&a.st->cap_flags, 4u);
+            }
+        }
+        return;
+    }
+nospace:  // IndexError: list index out of range (frender.py:169)
+    atomicMin((unsigned long long*)&a.st->err_nospace, (unsigned long long)(a.file_offset + tile0 + p));
+}
+
+__global__ __launch_bounds__(WG) void scan_kernel(ScanArgs a) {
+    __shared__ ScanShared sh;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wid = tid >> 6;
+    for (int i = tid; i < NS; i += WG) {
+        sh.key[i] = 0;
+        sh.cnt[i] = 0;
+        sh.mino[i] = 0xFFFFFFFFu;
+    }
+    if (tid == 0) {
+        sh.nkeys = 0;
+        sh.flags = 0;
+    }
+    const u64 base_lines = a.st->lines[a.par];
+    __syncthreads();
+
+    for (;;) {
+        if (tid == 0) {
+            sh.tile = atomicAdd(&a.st->ticket, 1u);
+            sh.nhdr = 0;
+        }
+        __syncthreads();
+        const u32 t = sh.tile;
+        if (t >= a.num_tiles) break;
+        const u64 tile0 = (u64)t * TILE;
+        const u32 tlen = (u32)min((u64)TILE, a.len - tile0);
+        const u32 nb = (u32)min((u64)(TILE + HALO), a.avail - tile0);
+
+        // ---- stage the tile (+halo) in LDS with 16-B loads --------------------------
+        for (u32 off = tid * 16; off < (u32)(TILE + HALO); off += WG * 16) {
+            uint4 v = make_uint4(0u, 0u, 0u, 0u);
+            if (off + 16 <= nb) {
+                v = *(const uint4*)(a.buf + tile0 + off);
+            } else if (off < nb) {
+                u32 w[4] = {0u, 0u, 0u, 0u};
+                for (u32 j = 0; off + j < nb; ++j) w[j >> 2] |= (u32)a.buf[tile0 + off + j] << (8 * (j & 3));
+                v = make_uint4(w[0], w[1], w[2], w[3]);
+            }
+            *(uint4*)(sh.buf + 16 + off) = v;
+        }
+        if (tid == 0) {  // the 16 bytes before the tile (only for UTF-8 continuation checks)
+            uint4 v = make_uint4(0u, 0u, 0u, 0u);
+            if (tile0 >= 16 || a.pre_valid) v = *(const uint4*)(a.buf + tile0 - 16);
+            *(uint4*)(sh.buf) = v;
+        }
+        __syncthreads();
+
+        // ---- line-terminator bitmap of this thread's 64 bytes -----------------------
+        const u32 s0 = tid * SEG;
+        u64 tmask = 0;
+        if (s0 < tlen) {
+            u64 nl = 0, cr = 0, hi = 0;
+#pragma unroll
+            for (int qv = 0; qv < SEG / 16; ++qv) {
+                const uint4 v = *(const uint4*)(sh.buf + 16 + s0 + qv * 16);
+                const u32 w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int sh4 = qv * 16 + k * 4;
+                    nl |= (u64)eq4(w[k], 0x0A0A0A0Au) << sh4;
+                    cr |= (u64)eq4(w[k], 0x0D0D0D0Du) << sh4;
+                    hi |= (u64)hi4(w[k]) << sh4;
+                }
+            }
+            const u64 nxt = (s0 + SEG < nb && sh.buf[16 + s0 + SEG] == '\n') ? 1ull : 0ull;
+            // '\r' ends a line unless a '\n' follows (then the '\n' ends it): universal newlines
+            tmask = nl | (cr & ~((nl >> 1) | (nxt << 63)));
+            const u32 valid = tlen - s0;
+            if (valid < SEG) {
+                const u64 vm = (1ull << valid) - 1ull;
+                tmask &= vm;
+                hi &= vm;
+            }
+            if (hi) {
+                atomicOr(&sh.flags, 1u);
+                if (!utf8_segment_ok(sh, (int)s0, (int)min(valid, (u32)SEG), (int)nb)) atomicOr(&sh.flags, 2u);
+            }
+        }
+
+        // ---- block scan of terminator counts + decoupled look-back ------------------
+        const u32 c = __popcll(tmask);
+        u32 x = c;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const u32 y = __shfl_up(x, d, 64);
+            if (lane >= d) x += y;
+        }
+        if (lane == 63) sh.wsum[wid] = x;
+        __syncthreads();
+        u32 wexcl = 0, tot = 0;
+#pragma unroll
+        for (int w = 0; w < WG / 64; ++w) {
+            const u32 v = sh.wsum[w];
+            wexcl += w < wid ? v : 0u;
+            tot += v;
+        }
+        if (wid == 0) {
+            const u64 ex = lookback(a, t, tot, lane);
+            if (lane == 0) {
+                sh.tile_excl = ex;
+                if (t == a.num_tiles - 1) a.st->lines[a.par ^ 1u] = base_lines + ex + tot;
+            }
+        }
+        __syncthreads();
+
+        // ---- every 4th line is a header (R1); collect their starts -------------------
+        u64 L = base_lines + sh.tile_excl + wexcl + (x - c);
+        u64 m = tmask;
+        while (m) {
+            const int j = __ffsll((long long)m) - 1;
+            m &= m - 1;
+            L += 1;  // index of the line that starts after this terminator
+            if ((L & 3ull) == 0) {
+                const u32 p = s0 + (u32)j + 1u;
+                const u64 gp = tile0 + p;
+                const bool mine = gp < a.len || (a.own_end && gp == a.len && gp < a.avail);
+                if (mine && (a.max_records <= 0 || (i64)(L >> 2) < a.max_records)) {
+                    const u32 slot = atomicAdd(&sh.nhdr, 1u);
+                    sh.hdr[slot] = (u16)p;
+                }
+            }
+        }
+        if (t == 0 && tid == 0 && a.own_start && (base_lines & 3ull) == 0 && a.avail > 0 &&
+            (a.max_records <= 0 || (i64)(base_lines >> 2) < a.max_records)) {
+            const u32 slot = atomicAdd(&sh.nhdr, 1u);
+            sh.hdr[slot] = 0;
+        }
+        __syncthreads();
+
+        // ---- parse headers (lane per header) and count their codes ------------------
+        const u32 nh = sh.nhdr;
+        for (u32 h = tid; h < nh; h += WG) process_header(sh, a, tile0, sh.hdr[h], nb);
+        __syncthreads();
+        if (sh.nkeys > (u32)(NS * 3 / 4)) {
+            lds_flush(sh, a);
+            __syncthreads();
+            if (tid == 0) sh.nkeys = 0;
+        }
+    }
+    __syncthreads();
+    lds_flush(sh, a);
+    if (tid == 0) {
+        if (sh.flags & 1u) atomicOr(&a.st->nonascii, 1u);
+        if (sh.flags & 2u) atomicOr(&a.st->utf8_bad, 1u);
+    }
+}
+
+hipError_t launch_scan(const ScanArgs& a, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(scan_kernel, dim3(grid), dim3(WG), 0, s, a);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------
+// table maintenance
+// ------------------------------------------------------------------------------------
+__global__ void table_init_kernel(GSlot* slots, u64 n) {
+    for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
+        GSlot g;
+        g.key = 0;
+        g.count = 0;
+        g.first = ~0ull;
+        g.last_tag = 0;
+        g.uidx = 0;
+        slots[i] = g;
+    }
+}
+
+hipError_t launch_table_init(GSlot* slots, u64 n, hipStream_t s) {
+    const int grid = (int)std::min<u64>((n + 255) / 256, 8192);
+    hipLaunchKernelGGL(table_init_kernel, dim3(grid > 0 ? grid : 1), dim3(256), 0, s, slots, n);
+    return hipGetLastError();
+}
+
+// re-insert overflow entries (after the table has grown); presence is re-derived
+__global__ void reinsert_kernel(Table t, DevState* st, const Overflow* src, u64 n) {
+    for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
+        const Overflow o = src[i];
+        global_insert(t, st, o.key, o.count, o.first, o.tag);
+    }
+}
+
+hipError_t launch_reinsert_overflow(Table t, DevState* st, const Overflow* src, u64 n, hipStream_t s) {
+    if (!n) return hipSuccess;
+    const int grid = (int)std::min<u64>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(reinsert_kernel, dim3(grid), dim3(256), 0, s, t, st, src, n);
+    return hipGetLastError();
+}
+
+// move every live slot of an old table into a bigger one (keeps count/first/last_tag)
+__global__ void rehash_kernel(Table t, const GSlot* src, u64 nsrc) {
+    for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i < nsrc; i += (u64)gridDim.x * blockDim.x) {
+        const GSlot g = src[i];
+        if (!g.key) continue;
+        u64 h = mix64(g.key) & t.mask;
+        for (;;) {
+            const u64 old = atomicCAS((unsigned long long*)&t.slots[h].key, 0ull, (unsigned long long)g.key);
+            if (old == 0) {
+                t.slots[h].count = g.count;
+                t.slots[h].first = g.first;
+                t.slots[h].last_tag = g.last_tag;
+                break;
+            }
+            h = (h + 1) & t.mask;
+        }
+    }
+}
+
+hipError_t launch_rehash(Table dst, DevState* st, const GSlot* src, u64 nsrc, hipStream_t s) {
+    (void)st;
+    const int grid = (int)std::min<u64>((nsrc + 255) / 256, 8192);
+    hipLaunchKernelGGL(rehash_kernel, dim3(grid), dim3(256), 0, s, dst, src, nsrc);
+    return hipGetLastError();
+}
+
+__global__ void compact_kernel(const GSlot* slots, u64 nslots, u64* keys, u64* counts, u64* first, u32* pos,
+                               u64* counter) {
+    for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i < nslots; i += (u64)gridDim.x * blockDim.x) {
+        const GSlot g = slots[i];
+        if (!g.key) continue;
+        const u64 p = atomicAdd((unsigned long long*)counter, 1ull);
+        keys[p] = g.key;
+        counts[p] = g.count;
+        first[p] = g.first;
+        pos[p] = (u32)p;
+    }
+}
+
+hipError_t launch_compact(const GSlot* slots, u64 nslots, u64* keys, u64* counts, u64* first, u32* pos,
+                          u64* counter, hipStream_t s) {
+    const int grid = (int)std::min<u64>((nslots + 255) / 256, 8192);
+    hipLaunchKernelGGL(compact_kernel, dim3(grid), dim3(256), 0, s, slots, nslots, keys, counts, first, pos,
+                       counter);
+    return hipGetLastError();
+}
+
+hipError_t launch_order(const u64* first_in, const u32* pos_in, u64 n, u64* first_out, u32* perm_out, void* temp,
+                        size_t* temp_bytes, hipStream_t s) {
+    return rocprim::radix_sort_pairs(temp, *temp_bytes, first_in, first_out, pos_in, perm_out, (size_t)n, 0,
+                                     64, s);
+}
+
+__global__ void gather_kernel(const u32* perm, u64 n, const u64* keys, const u64* counts, u64* keys_o,
+                              u64* counts_o, u32* rank) {
+    for (u64 j = blockIdx.x * (u64)blockDim.x + threadIdx.x; j < n; j += (u64)gridDim.x * blockDim.x) {
+        const u32 p = perm[j];
+        keys_o[j] = keys[p];
+        counts_o[j] = counts[p];
+        rank[p] = (u32)j;
+    }
+}
+
+hipError_t launch_gather(const u32* perm, u64 n, const u64* keys, const u64* counts, u64* keys_o, u64* counts_o,
+                         u32* rank, hipStream_t s) {
+    if (!n) return hipSuccess;
+    const int grid = (int)std::min<u64>((n + 255) / 256, 8192);
+    hipLaunchKernelGGL(gather_kernel, dim3(grid), dim3(256), 0, s, perm, n, keys, counts, keys_o, counts_o, rank);
+    return hipGetLastError();
+}
+
+__device__ __forceinline__ const GSlot* table_find(const GSlot* slots, u64 mask, u64 key) {
+    u64 h = mix64(key) & mask;
+    for (u64 probe = 0; probe <= mask; ++probe) {
+        const GSlot* s = &slots[h];
+        if (s->key == key) return s;
+        if (s->key == 0) return nullptr;
+        h = (h + 1) & mask;
+    }
+    return nullptr;
+}
+
+// write each live slot's sorted index into slot.uidx (keys in sorted order)
+__global__ void set_uidx_kernel(GSlot* slots, u64 mask, const u64* keys, u64 n) {
+    for (u64 j = blockIdx.x * (u64)blockDim.x + threadIdx.x; j < n; j += (u64)gridDim.x * blockDim.x) {
+        GSlot* s = const_cast<GSlot*>(table_find(slots, mask, keys[j]));
+        if (s) s->uidx = (u32)j;
+    }
+}
+
+hipError_t launch_set_uidx(GSlot* slots, u64 mask, const u64* keys, u64 n, const u32* rank_of_pos, hipStream_t s) {
+    (void)rank_of_pos;
+    if (!n) return hipSuccess;
+    const int grid = (int)std::min<u64>((n + 255) / 256, 8192);
+    hipLaunchKernelGGL(set_uidx_kernel, dim3(grid), dim3(256), 0, s, slots, mask, keys, n);
+    return hipGetLastError();
+}
+
+__global__ void presence_map_kernel(const GSlot* slots, u64 mask, const Presence* pres, u64 n, u32* uidx,
+                                    u32* file_idx) {
+    for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
+        const Presence p = pres[i];
+        const GSlot* s = table_find(slots, mask, p.key);
+        uidx[i] = s ? s->uidx : 0xFFFFFFFFu;
+        file_idx[i] = p.tag - 1u;
+    }
+}
+
+hipError_t launch_presence_map(const GSlot* slots, u64 mask, const Presence* pres, u64 n, u32* uidx,
+                               u32* file_idx, hipStream_t s) {
+    if (!n) return hipSuccess;
+    const int grid = (int)std::min<u64>((n + 255) / 256, 8192);
+    hipLaunchKernelGGL(presence_map_kernel, dim3(grid), dim3(256), 0, s, slots, mask, pres, n, uidx, file_idx);
+    return hipGetLastError();
+}
+
+// merge another GPU's compacted table into this one (count +, first min); presence of
+// remote keys travels separately (fr_get_presence on each rank)
+__global__ void merge_kernel(Table t, DevState* st, const u64* keys, const u64* counts, const u64* first, u64 n) {
+    for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x)
+        global_insert(t, st, keys[i], counts[i], first[i], 0u);
+}
+
+hipError_t launch_merge(Table t, DevState* st, const u64* keys, const u64* counts, const u64* first, u64 n,
+                        hipStream_t s) {
+    if (!n) return hipSuccess;
+    const int grid = (int)std::min<u64>((n + 255) / 256, 8192);
+    hipLaunchKernelGGL(merge_kernel, dim3(grid), dim3(256), 0, s, t, st, keys, counts, first, n);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------
+// classify: lane per unique code, the sheet broadcast from LDS
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ int mism(u64 q, u64 s) {  // Hamming distance of two 3-bit packed strings
+    const u64 x = q ^ s;
+    return __popcll((x | (x >> 1) | (x >> 2)) & 0x1249249249249249ull);
+}
+
+constexpr int CLS_WG = 256;
+constexpr int CLS_LDS_ROWS = 2048;
+constexpr int RC_LDS_NAMES = 1024;
+
+__device__ __forceinline__ void class_of(u64 q1, u64 q2, const u64* s1, const u64* s2, int S, int nsubs, int& m1,
+                                         int& m2, int& cls, int& row) {
+    m1 = -1;
+    m2 = -1;
+    int both = 0, r = -1;
+    for (int i = 0; i < S; ++i) {
+        const bool a = mism(q1, s1[i]) <= nsubs;
+        const bool b = mism(q2, s2[i]) <= nsubs;
+        if (a && m1 < 0) m1 = i;
+        if (b && m2 < 0) m2 = i;
+        if (a && b) {
+            if (!both) r = i;
+            ++both;
+        }
+    }
+    if (m1 >= 0 && m2 >= 0) {
+        cls = both == 0 ? CLS_HOP : both == 1 ? CLS_DEMUX : CLS_AMBIG;
+        row = both == 1 ? r : -1;
+    } else {
+        cls = CLS_UNDET;
+        m1 = -1;
+        m2 = -1;
+        row = -1;
+    }
+}
+
+__global__ __launch_bounds__(CLS_WG) void classify_kernel(const u64* keys, const u64* counts, u64 n, SheetArgs sh,
+                                                          int nsubs, int rc, ClassOut o) {
+    __shared__ u64 s1[CLS_LDS_ROWS], s2[CLS_LDS_ROWS], s2rc[CLS_LDS_ROWS];
+    __shared__ unsigned long long lf[RC_LDS_NAMES], lr[RC_LDS_NAMES];
+    const bool in_lds = sh.S <= CLS_LDS_ROWS;
+    const bool rc_lds = sh.n_names <= RC_LDS_NAMES;
+    if (in_lds) {
+        for (int i = threadIdx.x; i < sh.S; i += CLS_WG) {
+            s1[i] = sh.i1[i];
+            s2[i] = sh.i2[i];
+            s2rc[i] = rc ? sh.i2rc[i] : 0;
+        }
+    }
+    if (rc && rc_lds)
+        for (int i = threadIdx.x; i < sh.n_names; i += CLS_WG) lf[i] = lr[i] = 0;
+    __syncthreads();
+    const u64* S1 = in_lds ? s1 : sh.i1;
+    const u64* S2 = in_lds ? s2 : sh.i2;
+    const u64* S2rc = in_lds ? s2rc : sh.i2rc;
+
+    const u64 u = blockIdx.x * (u64)CLS_WG + threadIdx.x;
+    if (u < n) {
+        const u64 key = keys[u];
+        // split the code at '+' (symbol 6): idx1, idx2 = code.split("+")[0:2]  (frender.py:306)
+        int p1 = -1, p2 = MAXSYM, len = 0;
+        for (int i = 0; i < MAXSYM; ++i) {
+            const u32 sy = (u32)(key >> (3 * i)) & 7u;
+            if (!sy) break;
+            len = i + 1;
+            if (sy == 6u) {
+                if (p1 < 0) p1 = i;
+                else if (p2 == MAXSYM) p2 = i;
+            }
+        }
+        int err = 0;
+        int m1 = -1, m2 = -1, cls = CLS_UNDET, row = -1;
+        int rm2 = -1, rcls = CLS_UNDET, rrow = -1;
+        if (p1 < 0) {
+            err = 3;
+        } else {
+            const int n1 = p1;
+            const int e2 = p2 < len ? p2 : len;
+            const int n2 = e2 - p1 - 1;
+            // the length asserts (frender.py:227-229), idx1 list first
+            if (sh.S > 0 && (sh.L1u == -2 || sh.L1u != n1)) err = 1;
+            else if (sh.S > 0 && (sh.L2u == -2 || sh.L2u != n2)) err = 2;
+            else {
+                const u64 q1 = n1 ? (key & ((1ull << (3 * n1)) - 1ull)) : 0ull;
+                const u64 q2 = n2 ? ((key >> (3 * (p1 + 1))) & ((1ull << (3 * n2)) - 1ull)) : 0ull;
+                class_of(q1, q2, S1, S2, sh.S, nsubs, m1, m2, cls, row);
+                if (rc) {
+                    int rm1;
+                    class_of(q1, q2, S1, S2rc, sh.S, nsubs, rm1, rm2, rcls, rrow);
+                    // both calls demuxable to different sample NAMES -> ambiguous (frender.py:336-349)
+                    if (cls == CLS_DEMUX && rcls == CLS_DEMUX && sh.name[row] != sh.name[rrow]) {
+                        cls = CLS_AMBIG;
+                        row = -1;
+                        rcls = CLS_AMBIG;
+                        rrow = -1;
+                    }
+                }
+            }
+        }
+        if (err) {
+            atomicMin((unsigned long long*)o.err_first, (unsigned long long)u);
+            if (o.err_which) o.err_which[u] = err;
+        } else if (o.err_which) {
+            o.err_which[u] = 0;
+        }
+        o.m1[u] = (int16_t)m1;
+        o.m2[u] = (int16_t)m2;
+        o.cls[u] = (u8)cls;
+        o.row[u] = (int16_t)row;
+        if (rc) {
+            o.rc_m2[u] = (int16_t)rm2;
+            o.rc_cls[u] = (u8)rcls;
+            o.rc_row[u] = (int16_t)rrow;
+            const u64 cnt = counts[u];
+            if (cls == CLS_DEMUX) {
+                const int nm = sh.name[row];
+                if (rc_lds) atomicAdd(&lf[nm], (unsigned long long)cnt);
+                else atomicAdd((unsigned long long*)&o.rc_f[nm], (unsigned long long)cnt);
+            }
+            if (rcls == CLS_DEMUX) {
+                const int nm = sh.name[rrow];
+                if (rc_lds) atomicAdd(&lr[nm], (unsigned long long)cnt);
+                else atomicAdd((unsigned long long*)&o.rc_r[nm], (unsigned long long)cnt);
+            }
+        }
+    }
+    if (rc && rc_lds) {
+        __syncthreads();
+        for (int i = threadIdx.x; i < sh.n_names; i += CLS_WG) {
+            if (lf[i]) atomicAdd((unsigned long long*)&o.rc_f[i], lf[i]);
+            if (lr[i]) atomicAdd((unsigned long long*)&o.rc_r[i], lr[i]);
+        }
+    }
+}
+
+hipError_t launch_classify(const u64* keys, const u64* counts, u64 n, SheetArgs sh, int nsubs, int rc, ClassOut o,
+                           hipStream_t s) {
+    if (!n) return hipSuccess;
+    const u64 grid = (n + CLS_WG - 1) / CLS_WG;
+    hipLaunchKernelGGL(classify_kernel, dim3((u32)grid), dim3(CLS_WG), 0, s, keys, counts, n, sh, nsubs, rc, o);
+    return hipGetLastError();
+}
+
+// generic classifier over case-folded code points (codes outside the fast alphabet)
+__device__ void class_of_cp(const u32* q1, int n1, const u32* q2, int n2, const u32* s1, const u32* s2, int stride,
+                            int S, int nsubs, int& m1, int& m2, int& cls, int& row) {
+    m1 = -1;
+    m2 = -1;
+    int both = 0, r = -1;
+    for (int i = 0; i < S; ++i) {
+        int d1 = 0, d2 = 0;
+        for (int k = 0; k < n1; ++k) d1 += q1[k] != s1[(u64)i * stride + k];
+        for (int k = 0; k < n2; ++k) d2 += q2[k] != s2[(u64)i * stride + k];
+        const bool a = d1 <= nsubs, b = d2 <= nsubs;
+        if (a && m1 < 0) m1 = i;
+        if (b && m2 < 0) m2 = i;
+        if (a && b) {
+            if (!both) r = i;
+            ++both;
+        }
+    }
+    if (m1 >= 0 && m2 >= 0) {
+        cls = both == 0 ? CLS_HOP : both == 1 ? CLS_DEMUX : CLS_AMBIG;
+        row = both == 1 ? r : -1;
+    } else {
+        cls = CLS_UNDET;
+        m1 = m2 = row = -1;
+    }
+}
+
+__global__ void classify_cp_kernel(int n, const u32* q1, const int32_t* q1len, const u32* q2, const int32_t* q2len,
+                                   int stride, int S, const u32* s1, const int32_t* s1len, const u32* s2,
+                                   const int32_t* s2len, const u32* s2rc, const int32_t* name, int nsubs, int rc,
+                                   ClassOut o) {
+    const int u = blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= n) return;
+    const int n1 = q1len[u], n2 = q2len[u];
+    int err = 0;
+    for (int i = 0; i < S && !err; ++i)
+        if (s1len[i] != n1) err = 1;
+    for (int i = 0; i < S && !err; ++i)
+        if (s2len[i] != n2) err = 2;
+    int m1 = -1, m2 = -1, cls = CLS_UNDET, row = -1, rm2 = -1, rcls = CLS_UNDET, rrow = -1;
+    if (!err) {
+        class_of_cp(q1 + (u64)u * stride, n1, q2 + (u64)u * stride, n2, s1, s2, stride, S, nsubs, m1, m2, cls, row);
+        if (rc) {
+            int rm1;
+            class_of_cp(q1 + (u64)u * stride, n1, q2 + (u64)u * stride, n2, s1, s2rc, stride, S, nsubs, rm1, rm2,
+                        rcls, rrow);
+            if (cls == CLS_DEMUX && rcls == CLS_DEMUX && name[row] != name[rrow]) {
+                cls = rcls = CLS_AMBIG;
+                row = rrow = -1;
+            }
+        }
+    }
+    if (o.err_which) o.err_which[u] = err;
+    o.m1[u] = (int16_t)m1;
+    o.m2[u] = (int16_t)m2;
+    o.cls[u] = (u8)cls;
+    o.row[u] = (int16_t)row;
+    if (rc) {
+        o.rc_m2[u] = (int16_t)rm2;
+        o.rc_cls[u] = (u8)rcls;
+        o.rc_row[u] = (int16_t)rrow;
+    }
+}
+
+hipError_t launch_classify_cp(int n, const u32* q1, const int32_t* q1len, const u32* q2, const int32_t* q2len,
+                              int stride, int S, const u32* s1, const int32_t* s1len, const u32* s2,
+                              const int32_t* s2len, const u32* s2rc, const int32_t* name, int nsubs, int rc,
+                              ClassOut o, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(classify_cp_kernel, dim3((n + 127) / 128), dim3(128), 0, s, n, q1, q1len, q2, q2len, stride,
+                       S, s1, s1len, s2, s2len, s2rc, name, nsubs, rc, o);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------
+// SYN-v1 generator (byte-identical to frender_amd/synth.py generate_records)
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ u64 syn_h(u64 base, u64 r, u32 k) { return mix64(((r << 8) | k) ^ base); }
+
+__global__ void synth_kernel(u8* out, u64 r0, u64 n, int R, u64 base, const u8* idx1, const u8* idx2, int S, int L1,
+                             int L2) {
+    const u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const u64 r = r0 + i;
+    const int reclen = 36 + L1 + 1 + L2 + 1 + 2 * R + 4;
+    u8* o = out + i * (u64)reclen;
+    const char* ACGT = "ACGT";
+    u8 idx[64];
+    const u64 s = syn_h(base, r, 0) % (u64)S;
+    for (int j = 0; j < L1; ++j) idx[j] = idx1[s * L1 + j];
+    for (int j = 0; j < L2; ++j) idx[L1 + j] = idx2[s * L2 + j];
+    if (syn_h(base, r, 1) % 10000ull < 200ull) {
+        const u64 s2 = syn_h(base, r, 2) % (u64)S;
+        for (int j = 0; j < L2; ++j) idx[L1 + j] = idx2[s2 * L2 + j];
+    }
+    if (syn_h(base, r, 3) % 10000ull < 100ull) {
+        const u64 hj = syn_h(base, r, 4);
+        for (int j = 0; j < L1 + L2; ++j) idx[j] = ACGT[(hj >> (2 * j)) & 3ull];
+    }
+    for (int j = 0; j < L1 + L2; ++j) {
+        const u64 v = syn_h(base, r, 8 + j);
+        const u64 p = v % 10000ull;
+        if (p < 50ull) {
+            const u8 c = idx[j];
+            const u64 orig = c == 'A' ? 0 : c == 'C' ? 1 : c == 'G' ? 2 : c == 'T' ? 3 : 0;
+            idx[j] = ACGT[(orig + 1ull + (v >> 32) % 3ull) % 4ull];
+        } else if (p < 70ull) {
+            idx[j] = 'N';
+        }
+    }
+    int pos = 0;
+    const char* h0 = "@SYN:1:FCX:1:";
+    for (int k = 0; k < 13; ++k) o[pos++] = h0[k];
+    u64 v = (r / 10000000000ull) % 10000ull;
+    for (int k = 3; k >= 0; --k) { o[pos + k] = '0' + (u8)(v % 10ull); v /= 10ull; }
+    pos += 4;
+    o[pos++] = ':';
+    v = (r / 100000ull) % 100000ull;
+    for (int k = 4; k >= 0; --k) { o[pos + k] = '0' + (u8)(v % 10ull); v /= 10ull; }
+    pos += 5;
+    o[pos++] = ':';
+    v = r % 100000ull;
+    for (int k = 4; k >= 0; --k) { o[pos + k] = '0' + (u8)(v % 10ull); v /= 10ull; }
+    pos += 5;
+    const char* h1 = " 1:N:0:";
+    for (int k = 0; k < 7; ++k) o[pos++] = h1[k];
+    for (int j = 0; j < L1; ++j) o[pos++] = idx[j];
+    o[pos++] = '+';
+    for (int j = 0; j < L2; ++j) o[pos++] = idx[L1 + j];
+    o[pos++] = '\n';
+    for (int w = 0; w < (R + 31) / 32; ++w) {
+        const u64 hv = syn_h(base, r, 80 + w);
+        for (int j = 32 * w; j < R && j < 32 * w + 32; ++j) o[pos + j] = ACGT[(hv >> (2 * (j - 32 * w))) & 3ull];
+    }
+    pos += R;
+    o[pos++] = '\n';
+    o[pos++] = '+';
+    o[pos++] = '\n';
+    for (int w = 0; w < (R + 7) / 8; ++w) {
+        const u64 hv = syn_h(base, r, 100 + w);
+        for (int j = 8 * w; j < R && j < 8 * w + 8; ++j) o[pos + j] = (u8)(((hv >> (8 * (j - 8 * w))) & 0xFFull) % 42ull) + 33;
+    }
+    pos += R;
+    o[pos++] = '\n';
+}
+
+hipError_t launch_synth(u8* out, u64 r0, u64 n, int R, u64 seed, const u8* idx1, const u8* idx2, int S, int L1,
+                        int L2, hipStream_t s) {
+    if (!n) return hipSuccess;
+    const u64 base = mix64(seed + 0x9E3779B97F4A7C15ull);
+    const u64 grid = (n + 255) / 256;
+    hipLaunchKernelGGL(synth_kernel, dim3((u32)grid), dim3(256), 0, s, out, r0, n, R, base, idx1, idx2, S, L1, L2);
+    return hipGetLastError();
+}
+
+}  // namespace fr

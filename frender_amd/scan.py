@@ -1,0 +1,433 @@
+"""frender `scan` on MI355X — host driver around the C ABI (include/frender_amd.h).
+
+Mirrors the reference's scan interface (frender.py:154-642): the same function
+names, argument meaning, stdout lines, CSV formats and failure modes.  The hot
+path — per-read tally (scan_file/tally_barcodes), Hamming classification
+(process -> analyze_barcodes_with_rc -> analyze_barcode ->
+get_indexes_of_approx_matches) and the -rc per-name sums — runs in HIP kernels
+on the GPU through frender_amd._lib; nothing here falls back to a CPU path.
+
+Data model: the merged tally (`barcode_counter["total"]`, frender.py:199-203) is a
+UniqueTable of codes in first-occurrence order with counts and per-file presence;
+classification results are arrays aligned with it.  Codes over {A,C,G,T,N,+} up
+to 21 chars are "fast" keys counted entirely on the GPU; anything else
+(lowercase, other bytes, longer codes) is an "exotic" record the GPU captures
+verbatim into a device pool, merged here by string and classified on the GPU by
+the code-point classifier.
+"""
+from __future__ import annotations
+
+import csv
+import gzip
+import os
+import queue
+import re
+import threading
+from datetime import datetime, timezone
+from pathlib import Path
+
+import numpy as np
+
+from . import _lib
+from .host import find_barcode_file, get_cores, get_indexes, parse_files, reverse_complement
+
+READ_CHUNK = 64 << 20
+UNDET, HOP, DEMUX, AMBIG = 0, 1, 2, 3
+CLASS_NAMES = _lib.CLASS_NAMES
+ORD_SHIFT = 44
+
+_CTX = None
+
+
+def default_context() -> _lib.Context:
+    global _CTX
+    if _CTX is None:
+        dev = int(os.environ.get("LOCAL_RANK", "0"))
+        _CTX = _lib.Context(device=dev)
+    return _CTX
+
+
+class UniqueTable:
+    """The merged tally: codes in (file, first occurrence) order (R4/R5)."""
+
+    def __init__(self, codes, counts, first, fast_idx, exo_idx, pres_u, pres_f, files, records):
+        self.codes = codes            # list[str], merged order
+        self.counts = counts          # uint64
+        self.first = first            # uint64 ordinals (file_index+1) << 44 | byte offset
+        self.fast_idx = fast_idx      # merged -> index in the GPU's finalized table, or -1
+        self.exo_idx = exo_idx        # merged -> index in the exotic list, or -1
+        self.pres_u = pres_u          # (unique, file) presence pairs
+        self.pres_f = pres_f
+        self.files = files            # basenames in input order
+        self.records = records        # records per file
+
+    def __len__(self):
+        return len(self.codes)
+
+    def as_dict(self) -> dict:
+        """barcode_counter["total"] as a plain dict (small inputs / tests)."""
+        return {c: int(n) for c, n in zip(self.codes, self.counts)}
+
+
+def _gz_chunks(path, chunk=READ_CHUNK, depth=2):
+    """Inflate in a helper thread (zlib releases the GIL) while the GPU consumes."""
+    q: queue.Queue = queue.Queue(maxsize=depth)
+    stop = threading.Event()
+
+    def work():
+        try:
+            with gzip.open(path, "rb") as g:
+                while not stop.is_set():
+                    b = g.read(chunk)
+                    q.put(b)
+                    if not b:
+                        return
+        except BaseException as e:  # noqa: BLE001 - re-raised in the consumer
+            q.put(e)
+
+    t = threading.Thread(target=work, daemon=True)
+    t.start()
+    try:
+        while True:
+            item = q.get()
+            if isinstance(item, BaseException):
+                raise item
+            if not item:
+                return
+            yield item
+    finally:
+        stop.set()
+        while t.is_alive():
+            try:
+                q.get_nowait()
+            except queue.Empty:
+                t.join(0.01)
+
+
+def tally_barcodes(cores, files, sample=None, ctx=None) -> UniqueTable:
+    """frender.py:183-207 (+ scan_file :154-181) on the GPU: files in order, one context."""
+    print(f"Scanning {len(files)} files with {cores} core{'' if cores == 1 else 's'}...")
+    if sample:
+        assert sample >= 1, "Number of reads to sample must be ≥ 1!"
+        print(f"Sampling {sample} reads from the head of each file...")
+    ctx = ctx or default_context()
+    ctx.reset()
+    names, records = [], []
+    exo: dict = {}
+    exo_seen = 0
+    for fi, path in enumerate(files):
+        name = str(os.path.basename(path))
+        names.append(name)
+        print(f"Tallying barcodes from {name}...", end="")
+        ctx.begin_file(sample)
+        for chunk in _gz_chunks(path):
+            if ctx.feed(chunk):
+                break
+        st = ctx.end_file()
+        if st.error == _lib.FR_SCAN_NO_SPACE:  # frender.py:169 split(" ")[1]
+            raise IndexError("list index out of range")
+        if st.error == _lib.FR_SCAN_UTF8:  # gzip.open(..., "rt") decode (frender.py:159)
+            raise UnicodeDecodeError("utf-8", b"", 0, 1, "invalid start byte")
+        new_here = int(st.new_keys)
+        if st.exotic:
+            ords, lens, offs, pool = ctx.exotic()
+            for k in range(exo_seen, len(ords)):
+                code = bytes(pool[int(offs[k]):int(offs[k]) + int(lens[k])]).decode("utf-8")
+                e = exo.get(code)
+                if e is None:
+                    exo[code] = [1, int(ords[k]), {fi}]
+                    new_here += 1
+                else:
+                    e[0] += 1
+                    e[1] = min(e[1], int(ords[k]))
+                    if fi not in e[2]:
+                        e[2].add(fi)
+                        new_here += 1
+            exo_seen = len(ords)
+        records.append(int(st.records))
+        print(f"found {new_here} new barcode{'' if new_here == 1 else 's'} in {st.records} reads.")
+    print(type([]), len(files))
+    ctx.finalize()
+    keys, counts, first = ctx.unique()
+    pu, pf = ctx.presence()
+    fast_codes = _lib.decode_keys(keys)
+    exo_codes = list(exo.keys())
+    exo_counts = np.array([exo[c][0] for c in exo_codes], dtype=np.uint64)
+    exo_first = np.array([exo[c][1] for c in exo_codes], dtype=np.uint64)
+    all_first = np.concatenate([first, exo_first])
+    order = np.argsort(all_first, kind="stable")
+    nf = len(fast_codes)
+    all_codes = fast_codes + exo_codes
+    codes = [all_codes[i] for i in order.tolist()]
+    pos = np.empty(order.size, dtype=np.int64)
+    pos[order] = np.arange(order.size)
+    fast_idx = np.where(order < nf, order, -1)
+    exo_idx = np.where(order >= nf, order - nf, -1)
+    ep_u = [pos[nf + i] for i, c in enumerate(exo_codes) for _ in exo[c][2]]
+    ep_f = [f for c in exo_codes for f in sorted(exo[c][2])]
+    pres_u = np.concatenate([pos[pu.astype(np.int64)] if pu.size else np.zeros(0, np.int64),
+                             np.array(ep_u, dtype=np.int64)])
+    pres_f = np.concatenate([pf.astype(np.int64), np.array(ep_f, dtype=np.int64)])
+    return UniqueTable(codes, np.concatenate([counts, exo_counts])[order], all_first[order], fast_idx, exo_idx,
+                       pres_u, pres_f, names, records)
+
+
+class Results:
+    """process() output: arrays aligned with the UniqueTable (frender.py:286-291, :325-332)."""
+
+    def __init__(self, n, rc):
+        self.m1 = np.full(n, -1, np.int16)
+        self.m2 = np.full(n, -1, np.int16)
+        self.cls = np.zeros(n, np.uint8)
+        self.row = np.full(n, -1, np.int16)
+        self.rc = rc
+        if rc:
+            self.rc_m2 = np.full(n, -1, np.int16)
+            self.rc_cls = np.zeros(n, np.uint8)
+            self.rc_row = np.full(n, -1, np.int16)
+        self.rc_f = None
+        self.rc_r = None
+        self.idx1 = self.idx2 = self.ids = None
+        self.names = None
+
+
+def _sheet_names(ids):
+    names = list(dict.fromkeys(ids))
+    where = {n: i for i, n in enumerate(names)}
+    return names, [where[i] for i in ids]
+
+
+def _length_error(q: str, entries) -> AssertionError:
+    ql = q.lower()
+    for e in entries:
+        if len(ql) != len(e.lower()):
+            return AssertionError(f"Barcode {ql} doesn't match length of supplied barcode {e.lower()}")
+    return AssertionError("length mismatch")  # pragma: no cover
+
+
+def process(cores, table: UniqueTable, indexes: dict, num_subs: int, rc_mode: bool, ctx=None) -> Results:
+    """frender.py:391-426 on the GPU: classify every unique code (fast keys by packed
+    Hamming, exotic codes by the code-point classifier); raise the reference's first error."""
+    ctx = ctx or default_context()
+    idx1, idx2, ids = list(indexes["idx1"]), list(indexes["idx2"]), list(indexes["id"])
+    names, name_id = _sheet_names(ids)
+    ctx.set_sheet(idx1, idx2, [reverse_complement(x) for x in idx2], name_id, len(names))
+    if cores > 1:
+        print(f"Multiprocessing with {cores} cores")
+    n = len(table)
+    res = Results(n, rc_mode)
+    res.idx1, res.idx2, res.ids, res.names = idx1, idx2, ids, names
+    errs = []  # (merged position, exception)
+    fsel = np.nonzero(table.fast_idx >= 0)[0]
+    if fsel.size:
+        out = ctx.classify(num_subs, rc_mode)
+        fi = table.fast_idx[fsel]
+        res.m1[fsel], res.m2[fsel], res.cls[fsel], res.row[fsel] = out["m1"][fi], out["m2"][fi], out["cls"][fi], out["row"][fi]
+        if rc_mode:
+            res.rc_m2[fsel], res.rc_cls[fsel], res.rc_row[fsel] = out["rc_m2"][fi], out["rc_cls"][fi], out["rc_row"][fi]
+        if out["err_unique"] >= 0:
+            j = int(np.nonzero(table.fast_idx == out["err_unique"])[0][0])
+            errs.append((j, out["err_which"]))
+    esel = np.nonzero(table.exo_idx >= 0)[0]
+    f_add = np.zeros(len(names), np.uint64)
+    r_add = np.zeros(len(names), np.uint64)
+    if esel.size:
+        split_ok, q1, q2, js = [], [], [], []
+        for j in esel.tolist():
+            parts = table.codes[j].split("+")
+            if len(parts) < 2:
+                errs.append((j, 3))
+                continue
+            js.append(j)
+            q1.append(parts[0].lower())
+            q2.append(parts[1].lower())
+        if js:
+            out = ctx.classify_cp(q1, q2, num_subs, rc_mode)
+            ja = np.array(js)
+            res.m1[ja], res.m2[ja], res.cls[ja], res.row[ja] = out["m1"], out["m2"], out["cls"], out["row"]
+            if rc_mode:
+                res.rc_m2[ja], res.rc_cls[ja], res.rc_row[ja] = out["rc_m2"], out["rc_cls"], out["rc_row"]
+                for k, j in enumerate(js):
+                    if out["cls"][k] == DEMUX:
+                        f_add[name_id[out["row"][k]]] += table.counts[j]
+                    if out["rc_cls"][k] == DEMUX:
+                        r_add[name_id[out["rc_row"][k]]] += table.counts[j]
+            for k, j in enumerate(js):
+                if out["err"][k]:
+                    errs.append((j, int(out["err"][k])))
+    if errs:
+        j, which = min(errs)
+        code = table.codes[j]
+        if which == 3:  # idx1, idx2 = barcode.split("+")[0:2]  (frender.py:306)
+            raise ValueError("not enough values to unpack (expected 2, got 1)")
+        parts = code.split("+")
+        raise _length_error(parts[0], idx1) if which == 1 else _length_error(parts[1], idx2)
+    if rc_mode:
+        f, r = ctx.rc_counts()
+        res.rc_f = f + f_add
+        res.rc_r = r + r_add
+    return res
+
+
+def call_rc_mode_per_id(results: Results, ids) -> dict:
+    """frender.py:354-388: per distinct name, use rc idx2 iff its reads beat the forward ones."""
+    if len(results.cls) == 0:
+        raise IndexError("list index out of range")  # results_list[0] on an empty scan (:364)
+    assert results.rc, ("It looks like this frender result csv was not generated with the -rc flag. Either specify a "
+                        "different result csv, or run this command without setting the -rc flag.")
+    return {name: {"call": bool(int(f) < int(r)), "reads_f": int(f), "reads_rc": int(r)}
+            for name, f, r in zip(results.names, results.rc_f, results.rc_r)}
+
+
+def report_rc_call_info(rc_calls: dict, indexes: dict, out_csv_name: str) -> None:
+    """frender.py:429-479 (stdout table + frender-index-2-calls_*.csv)."""
+    rc_name = out_csv_name.replace("frender-scan-results_", "frender-index-2-calls_")
+    print("Based on the barcodes in the supplied fastq file, the following index 2 sequences will be used\n"
+          f"(also recorded in {rc_name}):\n")
+    print("Sample Name", "Supplied Index 2", "Reads supporting (forward)", "Reverse complement Index 2",
+          "Reads supporting (rev comp)", "Final call", sep="\t")
+    first_row = {}
+    for i, a in enumerate(indexes["id"]):
+        first_row.setdefault(a, i)
+    for a, c in rc_calls.items():
+        i2 = indexes["idx2"][first_row[a]]
+        print(a, i2, c["reads_f"], reverse_complement(i2), c["reads_rc"],
+              "reverse complement" if c["call"] else "forward", sep="\t")
+    with open(rc_name, "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["sample_name", "supplied_index_2", "reads_supplied_index_2", "rc_index_2", "reads_rc_index_2",
+                    "use_rc"])
+        for a, c in rc_calls.items():
+            i2 = indexes["idx2"][first_row[a]]
+            w.writerow([a, i2, c["reads_f"], reverse_complement(i2), c["reads_rc"], "TRUE" if c["call"] else "FALSE"])
+
+
+def call_barcodes_correctly_distributed(table: UniqueTable, results: Results, prefix: str):
+    """frender.py:504-564 (R10): per unique, every scanned file (by basename; the last
+    file of a basename wins, :204-205) holding it must match its class's pattern."""
+    basenames = list(dict.fromkeys(table.files))
+    if not basenames:
+        return None, set()
+    bidx = {b: i for i, b in enumerate(basenames)}
+    last_file = {b: i for i, b in enumerate(table.files)}
+    file_b = np.array([bidx[b] for b in table.files], dtype=np.int64)
+    file_live = np.array([last_file[b] == i for i, b in enumerate(table.files)], dtype=bool)
+    # the demuxable patterns are compiled per (barcode, file) by the reference: an invalid
+    # one raises at the first demuxable barcode in order
+    rows = results.row.astype(np.int64)
+    demux = np.nonzero(results.cls == DEMUX)[0]
+    pat = {}
+    for j in demux.tolist():
+        nm = results.ids[rows[j]]
+        if nm not in pat:
+            pat[nm] = re.compile(nm.removeprefix(prefix), re.I)
+    names = results.names
+    name_of = {n: k for k, n in enumerate(names)}
+    groups = [re.compile("undetermined", re.I), re.compile("undetermined|index-hop", re.I),
+              re.compile("undetermined|ambiguous", re.I)] + [pat.get(n) for n in names]
+    ok = np.ones((len(groups), len(basenames)), dtype=bool)
+    for g, rx in enumerate(groups):
+        if rx is None:
+            continue
+        for b, fn in enumerate(basenames):
+            ok[g, b] = bool(re.search(rx, fn))
+    grp = np.array([0, 1, -1, 2], dtype=np.int64)[results.cls.astype(np.int64)]  # undet, hop, -, ambiguous
+    if demux.size:
+        grp[demux] = 3 + np.array([name_of[results.ids[r]] for r in rows[demux].tolist()], dtype=np.int64)
+    pu, pf = table.pres_u, table.pres_f
+    keep = file_live[pf] if pf.size else np.zeros(0, bool)
+    pu, pf = pu[keep], pf[keep]
+    pair_ok = ok[grp[pu], file_b[pf]] if pu.size else np.zeros(0, bool)
+    demux_ok = np.ones(len(table), dtype=bool)
+    demux_ok[pu[~pair_ok]] = False
+    bad = {basenames[b] for b in np.unique(file_b[pf[~pair_ok]]).tolist()}
+    return demux_ok, bad
+
+
+def report_analysis(table: UniqueTable, results: Results, demux_ok, out_csv_name: str) -> None:
+    """frender.py:482-501: the scan CSV (excel dialect, columns in the code's order)."""
+    print(f"Analysis complete! Writing results to {out_csv_name}")
+    if len(table) == 0:
+        raise IndexError("list index out of range")  # results[0].keys() on an empty scan (:497)
+    idx1, idx2, ids = results.idx1, results.idx2, results.ids
+    m1, m2, cls, row = results.m1.tolist(), results.m2.tolist(), results.cls.tolist(), results.row.tolist()
+    counts = table.counts.tolist()
+    header = ["idx1", "idx2", "matched_idx1", "matched_idx2", "read_type", "sample_name", "reads"]
+    dok = demux_ok.tolist() if demux_ok is not None else None
+    if dok is not None:
+        header.append("demux_ok")
+
+    def rows():
+        for j, code in enumerate(table.codes):
+            parts = code.split("+")
+            r = [parts[0], parts[1], idx1[m1[j]] if m1[j] >= 0 else "", idx2[m2[j]] if m2[j] >= 0 else "",
+                 CLASS_NAMES[cls[j]], ids[row[j]] if row[j] >= 0 else "", counts[j]]
+            if dok is not None:
+                r.append(dok[j])
+            yield r
+
+    with open(out_csv_name, "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(header)
+        w.writerows(rows())
+
+
+def output_name(num_subs, user_infix, files_arg):
+    """frender.py:587-601."""
+    if len(files_arg) == 1:
+        p = Path(files_arg[0])
+        if Path.is_dir(p):
+            spec, tail = {"dir": p}, p.parts[-1]
+        elif Path.is_file(p):
+            spec, tail = {"file": p}, p.name
+        else:
+            raise SystemExit("Specified directory or file path doesn't seem to exist!")
+    else:
+        spec = {"file": [Path(f) for f in files_arg]}
+        tail = datetime.strftime(datetime.now(timezone.utc), "%Y-%M-%d_%H%M_%Z")
+    return f"frender-scan-results_{num_subs}-mismatches_{user_infix}_{tail}.csv".replace("__", "_"), spec
+
+
+def frender_scan(args, ctx=None) -> dict:
+    """frender.py:567-642 with the hot path on the GPU."""
+    num_subs = args.n
+    rc_mode = args.rc
+    cores = get_cores(args.c)
+    sample = args.s
+    user_infix = args.o if args.o else ""
+    prefix = args.p if args.p else ""
+    if args.b is None:
+        if len(args.files) != 1:
+            raise SystemExit("You have not specified a barcode table. Please either specify one with the argment -b or "
+                             "specify a directory including a barcode table")
+        barcode_file = find_barcode_file(Path(args.files[0]))
+    else:
+        barcode_file = Path(args.b)
+    indexes = get_indexes(barcode_file)
+    out_csv_name, spec = output_name(num_subs, user_infix, args.files)
+    files = parse_files(spec, just_r1=True)
+    ctx = ctx or default_context()
+    table = tally_barcodes(cores, files, sample, ctx=ctx)
+    print("Scanning complete! Analyzing barcodes...")
+    results = process(cores, table, indexes, num_subs, rc_mode, ctx=ctx)
+    if rc_mode:
+        rc_calls = call_rc_mode_per_id(results, indexes["id"])
+        print("First round of analysis complete.")
+        report_rc_call_info(rc_calls, indexes, out_csv_name)
+        indexes["idx2"] = [reverse_complement(indexes["idx2"][i]) if rc_calls[i_d]["call"] else indexes["idx2"][i]
+                           for i, i_d in enumerate(indexes["id"])]
+        print("\nRe-analyzing barcodes with corrected index 2 sequences...")
+        results = process(cores, table, indexes, num_subs, False, ctx=ctx)
+    demux_ok, mismatching = call_barcodes_correctly_distributed(table, results, prefix)
+    if mismatching:
+        print("Incorrectly demultiplexed barcodes found! Affected files:")
+        for a in mismatching:
+            print(a)
+    else:
+        print("It appears that all files are already correctly demultiplexed.")
+    report_analysis(table, results, demux_ok, out_csv_name)
+    return {"table": table, "results": results, "out_csv": out_csv_name}
+
+
+# the name the golden harness calls
+scan = frender_scan

@@ -1,0 +1,154 @@
+/*
+ * frender_amd.h — C ABI of libfrender_hip.so, the MI355X (gfx950) implementation of
+ * frender's `scan` hot path: per-read header scan + barcode tally, Hamming
+ * classification of the unique index combos, and the -rc per-sample call.
+ *
+ * The reference (njspix/frender, frender.py) has no FFI; its seam is three Python
+ * calls inside frender_scan (frender.py:606, :610/:628, :614).  The entry points
+ * below replace exactly those calls (each cites the reference function it
+ * replaces); the host CLI (frender_amd/scan.py) keeps the reference's flags and
+ * CSV formats and binds this header through ctypes (frender_amd/_lib.py).
+ *
+ * Conventions: every int-returning call returns FR_OK (0) or an FR_ERR_* code and
+ * leaves a message in fr_last_error(ctx).  All pointers are plain host pointers
+ * unless the name says _device.  Caller owns inputs; the library owns device
+ * memory and the arrays it hands back until the next call that rebuilds them.
+ * One context = one GPU = one host thread (not re-entrant).
+ */
+#ifndef FRENDER_AMD_H
+#define FRENDER_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FR_OK 0
+#define FR_ERR_INVALID 1   /* bad argument / call order */
+#define FR_ERR_HIP 2       /* HIP runtime error */
+#define FR_ERR_CAPACITY 3  /* a device table or pool is full */
+#define FR_ERR_DEVICE 4    /* a kernel reported an internal failure (look-back spin bound) */
+
+/* scan-time data errors: reported in fr_file_stats.error, mirroring the reference's crash */
+#define FR_SCAN_OK 0
+#define FR_SCAN_NO_SPACE 1 /* header line without ' ': IndexError at frender.py:169 */
+#define FR_SCAN_UTF8 2     /* invalid UTF-8: UnicodeDecodeError from gzip.open(...,"rt") at :159 */
+
+/* classification classes (read_type, frender.py:266-284) */
+#define FR_UNDETERMINED 0
+#define FR_INDEX_HOP 1
+#define FR_DEMUXABLE 2
+#define FR_AMBIGUOUS 3
+
+typedef struct fr_ctx fr_ctx;
+
+typedef struct fr_file_stats {
+    uint64_t records;        /* header lines counted (after -s), = `actual_reads` (frender.py:160-166) */
+    uint64_t lines;          /* lines in the file (universal newlines) */
+    uint64_t new_keys;       /* distinct fast-path codes in this file (`new_barcodes`, :175) */
+    uint64_t exotic;         /* records whose code left the fast alphabet (see fr_get_exotic) */
+    int32_t error;           /* FR_SCAN_* */
+    int32_t pad;
+    uint64_t error_offset;   /* file byte offset of the first offending header (FR_SCAN_NO_SPACE) */
+} fr_file_stats;
+
+typedef struct fr_timing {
+    uint64_t scan_launches;  /* tally kernel launches since fr_reset */
+    uint64_t scan_bytes;     /* decoded bytes those launches scanned */
+    double scan_ms;          /* summed HIP-event duration of those launches */
+    double last_scan_ms;     /* duration of the most recent launch */
+    double classify_ms;      /* last classify pass */
+    double finalize_ms;      /* last compaction + ordering */
+} fr_timing;
+
+/* ---- lifecycle ------------------------------------------------------------------ */
+fr_ctx* fr_create(int device, uint64_t chunk_bytes, uint64_t table_slots);
+void fr_destroy(fr_ctx* ctx);
+const char* fr_last_error(const fr_ctx* ctx);
+int fr_get_timing(fr_ctx* ctx, fr_timing* out);
+int fr_sync(fr_ctx* ctx);
+
+/* ---- sample sheet (the idx1/idx2/id lists of get_indexes, frender.py:90-116) -------
+ * idx*_packed: each entry case-folded (str.lower(), :226) and packed 3 bits/char,
+ * char i at bits [3i,3i+3): a=1 c=2 g=3 t=4 n=5, any other char=7; entries longer
+ * than 21 chars pack as 0 (they can only fail the length assert).  idx2rc_packed is
+ * the same for reverse_complement(idx2) (:210-211).  idx*_len are the case-folded
+ * lengths.  name_id[i] = index of row i's id among the distinct ids in
+ * first-appearance order (call_rc_mode_per_id's dict, :367).  The code-point
+ * arrays (stride `cp_stride`, may be NULL) feed the generic classifier used for
+ * codes outside the fast alphabet. */
+int fr_set_sheet(fr_ctx* ctx, int S,
+                 const uint64_t* idx1_packed, const int32_t* idx1_len,
+                 const uint64_t* idx2_packed, const int32_t* idx2_len,
+                 const uint64_t* idx2rc_packed, const int32_t* name_id, int n_names,
+                 const uint32_t* idx1_cp, const uint32_t* idx2_cp, const uint32_t* idx2rc_cp,
+                 int cp_stride);
+
+/* ---- tally: replaces tally_barcodes (frender.py:183-207) / scan_file (:154-181) ----
+ * Files are fed in parse_files order (:604); fr_reset starts a new scan. */
+int fr_reset(fr_ctx* ctx);
+int fr_begin_file(fr_ctx* ctx, int64_t max_records /* -s, <=0: no limit */);
+/* Decoded (gunzipped) bytes of the current file, any split; the library cuts at
+ * line ends, carries the remainder, copies through a pinned ring to HBM and
+ * launches.  Returns FR_OK, or 5 (FR_SAMPLE_DONE) once -s records were seen. */
+#define FR_SAMPLE_DONE 5
+int fr_feed(fr_ctx* ctx, const uint8_t* data, uint64_t len);
+/* The whole current file is already resident in HBM (bench / device producers). */
+int fr_feed_device(fr_ctx* ctx, const uint8_t* dev_data, uint64_t len);
+int fr_end_file(fr_ctx* ctx, fr_file_stats* out);
+
+/* ---- the merged unique table (barcode_counter["total"], :199-203) -----------------
+ * fr_finalize compacts the device hash table and orders it by first occurrence
+ * (file order, then byte offset) on the GPU; keys are 3-bit packed codes over
+ * {A=1,C=2,G=3,T=4,N=5,'+'=6}, char i at bits [3i,3i+3). */
+int fr_finalize(fr_ctx* ctx, uint64_t* n_unique, uint64_t* n_presence, uint64_t* n_exotic);
+int fr_get_unique(fr_ctx* ctx, uint64_t* keys, uint64_t* counts, uint64_t* first_ordinal);
+/* (unique index, file index) for every file a fast-path key occurs in (R10 demux_ok) */
+int fr_get_presence(fr_ctx* ctx, uint32_t* unique_idx, uint32_t* file_idx);
+/* raw exotic records: file byte offset | file index << 44, code length, pool offset */
+int fr_get_exotic(fr_ctx* ctx, uint64_t* ordinal, uint32_t* length, uint64_t* pool_offset,
+                  uint8_t* pool, uint64_t pool_bytes);
+
+/* ---- classify: replaces process (:391-426) -> analyze_barcodes_with_rc (:294-351)
+ *      -> analyze_barcode (:237-291) -> get_indexes_of_approx_matches (:214-234) ----
+ * Runs over the finalized unique table with the current sheet and num_subs.
+ * Per unique (host arrays of n_unique):  m1,m2 = first matching sheet row or -1
+ * (matched_idx1/2, :261-262), cls = FR_* class, row = the demux row or -1.  With
+ * rc_mode the rc_* arrays receive the rc(idx2) pass and the ambiguity override
+ * (:336-349) is applied; may be NULL otherwise.  err_unique receives the first
+ * unique index (in order) whose lengths fail the assert at :227 (or -1), and
+ * err_which 1 = idx1, 2 = idx2, 3 = no '+' (ValueError at :306). */
+int fr_classify(fr_ctx* ctx, int num_subs, int rc_mode,
+                int16_t* m1, int16_t* m2, uint8_t* cls, int16_t* row,
+                int16_t* rc_m2, uint8_t* rc_cls, int16_t* rc_row,
+                int64_t* err_unique, int32_t* err_which);
+/* per distinct name: reads demuxable with fwd idx2 / with rc idx2 (:367-373), from the
+ * last rc_mode classify */
+int fr_rc_counts(fr_ctx* ctx, uint64_t* reads_f, uint64_t* reads_rc);
+/* generic classifier for codes outside the fast alphabet: queries as case-folded
+ * code points (stride cp_stride), same outputs as fr_classify plus a per-query err_which */
+int fr_classify_cp(fr_ctx* ctx, int n, const uint32_t* q1, const int32_t* q1len,
+                   const uint32_t* q2, const int32_t* q2len, int cp_stride, int num_subs, int rc_mode,
+                   int16_t* m1, int16_t* m2, uint8_t* cls, int16_t* row,
+                   int16_t* rc_m2, uint8_t* rc_cls, int16_t* rc_row, int32_t* err_which);
+
+/* ---- multi-GPU merge: export / import the compacted table ----------- */
+int fr_export_unique_device(fr_ctx* ctx, void* dev_keys, void* dev_counts, void* dev_first, uint64_t cap);
+int fr_merge_unique_device(fr_ctx* ctx, const void* dev_keys, const void* dev_counts, const void* dev_first,
+                           uint64_t n);
+
+/* ---- device memory + SYN-v1 generator (bench and tests) --------------------------- */
+void* fr_device_alloc(fr_ctx* ctx, uint64_t bytes);
+int fr_device_free(fr_ctx* ctx, void* ptr);
+int fr_copy_to_host(fr_ctx* ctx, void* dst, const void* dev_src, uint64_t bytes);
+int fr_copy_to_device(fr_ctx* ctx, void* dev_dst, const void* src, uint64_t bytes);
+/* records r0..r0+n-1 of SYN-v1 (frender_amd/synth.py) into dev_out; idx ascii S*L */
+int fr_synth_device(fr_ctx* ctx, uint8_t* dev_out, uint64_t r0, uint64_t n, int R, uint64_t seed,
+                    const char* idx1_ascii, const char* idx2_ascii, int S, int L1, int L2);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

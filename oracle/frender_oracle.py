@@ -163,12 +163,8 @@ def code_of(line: str) -> str:
     return line.split(" ")[1].split(":")[-1]
 
 
-def tally_file(path, sample=None):
-    """R1-R4 for one file -> (basename, {code: count} in first-occurrence order, records)."""
-    name = os.path.basename(str(path))
-    print(f"Tallying barcodes from {name}...", end="")
-    with gzip.open(path, "rb") as g:
-        text = g.read().decode("utf-8")
+def tally_text(text: str, sample=None):
+    """R1-R4 on decoded text -> ({code: count} in first-occurrence order, records)."""
     counts: dict = {}
     records = 0
     for line in header_lines(text):
@@ -177,6 +173,16 @@ def tally_file(path, sample=None):
         records += 1
         code = code_of(line)
         counts[code] = counts.get(code, 0) + 1
+    return counts, records
+
+
+def tally_file(path, sample=None):
+    """R1-R4 for one file -> (basename, {code: count} in first-occurrence order, records)."""
+    name = os.path.basename(str(path))
+    print(f"Tallying barcodes from {name}...", end="")
+    with gzip.open(path, "rb") as g:
+        text = g.read().decode("utf-8")
+    counts, records = tally_text(text, sample)
     new = len(counts)
     print(f"found {new} new barcode{'' if new == 1 else 's'} in {records} reads.")
     return name, counts, records

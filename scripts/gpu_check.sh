@@ -1,0 +1,32 @@
+#!/bin/bash
+# On-box check: GPU parity tests, a short bench, and a rocprofv3 kernel-trace of the bench.
+# Every GPU step has its own time limit; a crash/timeout ends the script.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+STAGE=${1:-all}
+rc=0
+if [[ $STAGE == all || $STAGE == test ]]; then
+  timeout -k 10 900 python -m pytest tests -m gpu -q --maxfail=15 --timeout=600 -p no:cacheprovider \
+      > gpurun_out/pytest_gpu.log 2>&1
+  rc=$?
+  tail -30 gpurun_out/pytest_gpu.log
+  echo "pytest exit $rc"
+  if [[ $rc -ne 0 && $rc -ne 1 ]]; then exit $rc; fi
+fi
+if [[ $STAGE == all || $STAGE == bench ]]; then
+  timeout -k 10 400 python bench.py --steps 5 --warmup 2 ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1
+  b=$?; tail -5 gpurun_out/bench.log; echo "bench exit $b"
+  if [[ $b -ne 0 ]]; then exit $b; fi
+fi
+if [[ $STAGE == all || $STAGE == prof ]]; then
+  cd /tmp
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run \
+      --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 5 --warmup 1 --no-cpu \
+      > "$GRAFT_REPO_ROOT/gpurun_out/prof.log" 2>&1
+  p=$?; tail -3 "$GRAFT_REPO_ROOT/gpurun_out/prof.log"; echo "prof exit $p"
+  cd "$GRAFT_REPO_ROOT"
+  find gpurun_out/prof -name "*kernel_stats.csv" -exec head -20 {} \;
+fi
+exit $rc

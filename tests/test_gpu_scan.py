@@ -1,0 +1,254 @@
+"""GPU parity: the HIP scan path (through the C ABI) against the CPU oracle and the
+reference's golden vectors.  Bit-exact everywhere: this is integer/byte work."""
+import random
+
+import numpy as np
+import pytest
+
+from harness import case_names, run_case
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from frender_amd import _lib
+    return _lib
+
+
+@pytest.fixture(scope="module")
+def ctx(lib):
+    c = lib.Context(device=0, chunk_bytes=1 << 20, table_slots=1 << 16)
+    yield c
+    c.close()
+
+
+def gpu_tally(ctx, lib, files, sample=None, mode="host", pieces=None, rng=None):
+    """Tally fast-alphabet inputs on the GPU -> ({code: count} in order, [records])."""
+    ctx.reset()
+    recs = []
+    for data in files:
+        ctx.begin_file(sample)
+        if mode == "device":
+            p = ctx.device_alloc(len(data) + 16)
+            try:
+                if data:
+                    ctx.copy_to_device(p, data)
+                ctx.feed_device(p, len(data))
+                st = ctx.end_file()
+            finally:
+                ctx.device_free(p)
+        else:
+            pos = 0
+            while pos < len(data):
+                n = pieces(rng) if pieces else len(data)
+                if ctx.feed(data[pos:pos + n]):
+                    break
+                pos += n
+            st = ctx.end_file()
+        assert st.error == 0 and st.exotic == 0
+        recs.append(int(st.records))
+    ctx.finalize()
+    keys, counts, first = ctx.unique()
+    assert np.all(np.diff(first.astype(np.float64)) > 0)
+    return dict(zip(lib.decode_keys(keys), counts.tolist())), recs
+
+
+def oracle_tally(files, sample=None):
+    from oracle.frender_oracle import tally_text
+    total, recs = {}, []
+    for data in files:
+        c, r = tally_text(data.decode(), sample)
+        for k, v in c.items():
+            total[k] = total.get(k, 0) + v
+        recs.append(r)
+    return total, recs
+
+
+def assert_same(got, exp):
+    assert got[1] == exp[1], ("records", got[1], exp[1])
+    assert list(got[0].items()) == list(exp[0].items())
+
+
+# ---------------------------------------------------------------------------------------
+# golden vectors produced by the reference itself
+# ---------------------------------------------------------------------------------------
+@pytest.mark.parametrize("name", case_names())
+def test_golden_case_on_gpu(name):
+    from frender_amd import scan
+    diffs = run_case(name, scan.frender_scan)
+    assert not diffs, "\n".join(diffs)
+
+
+# ---------------------------------------------------------------------------------------
+# synthetic generator: device == host
+# ---------------------------------------------------------------------------------------
+@pytest.mark.parametrize("L,R", [(8, 8), (10, 150)])
+def test_device_synth_matches_host(ctx, L, R):
+    from frender_amd import synth
+    sheet = synth.make_sheet(96, L, L)
+    n, r0 = 3000, 123_456_789
+    want = synth.generate_bytes(sheet, r0, n, R=R, seed=5)
+    p = ctx.device_alloc(len(want))
+    try:
+        ctx.synth_device(p, r0, n, R, 5, sheet.idx1, sheet.idx2)
+        assert ctx.copy_to_host(p, len(want)) == want
+    finally:
+        ctx.device_free(p)
+
+
+# ---------------------------------------------------------------------------------------
+# tally parity on random inputs (look-back across many tiles and launches)
+# ---------------------------------------------------------------------------------------
+def random_fastq(rng, n, long_every=0, styles=("\n", "\r\n", "\r"), blank_seq=False):
+    out = []
+    alphabet = "ACGTN"
+    for i in range(n):
+        nl = rng.choice(styles)
+        a = "".join(rng.choice(alphabet) for _ in range(rng.randint(1, 10)))
+        b = "".join(rng.choice(alphabet) for _ in range(rng.randint(0, 10)))
+        code = a + "+" + b if rng.random() < 0.95 else a
+        pre = "@r%d:%s" % (i, "x" * (700 if long_every and i % long_every == 0 else rng.randint(0, 30)))
+        tag = rng.choice(["1:N:0:", "", "2:Y:18:", "::"])
+        tail = rng.choice(["", " more:stuff", " x"])
+        seq = "" if blank_seq and rng.random() < 0.2 else "ACGT" * rng.randint(0, 40)
+        out.append(f"{pre} {tag}{code}{tail}{nl}{seq}{nl}+{nl}{'F' * len(seq)}{nl}")
+    return "".join(out).encode()
+
+
+@pytest.mark.parametrize("mode", ["host", "device"])
+@pytest.mark.parametrize("seed", [1, 2])
+def test_random_fastq_tally(ctx, lib, mode, seed):
+    rng = random.Random(seed)
+    files = [random_fastq(rng, 20000, long_every=997, blank_seq=True), random_fastq(rng, 5000, styles=("\r\n",)),
+             b"", random_fastq(rng, 1)]
+    got = gpu_tally(ctx, lib, files, mode=mode, pieces=lambda r: r.choice([1, 7, 4096, 70000, 1 << 20]), rng=rng)
+    assert_same(got, oracle_tally(files))
+
+
+@pytest.mark.parametrize("sample", [1, 3, 1000, 19999, 50000])
+@pytest.mark.parametrize("mode", ["host", "device"])
+def test_sample_limit(ctx, lib, sample, mode):
+    rng = random.Random(sample)
+    files = [random_fastq(rng, 20000), random_fastq(rng, 300)]
+    got = gpu_tally(ctx, lib, files, sample=sample, mode=mode, pieces=lambda r: 65536, rng=rng)
+    assert_same(got, oracle_tally(files, sample))
+
+
+def test_no_trailing_newline_and_truncated(ctx, lib):
+    rng = random.Random(9)
+    base = random_fastq(rng, 50)
+    files = [base[:-1], base + b"@last 1:N:0:ACGT+TTTT", base + b"@last 1:N:0:ACGT+TTTT\nAC\n", b"\n\n\n\n"[:0]]
+    for mode in ("host", "device"):
+        assert_same(gpu_tally(ctx, lib, files, mode=mode), oracle_tally(files))
+
+
+def test_table_growth_and_overflow(lib):
+    """Start from a 1024-slot table with ~60k distinct codes: the table must grow
+    between launches (overflow list absorbs in-flight inserts) and stay exact."""
+    from frender_amd import synth
+    c = lib.Context(device=0, chunk_bytes=1 << 18, table_slots=1024)
+    try:
+        rng = np.random.default_rng(3)
+        n = 60000
+        codes = ["".join("ACGT"[x] for x in rng.integers(0, 4, 8)) + "+" + "".join("ACGT"[x] for x in rng.integers(0, 4, 8))
+                 for _ in range(n)]
+        data = "".join(f"@r{i} 1:N:0:{cd}\nA\n+\nF\n" for i, cd in enumerate(codes + codes[: n // 3])).encode()
+        for mode in ("host", "device"):
+            assert_same(gpu_tally(c, lib, [data], mode=mode), oracle_tally([data]))
+        sheet = synth.make_sheet(4, 8, 8)
+        big = synth.generate_bytes(sheet, 0, 200000, R=8, seed=11)
+        assert_same(gpu_tally(c, lib, [big, data], mode="device"), oracle_tally([big, data]))
+    finally:
+        c.close()
+
+
+def test_synthetic_device_scale(lib):
+    """A 2M-read SYN-v1 file generated and scanned in HBM (1 MiB launches) vs the oracle."""
+    from frender_amd import synth
+    from oracle.frender_oracle import tally_text
+    c = lib.Context(device=0, chunk_bytes=1 << 20, table_slots=1 << 20)
+    try:
+        sheet = synth.make_sheet(96, 8, 8)
+        n = 2_000_000
+        host = synth.generate_bytes(sheet, 0, n, R=8, seed=1)
+        p = c.device_alloc(len(host))
+        c.synth_device(p, 0, n, 8, 1, sheet.idx1, sheet.idx2)
+        c.reset()
+        c.begin_file(None)
+        c.feed_device(p, len(host))
+        st = c.end_file()
+        c.device_free(p)
+        assert st.records == n and st.error == 0
+        c.finalize()
+        keys, counts, first = c.unique()
+        got = dict(zip(lib.decode_keys(keys), counts.tolist()))
+        exp, recs = tally_text(host.decode())
+        assert recs == n
+        assert list(got.items()) == list(exp.items())
+        assert int(counts.sum()) == n
+    finally:
+        c.close()
+
+
+# ---------------------------------------------------------------------------------------
+# classification parity (packed Hamming vs the oracle's string Hamming)
+# ---------------------------------------------------------------------------------------
+@pytest.mark.parametrize("nsubs", [-1, 0, 1, 2, 3, 9])
+@pytest.mark.parametrize("rc", [False, True])
+def test_classify_random(ctx, lib, nsubs, rc):
+    from frender_amd import synth
+    from frender_amd.scan import _sheet_names
+    from frender_amd.host import reverse_complement
+    from oracle.frender_oracle import classify_code
+    rng = random.Random(nsubs * 7 + rc)
+    sheet = synth.make_sheet(24, 8, 8, seed=5, combinatorial=(6, 4) if nsubs % 2 else None)
+    ids = list(sheet.ids)
+    ids[5] = ids[3]  # a duplicated name
+    idx1, idx2 = list(sheet.idx1), list(sheet.idx2)
+    idx2[7] = idx2[7].lower()
+    idx2[8] = reverse_complement(idx2[2])
+    codes = []
+    for _ in range(3000):
+        s = rng.randrange(len(idx1))
+        a = list(idx1[s].upper())
+        b = list((idx2[rng.randrange(len(idx1))] if rng.random() < 0.3 else idx2[s]).upper())
+        if rng.random() < 0.2:
+            b = list(reverse_complement("".join(b)))
+        for arr in (a, b):
+            for _ in range(rng.randint(0, 3)):
+                arr[rng.randrange(8)] = rng.choice("ACGTN")
+        codes.append("".join(a) + "+" + "".join(b))
+    codes = list(dict.fromkeys(codes))
+    data = "".join(f"@r{i} 1:N:0:{c}\n\n+\n\n" for i, c in enumerate(codes)).encode()
+    ctx.reset()
+    ctx.begin_file(None)
+    ctx.feed(data)
+    ctx.end_file()
+    ctx.finalize()
+    keys, counts, _ = ctx.unique()
+    assert lib.decode_keys(keys) == codes
+    names, nid = _sheet_names(ids)
+    ctx.set_sheet(idx1, idx2, [reverse_complement(x) for x in idx2], nid, len(names))
+    out = ctx.classify(nsubs, rc)
+    assert out["err_unique"] == -1
+    f_exp = {n: 0 for n in names}
+    r_exp = {n: 0 for n in names}
+    for j, code in enumerate(codes):
+        e = classify_code(code, 1, idx1, idx2, ids, nsubs, rc)
+        got_t = lib.CLASS_NAMES[out["cls"][j]]
+        assert got_t == e["read_type"], (code, got_t, e)
+        assert (idx1[out["m1"][j]] if out["m1"][j] >= 0 else "") == e["matched_idx1"] or rc
+        assert (idx2[out["m2"][j]] if out["m2"][j] >= 0 else "") == e["matched_idx2"]
+        assert (ids[out["row"][j]] if out["row"][j] >= 0 else "") == e["sample_name"]
+        if rc:
+            assert lib.CLASS_NAMES[out["rc_cls"][j]] == e["rc_read_type"]
+            assert (ids[out["rc_row"][j]] if out["rc_row"][j] >= 0 else "") == e["rc_sample_name"]
+            if e["sample_name"]:
+                f_exp[e["sample_name"]] += 1
+            if e["rc_sample_name"]:
+                r_exp[e["rc_sample_name"]] += 1
+    if rc:
+        f, r = ctx.rc_counts()
+        assert f.tolist() == [f_exp[n] for n in names]
+        assert r.tolist() == [r_exp[n] for n in names]

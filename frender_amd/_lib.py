@@ -56,6 +56,7 @@ _SIGS = {
     "fr_last_error": (C.c_char_p, [P]),
     "fr_get_timing": (C.c_int, [P, C.POINTER(Timing)]),
     "fr_sync": (C.c_int, [P]),
+    "fr_get_diag": (C.c_int, [P, P, C.c_int]),
     "fr_set_sheet": (C.c_int, [P, C.c_int, P, P, P, P, P, P, C.c_int, P, P, P, C.c_int]),
     "fr_reset": (C.c_int, [P]),
     "fr_begin_file": (C.c_int, [P, C.c_int64]),
@@ -65,7 +66,7 @@ _SIGS = {
     "fr_finalize": (C.c_int, [P, u64p, u64p, u64p]),
     "fr_get_unique": (C.c_int, [P, P, P, P]),
     "fr_get_presence": (C.c_int, [P, P, P]),
-    "fr_get_exotic": (C.c_int, [P, P, P, P, P, C.c_uint64]),
+    "fr_get_exotic": (C.c_int, [P, C.c_uint64, C.c_uint64, P, P, P, P, C.c_uint64, u64p]),
     "fr_classify": (C.c_int, [P, C.c_int, C.c_int, P, P, P, P, P, P, P, P, P]),
     "fr_rc_counts": (C.c_int, [P, P, P]),
     "fr_classify_cp": (C.c_int, [P, C.c_int, P, P, P, P, C.c_int, C.c_int, C.c_int, P, P, P, P, P, P, P, P]),
@@ -209,16 +210,21 @@ class Context:
         self._ck(lib.fr_get_presence(self.h, _ptr(u), _ptr(f)), "fr_get_presence")
         return u, f
 
-    def exotic(self):
-        n = self.NE
-        ords = np.empty(n, dtype=np.uint64)
-        lens = np.empty(n, dtype=np.uint32)
-        offs = np.empty(n, dtype=np.uint64)
-        self._ck(lib.fr_get_exotic(self.h, _ptr(ords), _ptr(lens), _ptr(offs), None, 0), "fr_get_exotic")
-        pool_bytes = int((offs + lens).max()) if n else 0
+    def exotic(self, first: int, count: int):
+        """Exotic records [first, first+count): (ordinals, lengths, pool offsets, pool)."""
+        ords = np.empty(count, dtype=np.uint64)
+        lens = np.empty(count, dtype=np.uint32)
+        offs = np.empty(count, dtype=np.uint64)
+        got = C.c_uint64()
+        self._ck(lib.fr_get_exotic(self.h, first, count, _ptr(ords), _ptr(lens), _ptr(offs), None, 0,
+                                   C.byref(got)), "fr_get_exotic")
+        k = got.value
+        ords, lens, offs = ords[:k], lens[:k], offs[:k]
+        pool_bytes = int((offs + lens).max()) if k else 0
         pool = np.empty(max(pool_bytes, 1), dtype=np.uint8)
-        self._ck(lib.fr_get_exotic(self.h, _ptr(ords), _ptr(lens), _ptr(offs), _ptr(pool), pool_bytes),
-                 "fr_get_exotic")
+        if pool_bytes:
+            self._ck(lib.fr_get_exotic(self.h, first, 0, None, None, None, _ptr(pool), pool_bytes, None),
+                     "fr_get_exotic")
         return ords, lens, offs, pool
 
     # ---- classify -------------------------------------------------------------------
@@ -289,6 +295,16 @@ class Context:
         t = Timing()
         self._ck(lib.fr_get_timing(self.h, C.byref(t)), "fr_get_timing")
         return t
+
+    def diag(self) -> dict:
+        v = np.zeros(16, dtype=np.uint64)
+        self._ck(lib.fr_get_diag(self.h, _ptr(v), 16), "fr_get_diag")
+        d = dict(zip(("spin_max", "spin_total", "keys", "overflow", "presence", "exotic", "grid", "slots"),
+                     v[:8].tolist()))
+        if v[8:].any():  # FR_STAMPS build: cycles per phase summed over workgroups
+            d["stamps"] = dict(zip(("lookback", "barrier", "headers", "parse", "stage", "count", "flush",
+                                    "prologue"), v[8:].tolist()))
+        return d
 
     def sync(self):
         self._ck(lib.fr_sync(self.h), "fr_sync")

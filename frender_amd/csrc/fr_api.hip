@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -22,6 +23,8 @@ struct fr_ctx {
     hipStream_t copy = nullptr;    // H2D of host feeds
     std::string err;
     int grid = 0;
+    u32 flush_at = NS * 3 / 4;
+    u32 ablate = 0;
 
     DevState* st = nullptr;
     DevState* h_st = nullptr;      // pinned snapshot
@@ -171,20 +174,25 @@ static int grow_table(fr_ctx* ctx, bool force_bigger) {
         CK(hipStreamSynchronize(ctx->stream));
         CK(hipFree(old));
     }
-    // presence list: keep at least half free
-    rc = read_state(ctx);
+    return FR_OK;
+}
+
+// the presence list must take one more entry per live key (appended by the per-file scan)
+static int ensure_presence_cap(fr_ctx* ctx) {
+    int rc = read_state(ctx);
     if (rc) return rc;
-    if (ctx->h_st->n_presence * 2 > ctx->tab.pres_cap) {
-        const u64 ncap = ctx->tab.pres_cap * 4;
-        Presence* np = nullptr;
-        CK(dalloc(&np, ncap));
-        CK(hipMemcpyAsync(np, ctx->tab.pres, std::min(ctx->h_st->n_presence, ctx->tab.pres_cap) * sizeof(Presence),
-                          hipMemcpyDeviceToDevice, ctx->stream));
-        CK(hipStreamSynchronize(ctx->stream));
-        CK(hipFree(ctx->tab.pres));
-        ctx->tab.pres = np;
-        ctx->tab.pres_cap = ncap;
-    }
+    const u64 need = ctx->h_st->n_presence + ctx->h_st->n_keys + 1024;
+    if (need <= ctx->tab.pres_cap) return FR_OK;
+    u64 ncap = ctx->tab.pres_cap;
+    while (ncap < need * 2) ncap *= 2;
+    Presence* np = nullptr;
+    CK(dalloc(&np, ncap));
+    CK(hipMemcpyAsync(np, ctx->tab.pres, std::min(ctx->h_st->n_presence, ctx->tab.pres_cap) * sizeof(Presence),
+                      hipMemcpyDeviceToDevice, ctx->stream));
+    CK(hipStreamSynchronize(ctx->stream));
+    CK(hipFree(ctx->tab.pres));
+    ctx->tab.pres = np;
+    ctx->tab.pres_cap = ncap;
     return FR_OK;
 }
 
@@ -194,7 +202,7 @@ static int maybe_grow(fr_ctx* ctx) {
     if (hipEventQuery(ctx->st_ev) != hipSuccess) return FR_OK;
     ctx->st_pending = false;
     const DevState& s = *ctx->h_st;
-    if (s.n_overflow || s.n_keys * 2 > ctx->nslots || s.n_presence * 2 > ctx->tab.pres_cap) return grow_table(ctx, false);
+    if (s.n_overflow || s.n_keys * 2 > ctx->nslots) return grow_table(ctx, false);
     return FR_OK;
 }
 
@@ -222,6 +230,8 @@ static int launch_range(fr_ctx* ctx, const u8* dptr, u64 len, u64 avail, int own
     a.own_start = own_start;
     a.own_end = own_end;
     a.pre_valid = pre_valid;
+    a.flush_at = ctx->flush_at;
+    a.ablate = ctx->ablate;
     a.max_records = ctx->max_records;
     a.st = ctx->st;
     a.tiles = ctx->tiles;
@@ -269,6 +279,9 @@ fr_ctx* fr_create(int device, uint64_t chunk_bytes, uint64_t table_slots) {
     if ((e = hipGetDeviceProperties(&prop, device)) != hipSuccess) return bad("props", e);
     const int per_cu = 2;  // LDS-bound: ~58 KB per workgroup -> 2 per CU
     ctx->grid = prop.multiProcessorCount * per_cu;
+    if (const char* g = getenv("FR_GRID")) ctx->grid = std::max(1, atoi(g));
+    if (const char* f = getenv("FR_FLUSH_AT")) ctx->flush_at = (u32)atoi(f);
+    if (const char* f = getenv("FR_ABLATE")) ctx->ablate = (u32)atoi(f);
 
     ctx->chunk_bytes = chunk_bytes ? ((chunk_bytes + TILE - 1) / TILE) * TILE : (256ull << 20);
     if (ctx->chunk_bytes > RANGE_MAX) ctx->chunk_bytes = RANGE_MAX;
@@ -336,6 +349,17 @@ void fr_destroy(fr_ctx* ctx) {
 }
 
 const char* fr_last_error(const fr_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int fr_get_diag(fr_ctx* ctx, uint64_t* out, int n) {
+    int rc = read_state(ctx);
+    if (rc) return rc;
+    const DevState& s = *ctx->h_st;
+    const uint64_t v[] = {s.spin_max,   s.spin_total, s.n_keys,   s.n_overflow, s.n_presence, s.n_exotic,
+                          (uint64_t)ctx->grid, ctx->nslots, s.stamp[0], s.stamp[1], s.stamp[2], s.stamp[3],
+                          s.stamp[4],  s.stamp[5],  s.stamp[6], s.stamp[7]};
+    for (int i = 0; i < n && i < (int)(sizeof(v) / sizeof(v[0])); ++i) out[i] = v[i];
+    return FR_OK;
+}
 
 int fr_sync(fr_ctx* ctx) {
     CK(hipStreamSynchronize(ctx->stream));
@@ -546,6 +570,10 @@ int fr_end_file(fr_ctx* ctx, fr_file_stats* out) {
     CK(hipStreamSynchronize(ctx->copy));
     int rc = grow_table(ctx, false);  // re-inserts any overflow; exact state afterwards
     if (rc) return rc;
+    rc = ensure_presence_cap(ctx);
+    if (rc) return rc;
+    CK(launch_presence_scan(ctx->tab.slots, ctx->nslots, ctx->file_tag, ctx->tab.pres, ctx->tab.pres_cap, ctx->st,
+                            ctx->stream));
     rc = read_state(ctx);
     if (rc) return rc;
     const DevState& s = *ctx->h_st;
@@ -664,15 +692,20 @@ int fr_get_presence(fr_ctx* ctx, uint32_t* unique_idx, uint32_t* file_idx) {
     return FR_OK;
 }
 
-int fr_get_exotic(fr_ctx* ctx, uint64_t* ordinal, uint32_t* length, uint64_t* pool_offset, uint8_t* pool,
-                  uint64_t pool_bytes) {
-    const u64 n = ctx->n_exo;
-    if (!n) return FR_OK;
-    CK(hipMemcpy(ordinal, ctx->tab.exo_ord, n * 8, hipMemcpyDeviceToHost));
-    CK(hipMemcpy(length, ctx->tab.exo_len, n * 4, hipMemcpyDeviceToHost));
-    CK(hipMemcpy(pool_offset, ctx->tab.exo_off, n * 8, hipMemcpyDeviceToHost));
-    const u64 used = std::min<u64>(ctx->h_st->exo_pool_used, ctx->tab.exo_pool_cap);
-    if (pool && pool_bytes) CK(hipMemcpy(pool, ctx->tab.exo_pool, std::min(used, pool_bytes), hipMemcpyDeviceToHost));
+int fr_get_exotic(fr_ctx* ctx, uint64_t first, uint64_t count, uint64_t* ordinal, uint32_t* length,
+                  uint64_t* pool_offset, uint8_t* pool, uint64_t pool_bytes, uint64_t* written) {
+    const u64 have = ctx->n_exo;
+    const u64 n = first < have ? std::min<u64>(count, have - first) : 0;
+    if (written) *written = n;
+    if (n) {
+        if (ordinal) CK(hipMemcpy(ordinal, ctx->tab.exo_ord + first, n * 8, hipMemcpyDeviceToHost));
+        if (length) CK(hipMemcpy(length, ctx->tab.exo_len + first, n * 4, hipMemcpyDeviceToHost));
+        if (pool_offset) CK(hipMemcpy(pool_offset, ctx->tab.exo_off + first, n * 8, hipMemcpyDeviceToHost));
+    }
+    if (pool && pool_bytes) {
+        const u64 used = std::min<u64>(ctx->h_st->exo_pool_used, ctx->tab.exo_pool_cap);
+        CK(hipMemcpy(pool, ctx->tab.exo_pool, std::min(used, pool_bytes), hipMemcpyDeviceToHost));
+    }
     return FR_OK;
 }
 

@@ -59,7 +59,9 @@ struct DevState {
     u32 nonascii;        // a byte >= 0x80 was seen in the current file
     u32 utf8_bad;
     u32 cap_flags;       // 1 presence, 2 overflow list, 4 exotic pool
-    u32 pad;
+    u32 spin_max;        // diagnostics: longest look-back wait (polls)
+    u64 spin_total;      // diagnostics: total look-back polls that found a window not ready
+    u64 stamp[8];        // diagnostics (FR_STAMPS builds only): per-phase shader cycles, summed over workgroups
 };
 
 struct Table {
@@ -89,8 +91,10 @@ struct ScanArgs {
     int own_start;       // position 0 is a line start handled by this launch
     int own_end;         // a line start at position len is handled by this launch
     int pre_valid;       // buf[-16..-1] readable (device-split ranges)
-    int pad;
+    u32 flush_at;        // LDS table key cap: past it, new codes go to the HBM table directly
     i64 max_records;     // -s, <= 0: none
+    u32 ablate;          // timing ablation bits (FR_ABLATE; 0 in production): 1 parse, 2 encode, 4 insert
+    u32 pad2;
     DevState* st;
     u64* tiles;          // look-back descriptors
     Table tab;
@@ -153,6 +157,8 @@ hipError_t launch_classify_cp(int n, const u32* q1, const int32_t* q1len, const 
                               int stride, int S, const u32* s1, const int32_t* s1len, const u32* s2,
                               const int32_t* s2len, const u32* s2rc, const int32_t* name, int nsubs, int rc,
                               ClassOut o, hipStream_t s);
+hipError_t launch_presence_scan(const GSlot* slots, u64 n, u32 tag, Presence* pres, u64 cap, DevState* st,
+                                hipStream_t s);
 hipError_t launch_merge(Table t, DevState* st, const u64* keys, const u64* counts, const u64* first, u64 n,
                         hipStream_t s);
 hipError_t launch_synth(u8* out, u64 r0, u64 n, int R, u64 seed, const u8* idx1, const u8* idx2, int S, int L1,

@@ -60,36 +60,34 @@ __device__ __forceinline__ u64 wave_sum_u64(u64 v) {
 }
 
 // ------------------------------------------------------------------------------------
-// HBM table insert (count add, first-occurrence min, per-file presence)
+// HBM table insert: count add, first-occurrence min, last file tag (presence is derived per
+// file by presence_scan_kernel).  One 32-B slot load decides; the count add is
+// fire-and-forget and the min/max atomics run only when they can change the slot (a stale
+// load only ever over-estimates `first` / under-estimates `last_tag`, so skipping is safe).
+// Returns true when this call created the slot.  No global counters are touched here.
 // ------------------------------------------------------------------------------------
-__device__ void global_insert(const Table& T, DevState* st, u64 key, u64 cnt, u64 ord, u32 tag) {
+__device__ bool global_insert(const Table& T, DevState* st, u64 key, u64 cnt, u64 ord, u32 tag) {
     u64 h = mix64(key) & T.mask;
     for (int probe = 0; probe < GPROBE; ++probe) {
         GSlot* s = &T.slots[h];
-        u64 k = agent_load(&s->key);
+        const uint4 w0 = *(const uint4*)s;
+        const uint4 w1 = *((const uint4*)s + 1);
+        u64 k = ((u64)w0.y << 32) | w0.x;
+        u64 first = ((u64)w1.y << 32) | w1.x;
+        u32 ltag = w1.z;
+        bool created = false;
         if (k == 0) {
             const u64 old = atomicCAS((unsigned long long*)&s->key, 0ull, (unsigned long long)key);
-            if (old == 0) {
-                atomicAdd((unsigned long long*)&st->n_keys, 1ull);
-                k = key;
-            } else {
-                k = old;
-            }
+            created = old == 0;
+            k = created ? key : old;
+            first = ~0ull;
+            ltag = 0;
         }
         if (k == key) {
             atomicAdd((unsigned long long*)&s->count, (unsigned long long)cnt);
-            atomicMin((unsigned long long*)&s->first, (unsigned long long)ord);
-            const u32 prev = atomicMax(&s->last_tag, tag);
-            if (prev < tag) {
-                const u64 i = atomicAdd((unsigned long long*)&st->n_presence, 1ull);
-                if (i < T.pres_cap) {
-                    T.pres[i].key = key;
-                    T.pres[i].tag = tag;
-                } else {
-                    atomicOr(&st->cap_flags, 1u);
-                }
-            }
-            return;
+            if (ord < first) atomicMin((unsigned long long*)&s->first, (unsigned long long)ord);
+            if (ltag < tag) atomicMax(&s->last_tag, tag);
+            return created;
         }
         h = (h + 1) & T.mask;
     }
@@ -105,13 +103,22 @@ __device__ void global_insert(const Table& T, DevState* st, u64 key, u64 cnt, u6
     } else {
         atomicOr(&st->cap_flags, 2u);
     }
+    return false;
+}
+
+// block-wide count of created slots -> one global add per wave
+__device__ __forceinline__ void add_created(DevState* st, u32 mine) {
+    u64 v = mine;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd((unsigned long long*)&st->n_keys, (unsigned long long)v);
 }
 
 // ------------------------------------------------------------------------------------
 // the tally kernel
 // ------------------------------------------------------------------------------------
 struct ScanShared {
-    u8 buf[16 + TILE + HALO];        // [0,16) = the 16 bytes before the tile (UTF-8 look-back)
+    u8 buf[16 + TILE + HALO + 32];   // [0,16) = the 16 bytes before the tile; +32 pad for word reads
     u16 hdr[TILE / 4 + 4];
     u64 key[NS];
     u32 cnt[NS];
@@ -119,8 +126,10 @@ struct ScanShared {
     u32 wsum[WG / 64];
     u64 tile_excl;
     u32 tile;
+    u32 next;
     u32 nhdr;
-    u32 nkeys;
+    u32 nkeys;        // occupied LDS slots
+    u32 created;      // HBM slots this workgroup created (added to n_keys once, at exit)
     u32 flags;
 };
 
@@ -132,7 +141,8 @@ __device__ void lds_flush(ScanShared& sh, const ScanArgs& a) {
     for (int i = threadIdx.x; i < NS; i += WG) {
         const u64 k = sh.key[i];
         if (k) {
-            global_insert(a.tab, a.st, k, sh.cnt[i], make_ord(a, sh.mino[i]), a.file_tag);
+            if (global_insert(a.tab, a.st, k, sh.cnt[i], make_ord(a, sh.mino[i]), a.file_tag))
+                atomicAdd(&sh.created, 1u);
             sh.key[i] = 0;
             sh.cnt[i] = 0;
             sh.mino[i] = 0xFFFFFFFFu;
@@ -145,6 +155,9 @@ __device__ __forceinline__ void lds_insert(ScanShared& sh, const ScanArgs& a, u6
     for (int pr = 0; pr < LPROBE; ++pr) {
         u64 k = *(volatile u64*)&sh.key[h];
         if (k == 0) {
+            // a full LDS table stops claiming slots: the code goes to HBM directly; the
+            // codes already resident (the hot ones arrive first) keep aggregating here
+            if (*(volatile u32*)&sh.nkeys >= a.flush_at) break;
             const u64 old = atomicCAS((unsigned long long*)&sh.key[h], 0ull, (unsigned long long)key);
             if (old == 0) {
                 atomicAdd(&sh.nkeys, 1u);
@@ -160,46 +173,69 @@ __device__ __forceinline__ void lds_insert(ScanShared& sh, const ScanArgs& a, u6
         }
         h = (h + 1) & (NS - 1);
     }
-    global_insert(a.tab, a.st, key, 1, make_ord(a, off), a.file_tag);
+    if (global_insert(a.tab, a.st, key, 1, make_ord(a, off), a.file_tag)) atomicAdd(&sh.created, 1u);
 }
 
-// Decoupled look-back over the launch's tile descriptors: returns the number of line
-// terminators in tiles [0, t) of this range.  Descriptor = {tag = 2*epoch + inclusive, value}.
+// Decoupled look-back over the launch's tile descriptors {tag = 2*epoch + inclusive, value}.
+// The tile's own aggregate was published when it was staged (count_tile); this resolves its
+// exclusive prefix, reading 256 predecessors per poll (4 per lane), and publishes the
+// inclusive prefix.  Returns the number of line terminators in tiles [0, t) of the range.
 __device__ u64 lookback(const ScanArgs& a, u32 t, u32 agg, int lane) {
-    const u64 tagA = (u64)(2u * a.epoch) << 32;
+    if (t == 0) return 0;  // tile 0 published its inclusive value directly
     const u64 tagI = (u64)(2u * a.epoch + 1u) << 32;
-    if (t == 0) {
-        if (lane == 0) agent_store(&a.tiles[0], tagI | agg);
-        return 0;
-    }
-    if (lane == 0) agent_store(&a.tiles[t], tagA | agg);
     u64 excl = 0;
     i64 j = (i64)t - 1;
     u32 spins = 0;
     for (;;) {
-        const i64 idx = j - lane;
-        const u64 s = idx >= 0 ? agent_load(&a.tiles[idx]) : tagI;
-        const u32 tag = (u32)(s >> 32);
-        const bool ready = (tag >> 1) == a.epoch;
-        if (!__all(ready)) {
+        u64 sv[4], rdy[4], inc[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const i64 idx = j - 64 * k - lane;
+            sv[k] = idx >= 0 ? agent_load(&a.tiles[idx]) : tagI;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const u32 tag = (u32)(sv[k] >> 32);
+            const bool ready = (tag >> 1) == a.epoch;
+            rdy[k] = __ballot(ready);
+            inc[k] = __ballot(ready && (tag & 1u));
+        }
+        int kf = 4, lf = 63;
+#pragma unroll
+        for (int k = 3; k >= 0; --k)
+            if (inc[k]) {
+                kf = k;
+                lf = __ffsll((long long)inc[k]) - 1;
+            }
+        bool ok = true;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const u64 need = k < kf ? ~0ull : k == kf ? (lf == 63 ? ~0ull : ((1ull << (lf + 1)) - 1ull)) : 0ull;
+            ok &= (rdy[k] & need) == need;
+        }
+        if (!ok) {
             if (++spins > SPIN_MAX) {
                 if (lane == 0) atomicOr(&a.st->spin_fail, 1u);
                 return 0;
             }
-            __builtin_amdgcn_s_sleep(1);
+            if (spins > 2) __builtin_amdgcn_s_sleep(1);
             continue;
         }
-        const u64 inc = __ballot(tag & 1u);
-        const u32 v = (u32)s;
-        if (inc) {
-            const int first = __ffsll((long long)inc) - 1;
-            excl += wave_sum_u64(lane <= first ? (u64)v : 0ull);
-            break;
-        }
-        excl += wave_sum_u64((u64)v);
-        j -= 64;
+        u64 contrib = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (k < kf || (k == kf && lane <= lf)) contrib += (u32)sv[k];
+        excl += wave_sum_u64(contrib);
+        if (kf < 4) break;
+        j -= 256;
     }
-    if (lane == 0) agent_store(&a.tiles[t], tagI | (u64)(u32)(excl + agg));
+    if (lane == 0) {
+        agent_store(&a.tiles[t], tagI | (u64)(u32)(excl + agg));
+        if (spins) {
+            atomicMax(&a.st->spin_max, spins);
+            atomicAdd((unsigned long long*)&a.st->spin_total, (unsigned long long)spins);
+        }
+    }
     return excl;
 }
 
@@ -243,61 +279,278 @@ __device__ bool utf8_segment_ok(const ScanShared& sh, int s0, int n, int nb) {
     return true;
 }
 
-__device__ void process_header(ScanShared& sh, const ScanArgs& a, u64 tile0, u32 p, u32 nb) {
-    const u64 eof = a.avail - tile0;  // tile positions >= eof are past the end of the data
-    auto rd = [&](u64 q) -> u32 { return q < nb ? (u32)sh.buf[16 + q] : (u32)a.buf[tile0 + q]; };
-    u64 q = p;
-    // R2: the token after the first ' ' (frender.py:169 split(" ")[1]) ...
-    for (;;) {
-        if (q >= eof) goto nospace;
-        const u32 c = rd(q);
-        if (c == ' ') break;
-        if (c == '\n' || c == '\r') goto nospace;
-        ++q;
-    }
-    {
-        const u64 sp1 = q;
-        ++q;
-        i64 lc = -1;
-        for (;;) {
-            if (q >= eof) break;
-            const u32 c = rd(q);
-            if (c == ' ' || c == '\n' || c == '\r') break;
-            if (c == ':') lc = (i64)q;
-            ++q;
-        }
-        // ... and its suffix after the last ':' (.split(":")[-1])
-        const u64 start = (lc >= 0 ? (u64)lc : sp1) + 1;
-        const u64 n = q - start;
-        u64 key = 0;
-        bool fast = n >= 1 && n <= (u64)MAXSYM;
-        for (u64 i = 0; fast && i < n; ++i) {
-            const u32 s = sym_of(rd(start + i));
-            fast = s != 0;
-            key |= (u64)s << (3 * i);
-        }
-        if (fast) {
-            lds_insert(sh, a, key, (u32)(tile0 + p));
-        } else {  // exotic code: raw bytes to the exotic pool, merged by the host
-            const u64 i = atomicAdd((unsigned long long*)&a.st->n_exotic, 1ull);
-            const u64 po = atomicAdd((unsigned long long*)&a.st->exo_pool_used, (unsigned long long)n);
-            if (i < a.tab.exo_cap && po + n <= a.tab.exo_pool_cap) {
-                a.tab.exo_ord[i] = make_ord(a, tile0 + p);
-                a.tab.exo_off[i] = po;
-                a.tab.exo_len[i] = (u32)n;
-                for (u64 k = 0; k < n; ++k) a.tab.exo_pool[po + k] = (u8)rd(start + k);
-            } else {
-                atomicOr(&a.st->cap_flags, 4u);
-            }
-        }
+__device__ __forceinline__ void count_code(ScanShared& sh, const ScanArgs& a, u64 tile0, u32 p, u64 key) {
+    if (a.ablate & 4u) {  // ablation: skip the hash insert (keep the key live)
+        asm volatile("" ::"v"(key));
         return;
     }
-nospace:  // IndexError: list index out of range (frender.py:169)
+    lds_insert(sh, a, key, (u32)(tile0 + p));
+}
+
+__device__ void exotic_record(const ScanArgs& a, u64 tile0, u32 p, u64 start, u64 n, ScanShared& sh, u32 nb) {
+    const u64 i = atomicAdd((unsigned long long*)&a.st->n_exotic, 1ull);
+    const u64 po = atomicAdd((unsigned long long*)&a.st->exo_pool_used, (unsigned long long)n);
+    if (i < a.tab.exo_cap && po + n <= a.tab.exo_pool_cap) {
+        a.tab.exo_ord[i] = make_ord(a, tile0 + p);
+        a.tab.exo_off[i] = po;
+        a.tab.exo_len[i] = (u32)n;
+        for (u64 k = 0; k < n; ++k) {
+            const u64 q = start + k;
+            a.tab.exo_pool[po + k] = q < nb ? sh.buf[16 + q] : a.buf[tile0 + q];
+        }
+    } else {
+        atomicOr(&a.st->cap_flags, 4u);
+    }
+}
+
+__device__ __forceinline__ void nospace(const ScanArgs& a, u64 tile0, u32 p) {  // IndexError (frender.py:169)
     atomicMin((unsigned long long*)&a.st->err_nospace, (unsigned long long)(a.file_offset + tile0 + p));
 }
 
+// code bytes [start, start+n) -> fast key (false if outside the fast alphabet)
+__device__ __forceinline__ bool encode_lds(const u8* lb, u32 start, u32 n, u64& key) {
+    if (n < 1 || n > (u32)MAXSYM) return false;
+    u64 k = 0;
+    u32 bad = 0;
+#pragma unroll
+    for (int i = 0; i < MAXSYM; ++i) {  // independent LDS reads (buffer padded past the halo)
+        const u32 c = lb[start + i];
+        const u32 sy = sym_of(c);
+        const bool in = (u32)i < n;
+        bad |= in && sy == 0;
+        k |= (u64)(in ? sy : 0u) << (3 * i);
+    }
+    key = k;
+    return !bad;
+}
+
+// slow path: a header that runs past the LDS halo, read through global memory (rare)
+__device__ void process_header_global(ScanShared& sh, const ScanArgs& a, u64 tile0, u32 p, u32 nb) {
+    const u64 eof = a.avail - tile0;
+    auto rd = [&](u64 q) -> u32 { return q < nb ? (u32)sh.buf[16 + q] : (u32)a.buf[tile0 + q]; };
+    u64 q = p;
+    for (;;) {
+        if (q >= eof) return nospace(a, tile0, p);
+        const u32 c = rd(q);
+        if (c == ' ') break;
+        if (c == '\n' || c == '\r') return nospace(a, tile0, p);
+        ++q;
+    }
+    const u64 sp1 = q++;
+    i64 lc = -1;
+    for (;;) {
+        if (q >= eof) break;
+        const u32 c = rd(q);
+        if (c == ' ' || c == '\n' || c == '\r') break;
+        if (c == ':') lc = (i64)q;
+        ++q;
+    }
+    const u64 start = (lc >= 0 ? (u64)lc : sp1) + 1;
+    const u64 n = q - start;
+    u64 key = 0;
+    bool fast = n >= 1 && n <= (u64)MAXSYM;
+    for (u64 i = 0; fast && i < n; ++i) {
+        const u32 sy = sym_of(rd(start + i));
+        fast = sy != 0;
+        key |= (u64)sy << (3 * i);
+    }
+    if (fast) count_code(sh, a, tile0, p, key);
+    else exotic_record(a, tile0, p, start, n, sh, nb);
+}
+
+// R2 (frender.py:169): the token after the first ' ' up to the next ' ' or line end, then
+// its suffix after the last ':'.  Word-at-a-time SWAR over the LDS tile; bytes past the
+// end of the data read as zero and count as the line end.
+__device__ void process_header(ScanShared& sh, const ScanArgs& a, u64 tile0, u32 p, u32 nb) {
+    const u8* lb = sh.buf + 16;
+    const bool at_eof = (u64)nb >= a.avail - tile0;
+    u32 q = p & ~3u;
+    u32 fm = (0xFu << (p & 3u)) & 0xFu;
+    int sp1 = -1, lastc = -1, end = -1;
+    for (;;) {
+        u32 beyond = 0;
+        if (q + 4 > nb) {
+            if (!at_eof) return process_header_global(sh, a, tile0, p, nb);
+            beyond = q >= nb ? 0xFu : (0xFu << (nb - q)) & 0xFu;
+        }
+        const u32 w = *(const u32*)(lb + q);
+        u32 sp = eq4(w, 0x20202020u) & fm;
+        u32 eol = (eq4(w, 0x0A0A0A0Au) | eq4(w, 0x0D0D0D0Du) | beyond) & fm;
+        u32 col = eq4(w, 0x3A3A3A3Au) & fm;
+        fm = 0xFu;
+        if (sp1 < 0) {
+            const u32 ev = sp | eol;
+            if (!ev) {
+                q += 4;
+                continue;
+            }
+            const u32 b = __builtin_ctz(ev);
+            if ((eol >> b) & 1u) return nospace(a, tile0, p);
+            sp1 = (int)(q + b);
+            const u32 keep = ~((2u << b) - 1u) & 0xFu;
+            sp &= keep;
+            eol &= keep;
+            col &= keep;
+        }
+        const u32 ev = sp | eol;
+        if (ev) {
+            const u32 b = __builtin_ctz(ev);
+            const u32 cm = col & ((1u << b) - 1u);
+            if (cm) lastc = (int)(q + 31u - __builtin_clz(cm));
+            end = (int)(q + b);
+            break;
+        }
+        if (col) lastc = (int)(q + 31u - __builtin_clz(col));
+        q += 4;
+    }
+    const u32 start = (u32)((lastc > sp1 ? lastc : sp1) + 1);
+    const u32 n = (u32)end - start;
+    if (a.ablate & 2u) {  // ablation: skip the code encode
+        asm volatile("" ::"v"(start), "v"(n));
+        return;
+    }
+    u64 key;
+    if (encode_lds(lb, start, n, key)) count_code(sh, a, tile0, p, key);
+    else exotic_record(a, tile0, p, start, n, sh, nb);
+}
+
+// ---- tile staging: 16-B loads into registers (prefetch), then registers -> LDS ----------
+constexpr int STAGE_VECS = (TILE + HALO + WG * 16 - 1) / (WG * 16);  // 5
+
+struct TileRegs {
+    uint4 v[STAGE_VECS];
+    uint4 pre;  // the 16 bytes before the tile (thread 0; UTF-8 continuation checks)
+};
+
+__device__ __forceinline__ void tile_fetch(const ScanArgs& a, u32 t, TileRegs& r, int tid) {
+    if (t >= a.num_tiles) return;
+    const u64 tile0 = (u64)t * TILE;
+    const u32 nb = (u32)min((u64)(TILE + HALO), a.avail - tile0);
+#pragma unroll
+    for (int k = 0; k < STAGE_VECS; ++k) {
+        const u32 off = tid * 16 + k * WG * 16;
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);
+        if (off + 16 <= nb) {
+            v = *(const uint4*)(a.buf + tile0 + off);
+        } else if (off < nb) {
+            u32 w[4] = {0u, 0u, 0u, 0u};
+            for (u32 j = 0; off + j < nb; ++j) w[j >> 2] |= (u32)a.buf[tile0 + off + j] << (8 * (j & 3));
+            v = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+        r.v[k] = v;
+    }
+    if (tid == 0) {
+        r.pre = make_uint4(0u, 0u, 0u, 0u);
+        if (tile0 >= 16 || a.pre_valid) r.pre = *(const uint4*)(a.buf + tile0 - 16);
+    }
+}
+
+__device__ __forceinline__ void tile_stage(ScanShared& sh, const TileRegs& r, int tid) {
+#pragma unroll
+    for (int k = 0; k < STAGE_VECS; ++k) {
+        const u32 off = tid * 16 + k * WG * 16;
+        if (off < (u32)(TILE + HALO)) *(uint4*)(sh.buf + 16 + off) = r.v[k];
+    }
+    if (tid == 0) *(uint4*)(sh.buf) = r.pre;
+}
+
+struct TileCount {
+    u64 tmask;  // line-terminator bitmap of this thread's 64 bytes
+    u32 c;      // popcount(tmask)
+    u32 x;      // inclusive wave scan of c
+    u32 wexcl;  // terminators in earlier waves of this tile
+    u32 tot;    // terminators in the tile
+};
+
+// line-terminator bitmap of the staged tile t, block scan, and publication of its aggregate
+// (R1: universal newlines: '\n', '\r\n' and a lone '\r' each end one line)
+__device__ TileCount count_tile(ScanShared& sh, const ScanArgs& a, u32 t, int tid, int lane, int wid) {
+    const u64 tile0 = (u64)t * TILE;
+    const u32 tlen = (u32)min((u64)TILE, a.len - tile0);
+    const u32 nb = (u32)min((u64)(TILE + HALO), a.avail - tile0);
+    const u32 s0 = tid * SEG;
+    TileCount tc;
+    tc.tmask = 0;
+    if (s0 < tlen) {
+        u64 nl = 0, cr = 0, hi = 0;
+#pragma unroll
+        for (int qv = 0; qv < SEG / 16; ++qv) {
+            const uint4 v = *(const uint4*)(sh.buf + 16 + s0 + qv * 16);
+            const u32 w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int sh4 = qv * 16 + k * 4;
+                nl |= (u64)eq4(w[k], 0x0A0A0A0Au) << sh4;
+                cr |= (u64)eq4(w[k], 0x0D0D0D0Du) << sh4;
+                hi |= (u64)hi4(w[k]) << sh4;
+            }
+        }
+        const u64 nxt = (s0 + SEG < nb && sh.buf[16 + s0 + SEG] == '\n') ? 1ull : 0ull;
+        tc.tmask = nl | (cr & ~((nl >> 1) | (nxt << 63)));
+        const u32 valid = tlen - s0;
+        if (valid < SEG) {
+            const u64 vm = (1ull << valid) - 1ull;
+            tc.tmask &= vm;
+            hi &= vm;
+        }
+        if (hi) {
+            atomicOr(&sh.flags, 1u);
+            if (!utf8_segment_ok(sh, (int)s0, (int)min(valid, (u32)SEG), (int)nb)) atomicOr(&sh.flags, 2u);
+        }
+    }
+    tc.c = __popcll(tc.tmask);
+    u32 x = tc.c;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const u32 y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    tc.x = x;
+    if (lane == 63) sh.wsum[wid] = x;
+    __syncthreads();
+    u32 wexcl = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < WG / 64; ++w) {
+        const u32 v = sh.wsum[w];
+        wexcl += w < wid ? v : 0u;
+        tot += v;
+    }
+    tc.wexcl = wexcl;
+    tc.tot = tot;
+    if (tid == 0) {  // publish: tile 0 is inclusive at once, every other tile its aggregate
+        const u64 tag = (u64)(2u * a.epoch + (t == 0 ? 1u : 0u)) << 32;
+        agent_store(&a.tiles[t], tag | tot);
+    }
+    return tc;
+}
+
+// The tally kernel.  Persistent workgroups draw tiles from a ticket counter; per tile:
+//   look-back (prefix of line terminators) -> every 4th line start -> parse headers (lane per
+//   header) -> count codes in the LDS table (HBM table for the rest).
+// Software pipeline: while tile t is parsed, the next tile's ticket and bytes are already in
+// flight; the next tile is staged and its aggregate published before its own look-back, so
+// look-backs mostly find ready predecessors.
+#ifdef FR_STAMPS
+#define STAMP(i)                                                   \
+    do {                                                           \
+        __builtin_amdgcn_sched_barrier(0);                         \
+        const u64 now_ = __builtin_amdgcn_s_memtime();             \
+        __builtin_amdgcn_sched_barrier(0);                         \
+        if (tid == 0) stamps[i] += now_ - last_;                   \
+        last_ = now_;                                              \
+    } while (0)
+#else
+#define STAMP(i) \
+    do {         \
+    } while (0)
+#endif
+
 __global__ __launch_bounds__(WG) void scan_kernel(ScanArgs a) {
     __shared__ ScanShared sh;
+#ifdef FR_STAMPS
+    u64 stamps[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    u64 last_ = __builtin_amdgcn_s_memtime();
+#endif
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wid = tid >> 6;
@@ -306,105 +559,49 @@ __global__ __launch_bounds__(WG) void scan_kernel(ScanArgs a) {
         sh.cnt[i] = 0;
         sh.mino[i] = 0xFFFFFFFFu;
     }
+    if (tid < 2) *(uint4*)(sh.buf + 16 + TILE + HALO + 16 * tid) = make_uint4(0u, 0u, 0u, 0u);
     if (tid == 0) {
         sh.nkeys = 0;
+        sh.created = 0;
         sh.flags = 0;
+        sh.tile = atomicAdd(&a.st->ticket, 1u);
     }
     const u64 base_lines = a.st->lines[a.par];
     __syncthreads();
-
-    for (;;) {
-        if (tid == 0) {
-            sh.tile = atomicAdd(&a.st->ticket, 1u);
-            sh.nhdr = 0;
-        }
+    u32 t = sh.tile;
+    TileRegs r;
+    TileCount tc;
+    if (t < a.num_tiles) {
+        tile_fetch(a, t, r, tid);
+        tile_stage(sh, r, tid);
         __syncthreads();
-        const u32 t = sh.tile;
-        if (t >= a.num_tiles) break;
+        tc = count_tile(sh, a, t, tid, lane, wid);
+    }
+    STAMP(7);
+    while (t < a.num_tiles) {
         const u64 tile0 = (u64)t * TILE;
-        const u32 tlen = (u32)min((u64)TILE, a.len - tile0);
         const u32 nb = (u32)min((u64)(TILE + HALO), a.avail - tile0);
-
-        // ---- stage the tile (+halo) in LDS with 16-B loads --------------------------
-        for (u32 off = tid * 16; off < (u32)(TILE + HALO); off += WG * 16) {
-            uint4 v = make_uint4(0u, 0u, 0u, 0u);
-            if (off + 16 <= nb) {
-                v = *(const uint4*)(a.buf + tile0 + off);
-            } else if (off < nb) {
-                u32 w[4] = {0u, 0u, 0u, 0u};
-                for (u32 j = 0; off + j < nb; ++j) w[j >> 2] |= (u32)a.buf[tile0 + off + j] << (8 * (j & 3));
-                v = make_uint4(w[0], w[1], w[2], w[3]);
-            }
-            *(uint4*)(sh.buf + 16 + off) = v;
-        }
-        if (tid == 0) {  // the 16 bytes before the tile (only for UTF-8 continuation checks)
-            uint4 v = make_uint4(0u, 0u, 0u, 0u);
-            if (tile0 >= 16 || a.pre_valid) v = *(const uint4*)(a.buf + tile0 - 16);
-            *(uint4*)(sh.buf) = v;
-        }
-        __syncthreads();
-
-        // ---- line-terminator bitmap of this thread's 64 bytes -----------------------
-        const u32 s0 = tid * SEG;
-        u64 tmask = 0;
-        if (s0 < tlen) {
-            u64 nl = 0, cr = 0, hi = 0;
-#pragma unroll
-            for (int qv = 0; qv < SEG / 16; ++qv) {
-                const uint4 v = *(const uint4*)(sh.buf + 16 + s0 + qv * 16);
-                const u32 w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const int sh4 = qv * 16 + k * 4;
-                    nl |= (u64)eq4(w[k], 0x0A0A0A0Au) << sh4;
-                    cr |= (u64)eq4(w[k], 0x0D0D0D0Du) << sh4;
-                    hi |= (u64)hi4(w[k]) << sh4;
-                }
-            }
-            const u64 nxt = (s0 + SEG < nb && sh.buf[16 + s0 + SEG] == '\n') ? 1ull : 0ull;
-            // '\r' ends a line unless a '\n' follows (then the '\n' ends it): universal newlines
-            tmask = nl | (cr & ~((nl >> 1) | (nxt << 63)));
-            const u32 valid = tlen - s0;
-            if (valid < SEG) {
-                const u64 vm = (1ull << valid) - 1ull;
-                tmask &= vm;
-                hi &= vm;
-            }
-            if (hi) {
-                atomicOr(&sh.flags, 1u);
-                if (!utf8_segment_ok(sh, (int)s0, (int)min(valid, (u32)SEG), (int)nb)) atomicOr(&sh.flags, 2u);
-            }
-        }
-
-        // ---- block scan of terminator counts + decoupled look-back ------------------
-        const u32 c = __popcll(tmask);
-        u32 x = c;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const u32 y = __shfl_up(x, d, 64);
-            if (lane >= d) x += y;
-        }
-        if (lane == 63) sh.wsum[wid] = x;
-        __syncthreads();
-        u32 wexcl = 0, tot = 0;
-#pragma unroll
-        for (int w = 0; w < WG / 64; ++w) {
-            const u32 v = sh.wsum[w];
-            wexcl += w < wid ? v : 0u;
-            tot += v;
-        }
+        u32 tn = 0;
+        if (tid == 0) tn = atomicAdd(&a.st->ticket, 1u);  // returns during the look-back
         if (wid == 0) {
-            const u64 ex = lookback(a, t, tot, lane);
+            const u64 ex = lookback(a, t, tc.tot, lane);
             if (lane == 0) {
                 sh.tile_excl = ex;
-                if (t == a.num_tiles - 1) a.st->lines[a.par ^ 1u] = base_lines + ex + tot;
+                if (t == a.num_tiles - 1) a.st->lines[a.par ^ 1u] = base_lines + ex + tc.tot;
+                sh.next = tn;
+                sh.nhdr = 0;
             }
         }
+        STAMP(0);
         __syncthreads();
+        STAMP(1);
+        tn = sh.next;
+        tile_fetch(a, tn, r, tid);  // prefetch: lands while this tile is parsed
 
         // ---- every 4th line is a header (R1); collect their starts -------------------
-        u64 L = base_lines + sh.tile_excl + wexcl + (x - c);
-        u64 m = tmask;
+        u64 L = base_lines + sh.tile_excl + tc.wexcl + (tc.x - tc.c);
+        u64 m = tc.tmask;
+        const u32 s0 = tid * SEG;
         while (m) {
             const int j = __ffsll((long long)m) - 1;
             m &= m - 1;
@@ -425,20 +622,32 @@ __global__ __launch_bounds__(WG) void scan_kernel(ScanArgs a) {
             sh.hdr[slot] = 0;
         }
         __syncthreads();
+        STAMP(2);
 
         // ---- parse headers (lane per header) and count their codes ------------------
         const u32 nh = sh.nhdr;
-        for (u32 h = tid; h < nh; h += WG) process_header(sh, a, tile0, sh.hdr[h], nb);
+        if (!(a.ablate & 1u))
+            for (u32 h = tid; h < nh; h += WG) process_header(sh, a, tile0, sh.hdr[h], nb);
         __syncthreads();
-        if (sh.nkeys > (u32)(NS * 3 / 4)) {
-            lds_flush(sh, a);
-            __syncthreads();
-            if (tid == 0) sh.nkeys = 0;
-        }
+        STAMP(3);
+        if (tn >= a.num_tiles) break;
+        tile_stage(sh, r, tid);
+        __syncthreads();
+        STAMP(4);
+        tc = count_tile(sh, a, tn, tid, lane, wid);
+        STAMP(5);
+        t = tn;
     }
     __syncthreads();
     lds_flush(sh, a);
+    __syncthreads();
+    STAMP(6);
+#ifdef FR_STAMPS
+    if (tid == 0)
+        for (int i = 0; i < 8; ++i) atomicAdd((unsigned long long*)&a.st->stamp[i], (unsigned long long)stamps[i]);
+#endif
     if (tid == 0) {
+        if (sh.created) atomicAdd((unsigned long long*)&a.st->n_keys, (unsigned long long)sh.created);
         if (sh.flags & 1u) atomicOr(&a.st->nonascii, 1u);
         if (sh.flags & 2u) atomicOr(&a.st->utf8_bad, 1u);
     }
@@ -472,10 +681,12 @@ hipError_t launch_table_init(GSlot* slots, u64 n, hipStream_t s) {
 
 // re-insert overflow entries (after the table has grown); presence is re-derived
 __global__ void reinsert_kernel(Table t, DevState* st, const Overflow* src, u64 n) {
+    u32 made = 0;
     for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
         const Overflow o = src[i];
-        global_insert(t, st, o.key, o.count, o.first, o.tag);
+        made += global_insert(t, st, o.key, o.count, o.first, o.tag) ? 1u : 0u;
     }
+    add_created(st, made);
 }
 
 hipError_t launch_reinsert_overflow(Table t, DevState* st, const Overflow* src, u64 n, hipStream_t s) {
@@ -604,8 +815,47 @@ hipError_t launch_presence_map(const GSlot* slots, u64 mask, const Presence* pre
 // merge another GPU's compacted table into this one (count +, first min); presence of
 // remote keys travels separately (fr_get_presence on each rank)
 __global__ void merge_kernel(Table t, DevState* st, const u64* keys, const u64* counts, const u64* first, u64 n) {
+    u32 made = 0;
     for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x)
-        global_insert(t, st, keys[i], counts[i], first[i], 0u);
+        made += global_insert(t, st, keys[i], counts[i], first[i], 0u) ? 1u : 0u;
+    add_created(st, made);
+}
+
+// per-file presence (R10) and the per-file distinct-code count (frender.py:175): after a
+// file, exactly the slots whose last_tag is that file's tag hold a code seen in it
+__global__ void presence_scan_kernel(const GSlot* slots, u64 n, u32 tag, Presence* pres, u64 cap, DevState* st) {
+    const u64 stride = (u64)gridDim.x * blockDim.x;
+    for (u64 base = blockIdx.x * (u64)blockDim.x; base < n; base += stride) {
+        const u64 i = base + threadIdx.x;
+        GSlot g;
+        bool hit = false;
+        if (i < n) {
+            g = slots[i];
+            hit = g.key != 0 && g.last_tag == tag;
+        }
+        const u64 b = __ballot(hit);
+        if (!b) continue;
+        const int lane = threadIdx.x & 63;
+        u64 at = 0;
+        if (lane == 0) at = atomicAdd((unsigned long long*)&st->n_presence, (unsigned long long)__popcll(b));
+        at = __shfl(at, 0, 64);
+        if (hit) {
+            const u64 k = at + __popcll(b & ((1ull << lane) - 1ull));
+            if (k < cap) {
+                pres[k].key = g.key;
+                pres[k].tag = tag;
+            } else {
+                atomicOr(&st->cap_flags, 1u);
+            }
+        }
+    }
+}
+
+hipError_t launch_presence_scan(const GSlot* slots, u64 n, u32 tag, Presence* pres, u64 cap, DevState* st,
+                                hipStream_t s) {
+    const int grid = (int)std::min<u64>((n + 255) / 256, 8192);
+    hipLaunchKernelGGL(presence_scan_kernel, dim3(grid), dim3(256), 0, s, slots, n, tag, pres, cap, st);
+    return hipGetLastError();
 }
 
 hipError_t launch_merge(Table t, DevState* st, const u64* keys, const u64* counts, const u64* first, u64 n,

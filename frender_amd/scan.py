@@ -130,8 +130,8 @@ def tally_barcodes(cores, files, sample=None, ctx=None) -> UniqueTable:
             raise UnicodeDecodeError("utf-8", b"", 0, 1, "invalid start byte")
         new_here = int(st.new_keys)
         if st.exotic:
-            ords, lens, offs, pool = ctx.exotic()
-            for k in range(exo_seen, len(ords)):
+            ords, lens, offs, pool = ctx.exotic(exo_seen, int(st.exotic))
+            for k in range(len(ords)):
                 code = bytes(pool[int(offs[k]):int(offs[k]) + int(lens[k])]).decode("utf-8")
                 e = exo.get(code)
                 if e is None:
@@ -143,7 +143,7 @@ def tally_barcodes(cores, files, sample=None, ctx=None) -> UniqueTable:
                     if fi not in e[2]:
                         e[2].add(fi)
                         new_here += 1
-            exo_seen = len(ords)
+            exo_seen += len(ords)
         records.append(int(st.records))
         print(f"found {new_here} new barcode{'' if new_here == 1 else 's'} in {st.records} reads.")
     print(type([]), len(files))

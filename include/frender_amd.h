@@ -69,6 +69,8 @@ void fr_destroy(fr_ctx* ctx);
 const char* fr_last_error(const fr_ctx* ctx);
 int fr_get_timing(fr_ctx* ctx, fr_timing* out);
 int fr_sync(fr_ctx* ctx);
+/* diagnostics: {look-back max polls, total polls, keys, overflow, presence, exotic, grid, slots} */
+int fr_get_diag(fr_ctx* ctx, uint64_t* out, int n);
 
 /* ---- sample sheet (the idx1/idx2/id lists of get_indexes, frender.py:90-116) -------
  * idx*_packed: each entry case-folded (str.lower(), :226) and packed 3 bits/char,
@@ -107,9 +109,12 @@ int fr_finalize(fr_ctx* ctx, uint64_t* n_unique, uint64_t* n_presence, uint64_t*
 int fr_get_unique(fr_ctx* ctx, uint64_t* keys, uint64_t* counts, uint64_t* first_ordinal);
 /* (unique index, file index) for every file a fast-path key occurs in (R10 demux_ok) */
 int fr_get_presence(fr_ctx* ctx, uint32_t* unique_idx, uint32_t* file_idx);
-/* raw exotic records: file byte offset | file index << 44, code length, pool offset */
-int fr_get_exotic(fr_ctx* ctx, uint64_t* ordinal, uint32_t* length, uint64_t* pool_offset,
-                  uint8_t* pool, uint64_t pool_bytes);
+/* exotic records [first, first+count) (count is clamped to those captured so far):
+ * ordinal = (file index+1) << 44 | file byte offset of the header, code length, offset of
+ * the code's bytes in the pool; pool receives the first pool_bytes bytes of the pool.
+ * Returns the number of records written through *written. */
+int fr_get_exotic(fr_ctx* ctx, uint64_t first, uint64_t count, uint64_t* ordinal, uint32_t* length,
+                  uint64_t* pool_offset, uint8_t* pool, uint64_t pool_bytes, uint64_t* written);
 
 /* ---- classify: replaces process (:391-426) -> analyze_barcodes_with_rc (:294-351)
  *      -> analyze_barcode (:237-291) -> get_indexes_of_approx_matches (:214-234) ----

@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 STAGE=${1:-all}
 rc=0
 if [[ $STAGE == all || $STAGE == test ]]; then
-  timeout -k 10 900 python -m pytest tests -m gpu -q --maxfail=15 --timeout=600 -p no:cacheprovider \
+  timeout -k 10 900 python -m pytest tests -m gpu -q --maxfail=15 --timeout=600 -rf -p no:cacheprovider \
       > gpurun_out/pytest_gpu.log 2>&1
   rc=$?
   tail -30 gpurun_out/pytest_gpu.log

@@ -252,3 +252,32 @@ def test_classify_random(ctx, lib, nsubs, rc):
         f, r = ctx.rc_counts()
         assert f.tolist() == [f_exp[n] for n in names]
         assert r.tolist() == [r_exp[n] for n in names]
+
+
+@pytest.mark.parametrize("grid,cap,chunk", [(1, 1536, 1 << 24), (4, 0, 1 << 26), (64, 16, 1 << 26), (512, 1536, 1 << 30)])
+def test_many_tiles_per_workgroup(lib, monkeypatch, grid, cap, chunk):
+    """Few workgroups walking many tiles each (look-back windows sliding past 64 tiles),
+    with the LDS table capped so most codes take the direct-to-HBM path."""
+    from frender_amd import synth
+    from oracle.frender_oracle import tally_text
+    monkeypatch.setenv("FR_GRID", str(grid))
+    monkeypatch.setenv("FR_FLUSH_AT", str(cap))
+    c = lib.Context(device=0, chunk_bytes=chunk, table_slots=1 << 16)
+    try:
+        sheet = synth.make_sheet(96, 8, 8)
+        n = 1_500_000
+        host = synth.generate_bytes(sheet, 7, n, R=8, seed=2)
+        p = c.device_alloc(len(host))
+        c.synth_device(p, 7, n, 8, 2, sheet.idx1, sheet.idx2)
+        c.reset()
+        c.begin_file(None)
+        c.feed_device(p, len(host))
+        st = c.end_file()
+        c.device_free(p)
+        assert st.records == n and st.error == 0
+        c.finalize()
+        keys, counts, _ = c.unique()
+        exp, _ = tally_text(host.decode())
+        assert list(zip(lib.decode_keys(keys), counts.tolist())) == list(exp.items())
+    finally:
+        c.close()

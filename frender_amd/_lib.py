@@ -302,8 +302,10 @@ class Context:
         d = dict(zip(("spin_max", "spin_total", "keys", "overflow", "presence", "exotic", "grid", "slots"),
                      v[:8].tolist()))
         if v[8:].any():  # FR_STAMPS build: cycles per phase summed over workgroups
-            d["stamps"] = dict(zip(("lookback", "barrier", "headers", "parse", "stage", "count", "flush",
-                                    "prologue"), v[8:].tolist()))
+            names = (("lookback", "barrier", "headers", "parse", "stage", "count", "flush", "prologue")
+                     if os.environ.get("FR_KERNEL") == "0" else
+                     ("collect", "parse", "stage", "count", "first_tile", "infer", "lookback", "commit"))
+            d["stamps"] = dict(zip(names, v[8:].tolist()))
         return d
 
     def sync(self):

@@ -25,6 +25,9 @@ struct fr_ctx {
     int grid = 0;
     u32 flush_at = NS * 3 / 4;
     u32 ablate = 0;
+    int kernel = 1;  // 1 chunk kernel (v3), 0 per-tile look-back kernel (v2)
+    u64* cold = nullptr;
+    u32 cold_cap = 32768;
 
     DevState* st = nullptr;
     DevState* h_st = nullptr;      // pinned snapshot
@@ -251,8 +254,16 @@ static int launch_range(fr_ctx* ctx, const u8* dptr, u64 len, u64 avail, int own
         ctx->ev_b.push_back(e2);
     }
     CK(hipEventRecord(ctx->ev_a[ctx->ev_used], ctx->stream));
-    const int grid = (int)std::min<u64>((u64)ctx->grid, a.num_tiles);
-    CK(launch_scan(a, grid, ctx->stream));
+    if (ctx->kernel == 1) {
+        a.chunk_tiles = (u32)std::max<u64>(1, (a.num_tiles + ctx->grid - 1) / ctx->grid);
+        a.num_chunks = (a.num_tiles + a.chunk_tiles - 1) / a.chunk_tiles;
+        a.cold_cap = ctx->cold_cap;
+        a.cold = ctx->cold;
+        CK(launch_chunk_scan(a, (int)a.num_chunks, ctx->stream));
+    } else {
+        const int grid = (int)std::min<u64>((u64)ctx->grid, a.num_tiles);
+        CK(launch_scan(a, grid, ctx->stream));
+    }
     CK(hipEventRecord(ctx->ev_b[ctx->ev_used], ctx->stream));
     ctx->ev_used++;
     ctx->scan_launches++;
@@ -282,6 +293,9 @@ fr_ctx* fr_create(int device, uint64_t chunk_bytes, uint64_t table_slots) {
     if (const char* g = getenv("FR_GRID")) ctx->grid = std::max(1, atoi(g));
     if (const char* f = getenv("FR_FLUSH_AT")) ctx->flush_at = (u32)atoi(f);
     if (const char* f = getenv("FR_ABLATE")) ctx->ablate = (u32)atoi(f);
+    if (const char* f = getenv("FR_KERNEL")) ctx->kernel = atoi(f);
+    if (const char* f = getenv("FR_COLD_CAP")) ctx->cold_cap = (u32)std::max(1024, atoi(f));
+    if ((e = dalloc(&ctx->cold, 2ull * ctx->cold_cap * (u64)ctx->grid)) != hipSuccess) return bad("cold lists", e);
 
     ctx->chunk_bytes = chunk_bytes ? ((chunk_bytes + TILE - 1) / TILE) * TILE : (256ull << 20);
     if (ctx->chunk_bytes > RANGE_MAX) ctx->chunk_bytes = RANGE_MAX;
@@ -331,7 +345,7 @@ void fr_destroy(fr_ctx* ctx) {
                    ctx->d_cpl2, ctx->d_keys, ctx->d_counts, ctx->d_first, ctx->d_keys_s, ctx->d_counts_s,
                    ctx->d_first_s, ctx->d_pos, ctx->d_perm, ctx->d_rank, ctx->d_counter, ctx->d_temp, ctx->d_pres_u,
                    ctx->d_pres_f, ctx->d_m1, ctx->d_m2, ctx->d_row, ctx->d_rm2, ctx->d_rrow, ctx->d_cls, ctx->d_rcls,
-                   ctx->d_errw, ctx->d_errf, ctx->d_rcf, ctx->d_rcr};
+                   ctx->d_errw, ctx->d_errf, ctx->d_rcf, ctx->d_rcr, ctx->cold};
     for (void* p : dev)
         if (p) (void)hipFree(p);
     if (ctx->h_st) (void)hipHostFree(ctx->h_st);

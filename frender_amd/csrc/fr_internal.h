@@ -25,6 +25,8 @@ constexpr int MAXSYM = 21;           // fast key: <= 21 symbols of 3 bits
 constexpr u64 RANGE_MAX = 1ull << 30;  // bytes per tally launch (device feeds)
 constexpr u32 SPIN_MAX = 1u << 24;   // look-back spin bound (then FR_ERR_DEVICE)
 constexpr int ORD_SHIFT = 44;        // ordinal = file_tag << 44 | file byte offset
+constexpr int EXO_BUF = 32;          // chunk kernel: exotic records buffered while speculating
+constexpr int PHASE_LINES = 24;      // chunk kernel: lines inspected to guess a chunk's line phase
 
 // ---- HBM structures ---------------------------------------------------------------
 struct alignas(32) GSlot {           // open-addressing slot, one 32-B sector
@@ -94,7 +96,10 @@ struct ScanArgs {
     u32 flush_at;        // LDS table key cap: past it, new codes go to the HBM table directly
     i64 max_records;     // -s, <= 0: none
     u32 ablate;          // timing ablation bits (FR_ABLATE; 0 in production): 1 parse, 2 encode, 4 insert
-    u32 pad2;
+    u32 chunk_tiles;     // chunk kernel: tiles per chunk (a workgroup's contiguous unit)
+    u32 num_chunks;
+    u32 cold_cap;        // chunk kernel: entries of each workgroup's cold list
+    u64* cold;           // chunk kernel: cold lists, [grid][cold_cap] x {key, ordinal}
     DevState* st;
     u64* tiles;          // look-back descriptors
     Table tab;
@@ -139,6 +144,7 @@ __host__ __device__ inline u64 mix64(u64 x) {
 // ---- launchers (fr_kernels.hip) --------------------------------------------------
 hipError_t launch_table_init(GSlot* slots, u64 n, hipStream_t s);
 hipError_t launch_scan(const ScanArgs& a, int grid, hipStream_t s);
+hipError_t launch_chunk_scan(const ScanArgs& a, int grid, hipStream_t s);
 hipError_t launch_reinsert_overflow(Table t, DevState* st, const Overflow* src, u64 n, hipStream_t s);
 hipError_t launch_rehash(Table dst, DevState* st, const GSlot* src, u64 nsrc, hipStream_t s);
 hipError_t launch_compact(const GSlot* slots, u64 nslots, u64* keys, u64* counts, u64* first, u32* pos,

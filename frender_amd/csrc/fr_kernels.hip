@@ -46,6 +46,26 @@ __device__ __forceinline__ u32 sym_of(u32 c) {
     return ok ? ((symtab >> (4 * i)) & 0xFu) : 0u;
 }
 
+// Fused byte classifier, 4 bytes per call: per byte, bit0 '\n', bit1 '\r', bit2 ' ', bit3 ':'
+// (ASCII only).  Two nibble lookup tables through v_perm_b32: class = T_hi[c >> 4] & T_lo[c & 15].
+__device__ __forceinline__ u32 classify4(u32 w) {
+    const u32 hn = (w >> 4) & 0x07070707u;                                   // bit 3 handled by `kill`
+    const u32 ln = w & 0x0F0F0F0Fu;
+    const u32 l7 = ln & 0x07070707u;
+    const u32 ch = __builtin_amdgcn_perm(0u, 0x08040003u, hn);               // 0:{nl,cr} 2:sp 3:col
+    const u32 c0 = __builtin_amdgcn_perm(0u, 0x00000004u, l7);               // lo 0: sp
+    const u32 c1 = __builtin_amdgcn_perm(0x00000200u, 0x00090000u, l7);      // lo 0xA: nl|col, 0xD: cr
+    const u32 m8 = ((ln >> 3) & 0x01010101u) * 0xFFu;
+    const u32 kill = ((w >> 7) & 0x01010101u) * 0xFFu;
+    return ch & ((c0 & ~m8) | (c1 & m8)) & ~kill;
+}
+
+// gather bit k of each of the 4 bytes into a 4-bit mask (byte i -> bit i)
+template <int K>
+__device__ __forceinline__ u32 gather4(u32 c) {
+    return ((((c >> K) & 0x01010101u) * 0x00204081u) >> 21) & 0xFu;
+}
+
 __device__ __forceinline__ u64 agent_load(const u64* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -131,6 +151,21 @@ struct ScanShared {
     u32 nkeys;        // occupied LDS slots
     u32 created;      // HBM slots this workgroup created (added to n_keys once, at exit)
     u32 flags;
+    // ---- chunk kernel state ----
+    u32 buffered;     // LDS-table misses go to this workgroup's cold list (committed later)
+    u32 spec;         // speculating on the line phase: exotic records / errors are buffered
+    u32 spec_bad;     // a speculation buffer overflowed: redo this chunk exactly
+    u32 ncold;        // cold list fill
+    u32 nexo;         // buffered exotic records
+    u32 err_off;      // min range offset of a header without ' ' (buffered), ~0 none
+    u32 chunk;
+    int phase;        // guessed line phase (lines before the chunk, mod 4), -1 unsure
+    u32 exo_p[EXO_BUF], exo_start[EXO_BUF], exo_len[EXO_BUF];
+    u64 tbits[WG];    // line-terminator bitmap of a chunk's first tile (phase inference)
+    u64 bsp[WG];      // per 64-B segment of the staged tile: ' ' bitmap
+    u64 bcol[WG];     //                                      ':' bitmap
+    u64 beol[WG];     //                                      '\r' | '\n' bitmap
+    u32 hscan[WG / 64];
 };
 
 __device__ __forceinline__ u64 make_ord(const ScanArgs& a, u64 off_in_range) {
@@ -173,6 +208,20 @@ __device__ __forceinline__ void lds_insert(ScanShared& sh, const ScanArgs& a, u6
         }
         h = (h + 1) & (NS - 1);
     }
+    if (sh.buffered) {  // chunk kernel: park the miss in this workgroup's cold list
+        const u32 i = atomicAdd(&sh.ncold, 1u);
+        if (i < a.cold_cap) {
+            u64* c = a.cold + 2ull * ((u64)blockIdx.x * a.cold_cap + i);
+            c[0] = key;
+            c[1] = make_ord(a, off);
+            return;
+        }
+        if (sh.spec) {  // cannot buffer while speculating: this chunk will be redone exactly
+            atomicOr(&sh.spec_bad, 1u);
+            return;
+        }
+        // exact phase and a full cold list: insert directly
+    }
     if (global_insert(a.tab, a.st, key, 1, make_ord(a, off), a.file_tag)) atomicAdd(&sh.created, 1u);
 }
 
@@ -180,7 +229,7 @@ __device__ __forceinline__ void lds_insert(ScanShared& sh, const ScanArgs& a, u6
 // The tile's own aggregate was published when it was staged (count_tile); this resolves its
 // exclusive prefix, reading 256 predecessors per poll (4 per lane), and publishes the
 // inclusive prefix.  Returns the number of line terminators in tiles [0, t) of the range.
-__device__ u64 lookback(const ScanArgs& a, u32 t, u32 agg, int lane) {
+__device__ __forceinline__ u64 lookback(const ScanArgs& a, u32 t, u32 agg, int lane) {
     if (t == 0) return 0;  // tile 0 published its inclusive value directly
     const u64 tagI = (u64)(2u * a.epoch + 1u) << 32;
     u64 excl = 0;
@@ -218,7 +267,7 @@ __device__ u64 lookback(const ScanArgs& a, u32 t, u32 agg, int lane) {
                 if (lane == 0) atomicOr(&a.st->spin_fail, 1u);
                 return 0;
             }
-            if (spins > 2) __builtin_amdgcn_s_sleep(1);
+            if (spins > 2) __builtin_amdgcn_s_sleep(8);
             continue;
         }
         u64 contrib = 0;
@@ -288,6 +337,17 @@ __device__ __forceinline__ void count_code(ScanShared& sh, const ScanArgs& a, u6
 }
 
 __device__ void exotic_record(const ScanArgs& a, u64 tile0, u32 p, u64 start, u64 n, ScanShared& sh, u32 nb) {
+    if (sh.spec) {  // speculating: remember where it is; the bytes stay resident in HBM
+        const u32 k = atomicAdd(&sh.nexo, 1u);
+        if (k < (u32)EXO_BUF) {
+            sh.exo_p[k] = (u32)(tile0 + p);
+            sh.exo_start[k] = (u32)(tile0 + start);
+            sh.exo_len[k] = (u32)n;
+        } else {
+            atomicOr(&sh.spec_bad, 1u);
+        }
+        return;
+    }
     const u64 i = atomicAdd((unsigned long long*)&a.st->n_exotic, 1ull);
     const u64 po = atomicAdd((unsigned long long*)&a.st->exo_pool_used, (unsigned long long)n);
     if (i < a.tab.exo_cap && po + n <= a.tab.exo_pool_cap) {
@@ -303,8 +363,9 @@ __device__ void exotic_record(const ScanArgs& a, u64 tile0, u32 p, u64 start, u6
     }
 }
 
-__device__ __forceinline__ void nospace(const ScanArgs& a, u64 tile0, u32 p) {  // IndexError (frender.py:169)
-    atomicMin((unsigned long long*)&a.st->err_nospace, (unsigned long long)(a.file_offset + tile0 + p));
+__device__ __forceinline__ void nospace(const ScanArgs& a, u64 tile0, u32 p, ScanShared& sh) {  // IndexError (:169)
+    if (sh.spec) atomicMin(&sh.err_off, (u32)(tile0 + p));
+    else atomicMin((unsigned long long*)&a.st->err_nospace, (unsigned long long)(a.file_offset + tile0 + p));
 }
 
 // code bytes [start, start+n) -> fast key (false if outside the fast alphabet)
@@ -330,10 +391,10 @@ __device__ void process_header_global(ScanShared& sh, const ScanArgs& a, u64 til
     auto rd = [&](u64 q) -> u32 { return q < nb ? (u32)sh.buf[16 + q] : (u32)a.buf[tile0 + q]; };
     u64 q = p;
     for (;;) {
-        if (q >= eof) return nospace(a, tile0, p);
+        if (q >= eof) return nospace(a, tile0, p, sh);
         const u32 c = rd(q);
         if (c == ' ') break;
-        if (c == '\n' || c == '\r') return nospace(a, tile0, p);
+        if (c == '\n' || c == '\r') return nospace(a, tile0, p, sh);
         ++q;
     }
     const u64 sp1 = q++;
@@ -385,7 +446,7 @@ __device__ void process_header(ScanShared& sh, const ScanArgs& a, u64 tile0, u32
                 continue;
             }
             const u32 b = __builtin_ctz(ev);
-            if ((eol >> b) & 1u) return nospace(a, tile0, p);
+            if ((eol >> b) & 1u) return nospace(a, tile0, p, sh);
             sp1 = (int)(q + b);
             const u32 keep = ~((2u << b) - 1u) & 0xFu;
             sp &= keep;
@@ -464,15 +525,21 @@ struct TileCount {
 
 // line-terminator bitmap of the staged tile t, block scan, and publication of its aggregate
 // (R1: universal newlines: '\n', '\r\n' and a lone '\r' each end one line)
-__device__ TileCount count_tile(ScanShared& sh, const ScanArgs& a, u32 t, int tid, int lane, int wid) {
+__device__ __forceinline__ TileCount count_tile(ScanShared& sh, const ScanArgs& a, u32 t, int tid, int lane, int wid,
+                                bool publish = true) {
     const u64 tile0 = (u64)t * TILE;
     const u32 tlen = (u32)min((u64)TILE, a.len - tile0);
     const u32 nb = (u32)min((u64)(TILE + HALO), a.avail - tile0);
     const u32 s0 = tid * SEG;
     TileCount tc;
     tc.tmask = 0;
-    if (s0 < tlen) {
-        u64 nl = 0, cr = 0, hi = 0;
+    if (s0 >= tlen) {
+        sh.bsp[tid] = 0;
+        sh.bcol[tid] = 0;
+        sh.beol[tid] = 0;
+    } else {
+        u64 nl = 0, cr = 0, sp = 0, col = 0;
+        u32 hiw = 0;
 #pragma unroll
         for (int qv = 0; qv < SEG / 16; ++qv) {
             const uint4 v = *(const uint4*)(sh.buf + 16 + s0 + qv * 16);
@@ -480,19 +547,39 @@ __device__ TileCount count_tile(ScanShared& sh, const ScanArgs& a, u32 t, int ti
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const int sh4 = qv * 16 + k * 4;
-                nl |= (u64)eq4(w[k], 0x0A0A0A0Au) << sh4;
-                cr |= (u64)eq4(w[k], 0x0D0D0D0Du) << sh4;
-                hi |= (u64)hi4(w[k]) << sh4;
+                const u32 c = classify4(w[k]);
+                nl |= (u64)gather4<0>(c) << sh4;
+                cr |= (u64)gather4<1>(c) << sh4;
+                sp |= (u64)gather4<2>(c) << sh4;
+                col |= (u64)gather4<3>(c) << sh4;
+                hiw |= w[k];
             }
         }
         const u64 nxt = (s0 + SEG < nb && sh.buf[16 + s0 + SEG] == '\n') ? 1ull : 0ull;
         tc.tmask = nl | (cr & ~((nl >> 1) | (nxt << 63)));
+        u64 eol = nl | cr;
+        u64 hi = 0;
+        if (hiw & 0x80808080u) {  // rare: exact per-byte high-bit mask for the UTF-8 check
+#pragma unroll
+            for (int qv = 0; qv < SEG / 16; ++qv) {
+                const uint4 v = *(const uint4*)(sh.buf + 16 + s0 + qv * 16);
+                const u32 w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int k = 0; k < 4; ++k) hi |= (u64)hi4(w[k]) << (qv * 16 + k * 4);
+            }
+        }
         const u32 valid = tlen - s0;
         if (valid < SEG) {
             const u64 vm = (1ull << valid) - 1ull;
             tc.tmask &= vm;
             hi &= vm;
+            sp &= vm;
+            col &= vm;
+            eol &= vm;
         }
+        sh.bsp[tid] = sp;
+        sh.bcol[tid] = col;
+        sh.beol[tid] = eol;
         if (hi) {
             atomicOr(&sh.flags, 1u);
             if (!utf8_segment_ok(sh, (int)s0, (int)min(valid, (u32)SEG), (int)nb)) atomicOr(&sh.flags, 2u);
@@ -517,7 +604,7 @@ __device__ TileCount count_tile(ScanShared& sh, const ScanArgs& a, u32 t, int ti
     }
     tc.wexcl = wexcl;
     tc.tot = tot;
-    if (tid == 0) {  // publish: tile 0 is inclusive at once, every other tile its aggregate
+    if (publish && tid == 0) {  // publish: tile 0 is inclusive at once, every other tile its aggregate
         const u64 tag = (u64)(2u * a.epoch + (t == 0 ? 1u : 0u)) << 32;
         agent_store(&a.tiles[t], tag | tot);
     }
@@ -564,6 +651,8 @@ __global__ __launch_bounds__(WG) void scan_kernel(ScanArgs a) {
         sh.nkeys = 0;
         sh.created = 0;
         sh.flags = 0;
+        sh.buffered = 0;
+        sh.spec = 0;
         sh.tile = atomicAdd(&a.st->ticket, 1u);
     }
     const u64 base_lines = a.st->lines[a.par];
@@ -651,6 +740,501 @@ __global__ __launch_bounds__(WG) void scan_kernel(ScanArgs a) {
         if (sh.flags & 1u) atomicOr(&a.st->nonascii, 1u);
         if (sh.flags & 2u) atomicOr(&a.st->utf8_bad, 1u);
     }
+}
+
+// =====================================================================================
+// chunk kernel (v3): a workgroup owns a contiguous chunk of tiles and walks it in order, so
+// the line count is local; the chunk's starting line phase is guessed from the FASTQ record
+// structure, results are buffered (LDS table + the workgroup's cold list + buffered exotic
+// records / errors) and committed once the chunk's exact prefix (one chunk-level look-back)
+// confirms the guess.  A wrong/unsure guess, a buffer overflow or -s re-runs the chunk with
+// the exact prefix.  Correctness never depends on the guess.
+// =====================================================================================
+
+// every 4th line start of tile t -> sh.hdr (block scan, no shared counter)
+__device__ __forceinline__ void collect_headers(ScanShared& sh, const ScanArgs& a, u32 t, const TileCount& tc, u64 L0, int tid,
+                                int lane, int wid) {
+    const u64 tile0 = (u64)t * TILE;
+    const u32 s0 = tid * SEG;
+    u64 L = L0 + tc.wexcl + (tc.x - tc.c);
+    // pass 1: count this thread's headers
+    u32 n = 0;
+    {
+        u64 m = tc.tmask, l = L;
+        while (m) {
+            const int j = __ffsll((long long)m) - 1;
+            m &= m - 1;
+            l += 1;
+            if ((l & 3ull) == 0) {
+                const u64 gp = tile0 + s0 + (u32)j + 1u;
+                const bool mine = gp < a.len || (a.own_end && gp == a.len && gp < a.avail);
+                n += (mine && (a.max_records <= 0 || (i64)(l >> 2) < a.max_records)) ? 1u : 0u;
+            }
+        }
+    }
+    const bool own0 = t == 0 && tid == 0 && a.own_start && (L0 & 3ull) == 0 && a.avail > 0 &&
+                      (a.max_records <= 0 || (i64)(L0 >> 2) < a.max_records);
+    const u32 mine0 = own0 ? 1u : 0u;
+    u32 x = n + mine0;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const u32 y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) sh.hscan[wid] = x;
+    __syncthreads();
+    u32 base = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < WG / 64; ++w) {
+        const u32 v = sh.hscan[w];
+        base += w < wid ? v : 0u;
+        tot += v;
+    }
+    u32 o = base + x - (n + mine0);
+    if (own0) sh.hdr[o++] = 0;
+    {
+        u64 m = tc.tmask, l = L;
+        while (m) {
+            const int j = __ffsll((long long)m) - 1;
+            m &= m - 1;
+            l += 1;
+            if ((l & 3ull) == 0) {
+                const u32 p = s0 + (u32)j + 1u;
+                const u64 gp = tile0 + p;
+                const bool mine = gp < a.len || (a.own_end && gp == a.len && gp < a.avail);
+                if (mine && (a.max_records <= 0 || (i64)(l >> 2) < a.max_records)) sh.hdr[o++] = (u16)p;
+            }
+        }
+    }
+    if (tid == 0) sh.nhdr = tot;
+}
+
+// Guess P = (lines before the chunk) mod 4 from the first PHASE_LINES complete lines of the
+// staged first tile: with lines indexed P+k+1 after the k-th terminator, a FASTQ record has a
+// header ('@') at phase 0, '+' at phase 2 and equal seq/qual lengths at phases 1/3.  Exactly
+// one consistent P -> the guess; otherwise -1 (unsure).  One lane, once per chunk.
+__device__ __forceinline__ int infer_phase(const ScanShared& sh, u32 tlen) {
+    const u8* lb = sh.buf + 16;
+    bool ok[4] = {true, true, true, true};
+    int seqlen[4] = {-1, -1, -1, -1};
+    int prev = -1, k = 0;
+    for (int w = 0; w < WG && k < PHASE_LINES; ++w) {
+        u64 m = sh.tbits[w];
+        while (m && k < PHASE_LINES) {
+            const int e = w * SEG + (__ffsll((long long)m) - 1);
+            m &= m - 1;
+            if (prev >= 0) {  // the line [prev+1, e) (less a '\r' of "\r\n")
+                const int st = prev + 1;
+                int en = e;
+                if (lb[e] == '\n' && e - 1 >= st && lb[e - 1] == '\r') en = e - 1;
+                const int len = en - st;
+                const u32 c0 = len > 0 ? lb[st] : 0u;
+#pragma unroll
+                for (int P = 0; P < 4; ++P) {
+                    const int ph = (P + k + 1) & 3;
+                    if (ph == 0) ok[P] &= c0 == '@';
+                    else if (ph == 2) ok[P] &= c0 == '+';
+                    else if (ph == 1) seqlen[P] = len;
+                    else {
+                        if (seqlen[P] >= 0) ok[P] &= seqlen[P] == len;
+                        seqlen[P] = -1;
+                    }
+                }
+                ++k;
+            }
+            prev = e;
+        }
+    }
+    (void)tlen;
+    if (k < 8) return -1;
+    int found = -1, nfound = 0;
+#pragma unroll
+    for (int P = 0; P < 4; ++P)
+        if (ok[P]) {
+            found = P;
+            ++nfound;
+        }
+    return nfound == 1 ? found : -1;
+}
+
+// insert up to B entries with their first slot loads issued together (latency overlap)
+template <int B>
+__device__ __forceinline__ u32 insert_many(const ScanArgs& a, const u64 (&key)[B], const u64 (&cnt)[B],
+                                           const u64 (&ord)[B], const bool (&valid)[B]) {
+    const Table& T = a.tab;
+    uint4 w0[B], w1[B];
+    u64 h[B];
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+        h[b] = mix64(key[b]) & T.mask;
+        if (valid[b]) {
+            const GSlot* sl = &T.slots[h[b]];
+            w0[b] = *(const uint4*)sl;
+            w1[b] = *((const uint4*)sl + 1);
+        }
+    }
+    u32 made = 0;
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+        if (!valid[b]) continue;
+        const u64 k = ((u64)w0[b].y << 32) | w0[b].x;
+        if (k == key[b]) {  // the common case: the code is already in the table
+            GSlot* sl = &T.slots[h[b]];
+            atomicAdd((unsigned long long*)&sl->count, (unsigned long long)cnt[b]);
+            const u64 first = ((u64)w1[b].y << 32) | w1[b].x;
+            if (ord[b] < first) atomicMin((unsigned long long*)&sl->first, (unsigned long long)ord[b]);
+            if (w1[b].z < a.file_tag) atomicMax(&sl->last_tag, a.file_tag);
+        } else {
+            made += global_insert(T, a.st, key[b], cnt[b], ord[b], a.file_tag) ? 1u : 0u;
+        }
+    }
+    return made;
+}
+
+// publish the LDS table and/or the cold list / buffered side effects into HBM (all threads)
+__device__ __forceinline__ void commit_buffers(ScanShared& sh, const ScanArgs& a, bool table, int tid) {
+    __syncthreads();
+    u32 made = 0;
+    if (table) {
+        for (int i0 = tid; i0 < NS; i0 += 2 * WG) {
+            u64 key[2], cnt[2], ord[2];
+            bool v[2];
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                const int i = i0 + b * WG;
+                v[b] = i < NS && sh.key[i] != 0;
+                key[b] = v[b] ? sh.key[i] : 0;
+                cnt[b] = v[b] ? sh.cnt[i] : 0;
+                ord[b] = v[b] ? make_ord(a, sh.mino[i]) : 0;
+            }
+            made += insert_many<2>(a, key, cnt, ord, v);
+        }
+    }
+    const u32 nc = min(sh.ncold, a.cold_cap);
+    const u64* cl = a.cold + 2ull * (u64)blockIdx.x * a.cold_cap;
+    for (u32 i0 = tid; i0 < nc; i0 += 2 * WG) {
+        u64 key[2], cnt[2], ord[2];
+        bool v[2];
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            const u32 i = i0 + b * WG;
+            v[b] = i < nc;
+            key[b] = v[b] ? cl[2 * i] : 0;
+            ord[b] = v[b] ? cl[2 * i + 1] : 0;
+            cnt[b] = 1;
+        }
+        made += insert_many<2>(a, key, cnt, ord, v);
+    }
+    if (made) atomicAdd(&sh.created, made);
+    // buffered exotic records and the first "no space" error
+    const u32 ne = min(sh.nexo, (u32)EXO_BUF);
+    for (u32 k = tid; k < ne; k += WG) {
+        const u64 n = sh.exo_len[k];
+        const u64 i = atomicAdd((unsigned long long*)&a.st->n_exotic, 1ull);
+        const u64 po = atomicAdd((unsigned long long*)&a.st->exo_pool_used, (unsigned long long)n);
+        if (i < a.tab.exo_cap && po + n <= a.tab.exo_pool_cap) {
+            a.tab.exo_ord[i] = make_ord(a, sh.exo_p[k]);
+            a.tab.exo_off[i] = po;
+            a.tab.exo_len[i] = (u32)n;
+            for (u64 q = 0; q < n; ++q) a.tab.exo_pool[po + q] = a.buf[sh.exo_start[k] + q];
+        } else {
+            atomicOr(&a.st->cap_flags, 4u);
+        }
+    }
+    if (tid == 0 && sh.err_off != 0xFFFFFFFFu)
+        atomicMin((unsigned long long*)&a.st->err_nospace, (unsigned long long)(a.file_offset + sh.err_off));
+    __syncthreads();
+    if (table)
+        for (int i = tid; i < NS; i += WG) {
+            sh.key[i] = 0;
+            sh.cnt[i] = 0;
+            sh.mino[i] = 0xFFFFFFFFu;
+        }
+    if (tid == 0) {
+        if (table) sh.nkeys = 0;
+        sh.ncold = 0;
+        sh.nexo = 0;
+        sh.err_off = 0xFFFFFFFFu;
+    }
+    __syncthreads();
+}
+
+// drop everything buffered (a failed speculation)
+__device__ __forceinline__ void discard_buffers(ScanShared& sh, int tid) {
+    __syncthreads();
+    for (int i = tid; i < NS; i += WG) {
+        sh.key[i] = 0;
+        sh.cnt[i] = 0;
+        sh.mino[i] = 0xFFFFFFFFu;
+    }
+    if (tid == 0) {
+        sh.nkeys = 0;
+        sh.ncold = 0;
+        sh.nexo = 0;
+        sh.err_off = 0xFFFFFFFFu;
+        sh.spec_bad = 0;
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ bool uniform_flag(u32 v) { return __builtin_amdgcn_readfirstlane(v) != 0; }
+
+// code bytes [start, start+n) -> fast key with v_perm SWAR, 4 bytes per step (false if outside
+// the fast alphabet).  Byte index i = (c >> 1) & 7 selects the expected byte (A C T G - + - N)
+// and its symbol (A1 C2 G3 T4 N5 +6); a byte is valid iff it equals the expected one.
+__device__ __forceinline__ bool encode_perm(const u8* lb, u32 start, u32 n, u64& key) {
+    if (n < 1 || n > (u32)MAXSYM) return false;
+    const u32 b4 = start & ~3u;
+    const u32 sh8 = (start & 3u) * 8u;
+    u32 w[7];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) w[k] = *(const u32*)(lb + b4 + 4 * k);
+    u64 kk = 0;
+    u32 bad = 0;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        const u32 a = sh8 ? (u32)((((u64)w[k + 1] << 32) | w[k]) >> sh8) : w[k];
+        const u32 idx = (a >> 1) & 0x07070707u;
+        const u32 expect = __builtin_amdgcn_perm(0x4E002B00u, 0x47544341u, idx);
+        const u32 sym = __builtin_amdgcn_perm(0x05000600u, 0x03040201u, idx);
+        const int left = (int)n - 4 * k;  // bytes of the code in this word
+        const u32 vm = left >= 4 ? 0xFFFFFFFFu : left <= 0 ? 0u : (0xFFFFFFFFu >> (32 - 8 * left));
+        bad |= (expect ^ a) & vm;
+        const u32 sv = sym & vm;
+        const u32 packed = (sv & 0x7u) | ((sv >> 5) & 0x38u) | ((sv >> 10) & 0x1C0u) | ((sv >> 15) & 0xE00u);
+        kk |= (u64)packed << (12 * k);
+    }
+    key = kk;
+    return bad == 0;
+}
+
+// R2 via the tile's ' ' / ':' / line-end bitmaps: first ' ', then the next ' ' or line end,
+// then the last ':' between them.  Lines that reach past the tile's bitmaps fall back to the
+// word-scan parser.
+__device__ __forceinline__ void slow_header(ScanShared& sh, const ScanArgs& a, u64 tile0, u32 p, u32 nb, int r,
+                                         u32 start, u32 n) {
+    if (r == 2) process_header(sh, a, tile0, p, nb);
+    else if (r == 1) nospace(a, tile0, p, sh);
+    else exotic_record(a, tile0, p, start, n, sh, nb);
+}
+
+// returns 0 parsed (code at [start, start+n)), 1 no ' ' on the line, 2 fall back to the word scan
+__device__ __forceinline__ int locate_code_bm(const ScanShared& sh, u32 p, u32 tlen, u32& start, u32& n) {
+    u32 w = p >> 6;
+    if (p >= tlen) return 2;
+    const u64 m0 = ~0ull << (p & 63u);
+    u64 sp = sh.bsp[w] & m0, eol = sh.beol[w] & m0;
+    while (!(sp | eol)) {
+        if (++w * 64u >= tlen) return 2;
+        sp = sh.bsp[w];
+        eol = sh.beol[w];
+    }
+    const u32 b = __ffsll((long long)(sp | eol)) - 1;
+    if ((eol >> b) & 1ull) return 1;
+    const u32 sp1 = w * 64u + b;
+    const u64 m1 = b == 63u ? 0ull : (~0ull << (b + 1u));
+    sp &= m1;
+    eol &= m1;
+    while (!(sp | eol)) {
+        if (++w * 64u >= tlen) return 2;
+        sp = sh.bsp[w];
+        eol = sh.beol[w];
+    }
+    const u32 end = w * 64u + (u32)(__ffsll((long long)(sp | eol)) - 1);
+    // last ':' in (sp1, end)
+    u32 wc = end >> 6;
+    u64 cm = sh.bcol[wc] & ((1ull << (end & 63u)) - 1ull);
+    const u32 ws = sp1 >> 6;
+    u32 st = sp1 + 1u;
+    for (;;) {
+        if (wc == ws) cm &= (sp1 & 63u) == 63u ? 0ull : (~0ull << ((sp1 & 63u) + 1u));
+        if (cm) {
+            st = wc * 64u + 64u - (u32)__clzll((long long)cm);
+            break;
+        }
+        if (wc == ws) break;
+        cm = sh.bcol[--wc];
+    }
+    start = st;
+    n = end - st;
+    return 0;
+}
+
+// R2 via the tile's ' ' / ':' / line-end bitmaps: first ' ', then the next ' ' or line end,
+// then the last ':' between them.  Lines that reach past the tile's bitmaps fall back to the
+// word-scan parser (process_header).
+__device__ __forceinline__ void process_header_bm(ScanShared& sh, const ScanArgs& a, u64 tile0, u32 p, u32 tlen,
+                                                  u32 nb) {
+    u32 start = 0, n = 0;
+    const int r = locate_code_bm(sh, p, tlen, start, n);
+    u64 key = 0;
+    bool fast = false;
+    if (r == 0) {
+        if (a.ablate & 2u) {
+            asm volatile("" ::"v"(start), "v"(n));
+            return;
+        }
+        fast = encode_perm(sh.buf + 16, start, n, key);
+    }
+    if (fast) count_code(sh, a, tile0, p, key);
+    else slow_header(sh, a, tile0, p, nb, r, start, n);
+}
+
+// walk tiles [tb, te) of the range; L0 = line index (absolute, or mod-4 guess) at tile tb.
+// parse = false: count only.  (exact is kept for symmetry: with an exact phase a full cold
+// list falls back to direct HBM inserts inside lds_insert.)
+// Returns the line terminators in [tb, te).
+__device__ __forceinline__ u64 walk_chunk(ScanShared& sh, const ScanArgs& a, u32 tb, u32 te, u64 L0, bool parse, bool exact, int tid,
+                          int lane, int wid) {
+#ifdef FR_STAMPS
+    u64 stamps[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    u64 last_ = __builtin_amdgcn_s_memtime();
+#endif
+    TileRegs r;
+    tile_fetch(a, tb, r, tid);
+    tile_stage(sh, r, tid);
+    __syncthreads();
+    TileCount tc = count_tile(sh, a, tb, tid, lane, wid, false);
+    u64 lines = 0;
+    STAMP(4);
+    for (u32 t = tb; t < te; ++t) {
+        const bool more = t + 1 < te;
+        if (more) tile_fetch(a, t + 1, r, tid);  // lands while this tile is parsed
+        if (parse && !uniform_flag(sh.spec_bad)) {
+            collect_headers(sh, a, t, tc, L0 + lines, tid, lane, wid);
+            __syncthreads();
+            STAMP(0);
+            const u64 tile0 = (u64)t * TILE;
+            const u32 nb = (u32)min((u64)(TILE + HALO), a.avail - tile0);
+            const u32 tlen = (u32)min((u64)TILE, a.len - tile0);
+            const u32 nh = sh.nhdr;
+            if (!(a.ablate & 1u))
+                for (u32 h = tid; h < nh; h += WG) process_header_bm(sh, a, tile0, sh.hdr[h], tlen, nb);
+        }
+        __syncthreads();
+        STAMP(1);
+        lines += tc.tot;
+        if (more) {
+            tile_stage(sh, r, tid);
+            __syncthreads();
+            STAMP(2);
+            tc = count_tile(sh, a, t + 1, tid, lane, wid, false);
+            STAMP(3);
+        }
+    }
+#ifdef FR_STAMPS
+    if (tid == 0)
+        for (int i = 0; i < 8; ++i)
+            if (stamps[i]) atomicAdd((unsigned long long*)&a.st->stamp[i], (unsigned long long)stamps[i]);
+#endif
+    return lines;
+}
+
+__global__ __launch_bounds__(WG, 2) void chunk_kernel(ScanArgs a) {
+    __shared__ ScanShared sh;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wid = tid >> 6;
+    for (int i = tid; i < NS; i += WG) {
+        sh.key[i] = 0;
+        sh.cnt[i] = 0;
+        sh.mino[i] = 0xFFFFFFFFu;
+    }
+    if (tid < 2) *(uint4*)(sh.buf + 16 + TILE + HALO + 16 * tid) = make_uint4(0u, 0u, 0u, 0u);
+    if (tid == 0) {
+        sh.nkeys = 0;
+        sh.created = 0;
+        sh.flags = 0;
+        sh.buffered = 1;
+        sh.spec = 0;
+        sh.spec_bad = 0;
+        sh.ncold = 0;
+        sh.nexo = 0;
+        sh.err_off = 0xFFFFFFFFu;
+    }
+    const u64 base_lines = a.st->lines[a.par];
+    for (;;) {
+        if (tid == 0) sh.chunk = atomicAdd(&a.st->ticket, 1u);
+        __syncthreads();
+        const u32 c = sh.chunk;
+        if (c >= a.num_chunks) break;
+        const u32 tb = c * a.chunk_tiles;
+        const u32 te = min(tb + a.chunk_tiles, a.num_tiles);
+        // ---- the line phase at the chunk start: exact for chunk 0, else guessed ----------
+#ifdef FR_STAMPS
+        u64 stamps[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        u64 last_ = __builtin_amdgcn_s_memtime();
+#endif
+        int P = -1;
+        if (c == 0) {
+            P = (int)(base_lines & 3ull);
+        } else if (a.max_records <= 0) {
+            TileRegs r;
+            tile_fetch(a, tb, r, tid);
+            tile_stage(sh, r, tid);
+            __syncthreads();
+            const TileCount tc0 = count_tile(sh, a, tb, tid, lane, wid, false);
+            sh.tbits[tid] = tc0.tmask;
+            __syncthreads();
+            if (tid == 0) sh.phase = infer_phase(sh, 0);
+            __syncthreads();
+            P = sh.phase;
+        }
+        STAMP(5);
+        // pass 0: exact (chunk 0) / speculative (guessed phase) / count-only (unsure, -s);
+        // pass 1 (only when pass 0 cannot be kept): exact, after the chunk-level look-back
+        const bool spec = c != 0 && P >= 0;
+        u64 L0 = c == 0 ? base_lines : (u64)(P >= 0 ? P : 0);
+        bool parse = c == 0 || spec;
+        bool exact = c == 0;
+        if (tid == 0) sh.spec = spec ? 1u : 0u;
+        __syncthreads();
+        for (int pass = 0;; ++pass) {
+            const u64 cnt = walk_chunk(sh, a, tb, te, L0, parse, exact, tid, lane, wid);
+#ifdef FR_STAMPS
+            last_ = __builtin_amdgcn_s_memtime();
+#endif
+            if (pass == 1) break;
+            // ---- publish the chunk's aggregate, resolve its exact prefix ---------------
+            if (tid == 0) {
+                sh.spec = 0;
+                agent_store(&a.tiles[c], ((u64)(2u * a.epoch + (c == 0 ? 1u : 0u)) << 32) | (u32)cnt);
+            }
+            if (wid == 0) {
+                const u64 ex = lookback(a, c, (u32)cnt, lane);
+                if (lane == 0) {
+                    sh.tile_excl = ex;
+                    if (c == a.num_chunks - 1) a.st->lines[a.par ^ 1u] = base_lines + ex + cnt;
+                }
+            }
+            __syncthreads();
+            STAMP(6);
+            const u64 exact_L = base_lines + sh.tile_excl;
+            const bool keep = c == 0 || (spec && (u32)P == (u32)(exact_L & 3ull) && !uniform_flag(sh.spec_bad));
+            if (keep) break;
+            discard_buffers(sh, tid);
+            L0 = exact_L;
+            parse = true;
+            exact = true;
+        }
+        commit_buffers(sh, a, true, tid);
+        STAMP(7);
+#ifdef FR_STAMPS
+        if (tid == 0)
+            for (int i = 5; i < 8; ++i) atomicAdd((unsigned long long*)&a.st->stamp[i], (unsigned long long)stamps[i]);
+#endif
+    }
+    __syncthreads();
+    if (tid == 0) {
+        if (sh.created) atomicAdd((unsigned long long*)&a.st->n_keys, (unsigned long long)sh.created);
+        if (sh.flags & 1u) atomicOr(&a.st->nonascii, 1u);
+        if (sh.flags & 2u) atomicOr(&a.st->utf8_bad, 1u);
+    }
+}
+
+hipError_t launch_chunk_scan(const ScanArgs& a, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(chunk_kernel, dim3(grid), dim3(WG), 0, s, a);
+    return hipGetLastError();
 }
 
 hipError_t launch_scan(const ScanArgs& a, int grid, hipStream_t s) {

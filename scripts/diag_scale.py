@@ -1,6 +1,6 @@
 """Diagnostic: device-feed SYN-v1 data at several launch sizes / totals; report records."""
 import sys, time
-sys.path.insert(0, ".")
+import os; sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from frender_amd import _lib, synth
 
 sheet = synth.make_sheet(96, 8, 8)

@@ -11,8 +11,9 @@ tally kernel over every byte (header scan, code pack, LDS-privatised hash count)
 -> compaction + first-occurrence ordering -> Hamming classification of every
 unique code (+ with --rc the rc pass, per-name call and pass B).  With N>1 GPUs
 (torchrun, one process per GPU) each rank scans its own 100M reads (weak
-scaling) and the per-GPU tables are merged over RCCL (all-gather of the
-compacted tables, merged into rank 0's table on the GPU) before classification.
+scaling) and the per-GPU tables are merged over RCCL (binary-tree send/recv of
+the compacted tables, merged on the GPU, frender_amd/dist.py) into rank 0, which
+classifies the merged table.
 
 Prints ONE JSON line (rank 0): value = total reads of all ranks / max-over-ranks
 step time, plus roofline (tally kernel, HIP events on the library's stream) and
@@ -47,6 +48,8 @@ def parse():
     ap.add_argument("--cpu-reads", type=int, default=2_000_000, help="bounded sample for the CPU baseline")
     ap.add_argument("--cpu-cores", type=int, default=8)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL, one GPU per rank); gloo only to rehearse N ranks on one GPU")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"),
                     help="per-launch HBM bytes of the tally kernel from rocprofv3 PMC (null if absent)")
     return ap.parse_args()
@@ -93,10 +96,16 @@ def main():
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "gloo":  # rehearsal: every rank on this box's GPU(s)
+            local = local % torch.cuda.device_count()
+            torch.cuda.set_device(local)
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from frender_amd import _lib, synth
+    from frender_amd.dist import device_callbacks, tree_merge
     from frender_amd.host import reverse_complement
     from frender_amd.scan import _sheet_names
 
@@ -109,6 +118,7 @@ def main():
     buf = ctx.device_alloc(nbytes + 64)
     ctx.synth_device(buf, rank * n, n, args.read_len, 1, sheet.idx1, sheet.idx2)
     names, nid = _sheet_names(sheet.ids)
+    merge_cbs = device_callbacks(ctx)
     idx2rc = [reverse_complement(x) for x in sheet.idx2]
 
     def step():
@@ -118,22 +128,8 @@ def main():
         st = ctx.end_file()
         assert st.records == n and st.error == 0, (st.records, st.error)
         U, _, _ = ctx.finalize()
-        if world > 1:
-            import torch
-            sizes = torch.zeros(world, dtype=torch.int64, device="cuda")
-            mine = torch.tensor([U], dtype=torch.int64, device="cuda")
-            dist.all_gather_into_tensor(sizes, mine)
-            cap = int(sizes.max().item())
-            loc = torch.empty((3, cap), dtype=torch.int64, device="cuda")
-            ctx.export_unique_device(loc[0].data_ptr(), loc[1].data_ptr(), loc[2].data_ptr(), cap)
-            allt = torch.empty((world, 3, cap), dtype=torch.int64, device="cuda")
-            dist.all_gather_into_tensor(allt, loc)
-            torch.cuda.synchronize()
-            if rank == 0:
-                for r in range(1, world):
-                    ctx.merge_unique_device(allt[r, 0].data_ptr(), allt[r, 1].data_ptr(), allt[r, 2].data_ptr(),
-                                            int(sizes[r].item()))
-                ctx.finalize()
+        if world > 1:  # weak-scaled shards, one exchange: tree merge of the tables (dist.py)
+            U = tree_merge(dist, "cuda", U, *merge_cbs)
         if rank == 0 or world == 1:
             ctx.set_sheet(sheet.idx1, sheet.idx2, idx2rc, nid, len(names))
             ctx.classify(args.nsubs, args.rc, to_host=False)
@@ -164,7 +160,7 @@ def main():
     ms = dt / args.steps * 1e3
     if world > 1:
         import torch
-        x = torch.tensor([ms], dtype=torch.float64, device="cuda")
+        x = torch.tensor([ms], dtype=torch.float64, device="cpu" if args.dist_backend == "gloo" else "cuda")
         dist.all_reduce(x, op=dist.ReduceOp.MAX)
         ms = float(x.item())
 
@@ -188,7 +184,7 @@ def main():
         cpu = None if args.no_cpu else cpu_baseline(args)
         value = world * n / (ms / 1e3) / 1e6
         out = {
-            "metric": "M reads/sec scanned+classified (96 samples, 8+8bp, n=1)",
+            "metric": "M reads/sec scanned+classified (96 samples, 8+8bp, n=1) at 1/2/4/8 MI355X",
             "value": round(value, 2),
             "unit": "M reads/s",
             "n_gpus": world,
@@ -206,10 +202,10 @@ def main():
                                    f"decoded FASTQ resident in HBM",
                        "reads_per_gpu": n, "bytes_per_record": reclen, "samples": args.samples,
                        "nsubs": args.nsubs, "rc": bool(args.rc), "unique_codes": int(U),
-                       "parallelism": f"dp{world} (record shards) + RCCL table merge" if world > 1 else "1 GPU"},
+                       "parallelism": f"dp{world} (record shards) + {'RCCL' if args.dist_backend == 'nccl' else 'gloo'} tree merge of the tables" if world > 1 else "1 GPU"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "fr::scan_kernel", "bytes_per_launch": int(per_launch_bytes),
+                         "kernel": "fr::chunk_kernel", "bytes_per_launch": int(per_launch_bytes),
                          "avg_launch_ms": round(per_launch_ms, 4), "launches_per_step": int(launches)},
             "cpu_baseline": cpu,
         }

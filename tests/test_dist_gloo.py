@@ -1,0 +1,76 @@
+"""The multi-GPU merge protocol (frender_amd/dist.py) over gloo on CPU, world sizes 2-5.
+
+Each rank holds a random table {key: (count, first)}; the tree merge must leave
+rank 0 with the exact union (count = sum, first = min), as the reference's
+parent-process dict merge does (frender.py:199-205).  The device merge kernel is
+covered by tests/test_gpu_scan.py::test_merge_unique_device.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from frender_amd.dist import tree_merge
+
+
+def _table(rank, seed):
+    rng = np.random.default_rng(seed * 100 + rank)
+    n = int(rng.integers(0, 50)) if rank % 3 != 2 else 0  # some ranks are empty
+    keys = rng.choice(np.arange(1, 80), size=n, replace=False)
+    return {int(k): (int(rng.integers(1, 1000)), int(rng.integers(0, 1 << 50))) for k in keys}
+
+
+def _worker(rank, world, port, seed, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    table = dict(_table(rank, seed))
+
+    def export(buf, n):
+        ks = sorted(table)
+        assert len(ks) == n
+        buf[0] = torch.tensor(ks, dtype=torch.int64)
+        buf[1] = torch.tensor([table[k][0] for k in ks], dtype=torch.int64)
+        buf[2] = torch.tensor([table[k][1] for k in ks], dtype=torch.int64)
+
+    def merge(buf, n):
+        for k, c, f in zip(buf[0].tolist(), buf[1].tolist(), buf[2].tolist()):
+            c0, f0 = table.get(k, (0, 1 << 62))
+            table[k] = (c0 + c, min(f0, f))
+
+    n = tree_merge(dist, "cpu", len(table), export, merge, lambda: len(table))
+    if rank == 0:
+        out.put((n, sorted(table.items())))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("world,seed", [(2, 1), (3, 2), (4, 3), (5, 4)])
+def test_tree_merge_gloo(world, seed):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, seed, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    n, got = q.get(timeout=120)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    want = {}
+    for r in range(world):
+        for k, (c, f) in _table(r, seed).items():
+            c0, f0 = want.get(k, (0, 1 << 62))
+            want[k] = (c0 + c, min(f0, f))
+    assert got == sorted(want.items())
+    assert n == len(want)

@@ -281,3 +281,38 @@ def test_many_tiles_per_workgroup(lib, monkeypatch, grid, cap, chunk):
         assert list(zip(lib.decode_keys(keys), counts.tolist())) == list(exp.items())
     finally:
         c.close()
+
+
+# ---------------------------------------------------------------------------------------
+# multi-GPU merge kernel: export one context's table, merge it into another's
+# ---------------------------------------------------------------------------------------
+def test_merge_unique_device(lib):
+    """Shard a dataset over 3 contexts (ranks); merging their compacted tables into
+    rank 0 through fr_export_unique_device / fr_merge_unique_device must equal one
+    context scanning the shards as consecutive files (count = sum, first = min)."""
+    from frender_amd import synth
+    from frender_amd.dist import device_callbacks
+    import torch
+    sheet = synth.make_sheet(24, 8, 8)
+    shards = [synth.generate_bytes(sheet, 50_000 * i, 50_000, R=8, seed=3) for i in range(3)]
+    ref = lib.Context(device=0, chunk_bytes=1 << 20, table_slots=1 << 12)
+    ranks = [lib.Context(device=0, chunk_bytes=1 << 20, table_slots=1 << 12) for _ in shards]
+    try:
+        want = gpu_tally(ref, lib, shards, mode="device")
+        kref, cref, fref = ref.unique()
+        for r, c in enumerate(ranks):  # rank r scans shard r as its file r (global file index)
+            gpu_tally(c, lib, [b""] * r + [shards[r]], mode="device")
+        export0, merge0, refin0 = device_callbacks(ranks[0])
+        for c in ranks[1:]:
+            export, _, _ = device_callbacks(c)
+            buf = torch.empty((3, c.U), dtype=torch.int64, device="cuda")
+            export(buf, c.U)
+            merge0(buf, c.U)
+        refin0()
+        k, cnt, f = ranks[0].unique()
+        assert np.array_equal(k, kref) and np.array_equal(cnt, cref) and np.array_equal(f, fref)
+        assert dict(zip(lib.decode_keys(k), cnt.tolist())) == want[0]
+    finally:
+        ref.close()
+        for c in ranks:
+            c.close()

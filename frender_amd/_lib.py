@@ -125,6 +125,7 @@ class Context:
         if err:
             raise FrenderError(f"fr_create: {err.decode()}")
         self.n_names = 0
+        self._sheet_cache: dict = {}
 
     def close(self):
         if self.h:
@@ -144,6 +145,24 @@ class Context:
 
     # ---- sheet ----------------------------------------------------------------------
     def set_sheet(self, idx1: list, idx2: list, idx2rc: list, name_id: list, n_names: int):
+        key = (tuple(idx1), tuple(idx2), tuple(idx2rc), tuple(name_id), n_names)
+        packed = self._sheet_cache.get(key)
+        if packed is None:
+            packed = self._pack_sheet(idx1, idx2, idx2rc, name_id)
+            if len(self._sheet_cache) >= 8:
+                self._sheet_cache.clear()
+            self._sheet_cache[key] = packed
+        p1, p2, p2rc, len1, len2, nid, cp, stride = packed
+        self.cp_stride = stride
+        self._sheet_keep = packed
+        self.n_names = n_names
+        self._ck(lib.fr_set_sheet(self.h, len(idx1), _ptr(p1), _ptr(len1), _ptr(p2), _ptr(len2), _ptr(p2rc),
+                                  _ptr(nid), n_names, _ptr(cp[0]), _ptr(cp[1]), _ptr(cp[2]), stride),
+                 "fr_set_sheet")
+
+    @staticmethod
+    def _pack_sheet(idx1, idx2, idx2rc, name_id):
+        """Host-side encoding of the sheet lists (case-folded, 3-bit packed + code points)."""
         S = len(idx1)
         l1 = [s.lower() for s in idx1]
         l2 = [s.lower() for s in idx2]
@@ -155,15 +174,11 @@ class Context:
         len2 = np.array([len(s) for s in l2], dtype=np.int32)
         nid = np.array(name_id, dtype=np.int32)
         stride = max([1] + [len(s) for s in l1 + l2])
-        self.cp_stride = stride
         cp = [np.zeros((S, stride), dtype=np.uint32) for _ in range(3)]
         for arr, strs in zip(cp, (l1, l2, l2rc)):
             for i, s in enumerate(strs):
                 arr[i, :len(s)] = [ord(ch) for ch in s]
-        self._sheet_keep = (p1, p2, p2rc, len1, len2, nid, cp)
-        self.n_names = n_names
-        self._ck(lib.fr_set_sheet(self.h, S, _ptr(p1), _ptr(len1), _ptr(p2), _ptr(len2), _ptr(p2rc), _ptr(nid),
-                                  n_names, _ptr(cp[0]), _ptr(cp[1]), _ptr(cp[2]), stride), "fr_set_sheet")
+        return p1, p2, p2rc, len1, len2, nid, cp, stride
 
     # ---- tally ----------------------------------------------------------------------
     def reset(self):

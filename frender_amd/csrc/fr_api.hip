@@ -55,6 +55,7 @@ struct fr_ctx {
     bool scanning = false;
     bool file_open = false;
     u32 file_tag = 0;
+    bool merged = false;  // the table holds ordinals merged from other contexts (any file tag)
     u64 file_offset = 0;
     i64 max_records = 0;
     int last_byte = -1;
@@ -70,6 +71,9 @@ struct fr_ctx {
     int32_t* d_name = nullptr;
     u32 *d_cp1 = nullptr, *d_cp2 = nullptr, *d_cp2rc = nullptr;
     int32_t *d_cpl1 = nullptr, *d_cpl2 = nullptr;
+    u8* d_sheet = nullptr;  // one device blob holding every sheet array above
+    u8* h_sheet = nullptr;  // its pinned staging copy
+    u64 sheet_cap = 0;
     int cp_stride = 0;
 
     // finalized table
@@ -340,15 +344,15 @@ void fr_destroy(fr_ctx* ctx) {
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->copy) (void)hipStreamSynchronize(ctx->copy);
     void* dev[] = {ctx->st, ctx->tiles, ctx->tab.slots, ctx->tab.ovf, ctx->tab.pres, ctx->tab.exo_ord,
-                   ctx->tab.exo_off, ctx->tab.exo_len, ctx->tab.exo_pool, ctx->dbuf[0], ctx->dbuf[1], ctx->d_i1,
-                   ctx->d_i2, ctx->d_i2rc, ctx->d_name, ctx->d_cp1, ctx->d_cp2, ctx->d_cp2rc, ctx->d_cpl1,
-                   ctx->d_cpl2, ctx->d_keys, ctx->d_counts, ctx->d_first, ctx->d_keys_s, ctx->d_counts_s,
+                   ctx->tab.exo_off, ctx->tab.exo_len, ctx->tab.exo_pool, ctx->dbuf[0], ctx->dbuf[1], ctx->d_sheet,
+                   ctx->d_keys, ctx->d_counts, ctx->d_first, ctx->d_keys_s, ctx->d_counts_s,
                    ctx->d_first_s, ctx->d_pos, ctx->d_perm, ctx->d_rank, ctx->d_counter, ctx->d_temp, ctx->d_pres_u,
                    ctx->d_pres_f, ctx->d_m1, ctx->d_m2, ctx->d_row, ctx->d_rm2, ctx->d_rrow, ctx->d_cls, ctx->d_rcls,
                    ctx->d_errw, ctx->d_errf, ctx->d_rcf, ctx->d_rcr, ctx->cold};
     for (void* p : dev)
         if (p) (void)hipFree(p);
     if (ctx->h_st) (void)hipHostFree(ctx->h_st);
+    if (ctx->h_sheet) (void)hipHostFree(ctx->h_sheet);
     for (int i = 0; i < 2; ++i) {
         if (ctx->pin[i]) (void)hipHostFree(ctx->pin[i]);
         if (ctx->copied[i]) (void)hipEventDestroy(ctx->copied[i]);
@@ -404,23 +408,52 @@ int fr_set_sheet(fr_ctx* ctx, int S, const uint64_t* idx1_packed, const int32_t*
                  const int32_t* name_id, int n_names, const uint32_t* idx1_cp, const uint32_t* idx2_cp,
                  const uint32_t* idx2rc_cp, int cp_stride) {
     if (S < 0 || S > 32767) return fail(ctx, FR_ERR_INVALID, "sheet rows must be in [0, 32767]");
-    CK(hipStreamSynchronize(ctx->stream));
-    void* old[] = {ctx->d_i1, ctx->d_i2, ctx->d_i2rc, ctx->d_name, ctx->d_cp1, ctx->d_cp2, ctx->d_cp2rc,
-                   ctx->d_cpl1, ctx->d_cpl2};
-    for (void* p : old)
-        if (p) CK(hipFree(p));
-    ctx->d_cp1 = ctx->d_cp2 = ctx->d_cp2rc = nullptr;
-    ctx->d_cpl1 = ctx->d_cpl2 = nullptr;
-    CK(dalloc(&ctx->d_i1, S));
-    CK(dalloc(&ctx->d_i2, S));
-    CK(dalloc(&ctx->d_i2rc, S));
-    CK(dalloc(&ctx->d_name, S));
-    if (S) {
-        CK(hipMemcpy(ctx->d_i1, idx1_packed, S * sizeof(u64), hipMemcpyHostToDevice));
-        CK(hipMemcpy(ctx->d_i2, idx2_packed, S * sizeof(u64), hipMemcpyHostToDevice));
-        CK(hipMemcpy(ctx->d_i2rc, idx2rc_packed, S * sizeof(u64), hipMemcpyHostToDevice));
-        CK(hipMemcpy(ctx->d_name, name_id, S * sizeof(int32_t), hipMemcpyHostToDevice));
+    const bool with_cp = idx1_cp && idx2_cp && idx2rc_cp && cp_stride > 0 && S > 0;
+    const u64 ncp = with_cp ? (u64)S * cp_stride : 0;
+    // blob layout (8-B aligned pieces): i1 i2 i2rc [S] u64 | name [S] i32 | cp1 cp2 cp2rc [S*stride] u32 |
+    // cpl1 cpl2 [S] i32
+    auto al = [](u64 b) { return (b + 7) & ~7ull; };
+    const u64 o_i2 = al(S * 8ull), o_i2rc = o_i2 + al(S * 8ull), o_name = o_i2rc + al(S * 8ull);
+    const u64 o_cp1 = o_name + al(S * 4ull), o_cp2 = o_cp1 + al(ncp * 4), o_cp2rc = o_cp2 + al(ncp * 4);
+    const u64 o_l1 = o_cp2rc + al(ncp * 4), o_l2 = o_l1 + (with_cp ? al(S * 4ull) : 0);
+    const u64 total = o_l2 + (with_cp ? al(S * 4ull) : 0) + 8;
+    CK(hipStreamSynchronize(ctx->stream));  // the previous sheet may still be in use / in flight
+    if (total > ctx->sheet_cap) {
+        if (ctx->d_sheet) CK(hipFree(ctx->d_sheet));
+        if (ctx->h_sheet) CK(hipHostFree(ctx->h_sheet));
+        ctx->d_sheet = nullptr;
+        ctx->h_sheet = nullptr;
+        const u64 cap = std::max<u64>(total * 2, 4096);
+        CK(hipMalloc(&ctx->d_sheet, cap));
+        CK(hipHostMalloc(&ctx->h_sheet, cap, hipHostMallocDefault));
+        ctx->sheet_cap = cap;
     }
+    u8* h = ctx->h_sheet;
+    if (S) {
+        std::memcpy(h, idx1_packed, S * 8ull);
+        std::memcpy(h + o_i2, idx2_packed, S * 8ull);
+        std::memcpy(h + o_i2rc, idx2rc_packed, S * 8ull);
+        std::memcpy(h + o_name, name_id, S * 4ull);
+    }
+    if (with_cp) {
+        std::memcpy(h + o_cp1, idx1_cp, ncp * 4);
+        std::memcpy(h + o_cp2, idx2_cp, ncp * 4);
+        std::memcpy(h + o_cp2rc, idx2rc_cp, ncp * 4);
+        std::memcpy(h + o_l1, idx1_len, S * 4ull);
+        std::memcpy(h + o_l2, idx2_len, S * 4ull);
+    }
+    CK(hipMemcpyAsync(ctx->d_sheet, h, total, hipMemcpyHostToDevice, ctx->stream));
+    u8* d = ctx->d_sheet;
+    ctx->d_i1 = (u64*)d;
+    ctx->d_i2 = (u64*)(d + o_i2);
+    ctx->d_i2rc = (u64*)(d + o_i2rc);
+    ctx->d_name = (int32_t*)(d + o_name);
+    ctx->d_cp1 = with_cp ? (u32*)(d + o_cp1) : nullptr;
+    ctx->d_cp2 = with_cp ? (u32*)(d + o_cp2) : nullptr;
+    ctx->d_cp2rc = with_cp ? (u32*)(d + o_cp2rc) : nullptr;
+    ctx->d_cpl1 = with_cp ? (int32_t*)(d + o_l1) : nullptr;
+    ctx->d_cpl2 = with_cp ? (int32_t*)(d + o_l2) : nullptr;
+    ctx->cp_stride = with_cp ? cp_stride : 0;
     ctx->S = S;
     ctx->n_names = n_names;
     auto common = [&](const int32_t* l) {
@@ -431,22 +464,6 @@ int fr_set_sheet(fr_ctx* ctx, int S, const uint64_t* idx1_packed, const int32_t*
     };
     ctx->L1u = common(idx1_len);
     ctx->L2u = common(idx2_len);
-    if (idx1_cp && idx2_cp && idx2rc_cp && cp_stride > 0 && S > 0) {
-        const u64 n = (u64)S * cp_stride;
-        CK(dalloc(&ctx->d_cp1, n));
-        CK(dalloc(&ctx->d_cp2, n));
-        CK(dalloc(&ctx->d_cp2rc, n));
-        CK(dalloc(&ctx->d_cpl1, S));
-        CK(dalloc(&ctx->d_cpl2, S));
-        CK(hipMemcpy(ctx->d_cp1, idx1_cp, n * 4, hipMemcpyHostToDevice));
-        CK(hipMemcpy(ctx->d_cp2, idx2_cp, n * 4, hipMemcpyHostToDevice));
-        CK(hipMemcpy(ctx->d_cp2rc, idx2rc_cp, n * 4, hipMemcpyHostToDevice));
-        CK(hipMemcpy(ctx->d_cpl1, idx1_len, S * 4, hipMemcpyHostToDevice));
-        CK(hipMemcpy(ctx->d_cpl2, idx2_len, S * 4, hipMemcpyHostToDevice));
-        ctx->cp_stride = cp_stride;
-    } else {
-        ctx->cp_stride = 0;
-    }
     return FR_OK;
 }
 
@@ -459,6 +476,7 @@ int fr_reset(fr_ctx* ctx) {
     ctx->scanning = true;
     ctx->file_open = false;
     ctx->file_tag = 0;
+    ctx->merged = false;
     ctx->par = 0;
     ctx->U = 0;
     ctx->n_pres = 0;
@@ -648,15 +666,23 @@ int fr_finalize(fr_ctx* ctx, uint64_t* n_unique, uint64_t* n_presence, uint64_t*
     CK(hipMemsetAsync(ctx->d_counter, 0, sizeof(u64), ctx->stream));
     CK(launch_compact(ctx->tab.slots, ctx->nslots, ctx->d_keys, ctx->d_counts, ctx->d_first, ctx->d_pos,
                       ctx->d_counter, ctx->stream));
+    // ordinals are < (file_tag + 1) << ORD_SHIFT: sort only the bits that can be set
+    int end_bit = 64;
+    if (!ctx->merged) {
+        end_bit = ORD_SHIFT;
+        while (end_bit < 64 && ((u64)ctx->file_tag >> (end_bit - ORD_SHIFT)) != 0) ++end_bit;
+    }
     size_t need = 0;
-    CK(launch_order(ctx->d_first, ctx->d_pos, nk, ctx->d_first_s, ctx->d_perm, nullptr, &need, ctx->stream));
+    CK(launch_order(ctx->d_first, ctx->d_pos, nk, ctx->d_first_s, ctx->d_perm, nullptr, &need, end_bit, ctx->stream));
     if (need > ctx->temp_bytes) {
         if (ctx->d_temp) CK(hipFree(ctx->d_temp));
         CK(hipMalloc(&ctx->d_temp, need));
         ctx->temp_bytes = need;
     }
     size_t tb = ctx->temp_bytes;
-    if (nk) CK(launch_order(ctx->d_first, ctx->d_pos, nk, ctx->d_first_s, ctx->d_perm, ctx->d_temp, &tb, ctx->stream));
+    if (nk)
+        CK(launch_order(ctx->d_first, ctx->d_pos, nk, ctx->d_first_s, ctx->d_perm, ctx->d_temp, &tb, end_bit,
+                        ctx->stream));
     CK(launch_gather(ctx->d_perm, nk, ctx->d_keys, ctx->d_counts, ctx->d_keys_s, ctx->d_counts_s, ctx->d_rank,
                      ctx->stream));
     CK(launch_set_uidx(ctx->tab.slots, ctx->tab.mask, ctx->d_keys_s, nk, ctx->d_rank, ctx->stream));
@@ -868,6 +894,7 @@ int fr_export_unique_device(fr_ctx* ctx, void* dev_keys, void* dev_counts, void*
 int fr_merge_unique_device(fr_ctx* ctx, const void* dev_keys, const void* dev_counts, const void* dev_first,
                            uint64_t n) {
     if (ctx->file_open) return fail(ctx, FR_ERR_INVALID, "fr_merge_unique_device: a file is open");
+    ctx->merged = true;
     int rc = read_state(ctx);
     if (rc) return rc;
     if ((ctx->h_st->n_keys + n) * 2 > ctx->nslots) {

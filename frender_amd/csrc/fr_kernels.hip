@@ -1306,31 +1306,83 @@ hipError_t launch_rehash(Table dst, DevState* st, const GSlot* src, u64 nsrc, hi
     return hipGetLastError();
 }
 
-__global__ void compact_kernel(const GSlot* slots, u64 nslots, u64* keys, u64* counts, u64* first, u32* pos,
-                               u64* counter) {
-    for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i < nslots; i += (u64)gridDim.x * blockDim.x) {
+// Stream compaction of table slots with one atomic per workgroup (single-address atomics
+// serialise at ~11 ns each: a per-wave append over a 4 Mi-slot table costs ~0.8 ms).  Each
+// workgroup owns a contiguous slot range: pass 1 counts its hits and reserves one output
+// range, pass 2 re-reads the (L2-warm) range and writes hits in slot order.
+constexpr int CWG = 256;
+
+template <class Pred>
+__device__ __forceinline__ u64 block_reserve(u64 lo, u64 hi, Pred pred, u64* counter, u32* red) {
+    const int tid = threadIdx.x;
+    u32 mine = 0;
+    for (u64 i = lo + tid; i < hi; i += CWG) mine += pred(i) ? 1u : 0u;
+    for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o, 64);
+    if ((tid & 63) == 0) red[tid >> 6] = mine;
+    __syncthreads();
+    if (tid == 0) {
+        const u32 tot = red[0] + red[1] + red[2] + red[3];
+        *(u64*)&red[4] = tot ? atomicAdd((unsigned long long*)counter, (unsigned long long)tot) : 0ull;
+    }
+    __syncthreads();
+    return *(const u64*)&red[4];
+}
+
+// calls emit(out_index, slot_index) for every hit of [lo, hi), in slot order
+template <class Pred, class Emit>
+__device__ __forceinline__ void block_emit(u64 lo, u64 hi, u64 base, Pred pred, Emit emit, u32* wc) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    for (u64 b = lo; b < hi; b += CWG) {
+        const u64 i = b + tid;
+        const bool hit = i < hi && pred(i);
+        const u64 m = __ballot(hit);
+        if (lane == 0) wc[wid] = (u32)__popcll(m);
+        __syncthreads();
+        u32 before = 0, tot = 0;
+        for (int w = 0; w < CWG / 64; ++w) {
+            before += w < wid ? wc[w] : 0u;
+            tot += wc[w];
+        }
+        if (hit) emit(base + before + (u64)__popcll(m & ((1ull << lane) - 1ull)), i);
+        base += tot;
+        __syncthreads();
+    }
+}
+
+__device__ __forceinline__ void block_range(u64 n, u64& lo, u64& hi) {
+    const u64 per = (n + gridDim.x - 1) / gridDim.x;
+    lo = min(n, (u64)blockIdx.x * per);
+    hi = min(n, lo + per);
+}
+
+__global__ __launch_bounds__(CWG) void compact_kernel(const GSlot* slots, u64 nslots, u64* keys, u64* counts,
+                                                      u64* first, u32* pos, u64* counter) {
+    __shared__ u32 red[8];
+    u64 lo, hi;
+    block_range(nslots, lo, hi);
+    auto pred = [&](u64 i) { return slots[i].key != 0; };
+    const u64 base = block_reserve(lo, hi, pred, counter, red);
+    block_emit(lo, hi, base, pred, [&](u64 p, u64 i) {
         const GSlot g = slots[i];
-        if (!g.key) continue;
-        const u64 p = atomicAdd((unsigned long long*)counter, 1ull);
         keys[p] = g.key;
         counts[p] = g.count;
         first[p] = g.first;
         pos[p] = (u32)p;
-    }
+    }, red);
 }
 
 hipError_t launch_compact(const GSlot* slots, u64 nslots, u64* keys, u64* counts, u64* first, u32* pos,
                           u64* counter, hipStream_t s) {
-    const int grid = (int)std::min<u64>((nslots + 255) / 256, 8192);
-    hipLaunchKernelGGL(compact_kernel, dim3(grid), dim3(256), 0, s, slots, nslots, keys, counts, first, pos,
+    const int grid = (int)std::max<u64>(1, std::min<u64>((nslots + 4095) / 4096, 2048));
+    hipLaunchKernelGGL(compact_kernel, dim3(grid), dim3(CWG), 0, s, slots, nslots, keys, counts, first, pos,
                        counter);
     return hipGetLastError();
 }
 
 hipError_t launch_order(const u64* first_in, const u32* pos_in, u64 n, u64* first_out, u32* perm_out, void* temp,
-                        size_t* temp_bytes, hipStream_t s) {
+                        size_t* temp_bytes, int end_bit, hipStream_t s) {
     return rocprim::radix_sort_pairs(temp, *temp_bytes, first_in, first_out, pos_in, perm_out, (size_t)n, 0,
-                                     64, s);
+                                     (unsigned)end_bit, s);
 }
 
 __global__ void gather_kernel(const u32* perm, u64 n, const u64* keys, const u64* counts, u64* keys_o,
@@ -1407,38 +1459,31 @@ __global__ void merge_kernel(Table t, DevState* st, const u64* keys, const u64* 
 
 // per-file presence (R10) and the per-file distinct-code count (frender.py:175): after a
 // file, exactly the slots whose last_tag is that file's tag hold a code seen in it
-__global__ void presence_scan_kernel(const GSlot* slots, u64 n, u32 tag, Presence* pres, u64 cap, DevState* st) {
-    const u64 stride = (u64)gridDim.x * blockDim.x;
-    for (u64 base = blockIdx.x * (u64)blockDim.x; base < n; base += stride) {
-        const u64 i = base + threadIdx.x;
-        GSlot g;
-        bool hit = false;
-        if (i < n) {
-            g = slots[i];
-            hit = g.key != 0 && g.last_tag == tag;
+__global__ __launch_bounds__(CWG) void presence_scan_kernel(const GSlot* slots, u64 n, u32 tag, Presence* pres,
+                                                            u64 cap, DevState* st) {
+    __shared__ u32 red[8];
+    u64 lo, hi;
+    block_range(n, lo, hi);
+    auto pred = [&](u64 i) {
+        const uint4 w0 = *(const uint4*)&slots[i];
+        const uint4 w1 = *((const uint4*)&slots[i] + 1);
+        return (w0.x | w0.y) != 0u && w1.z == tag;
+    };
+    const u64 base = block_reserve(lo, hi, pred, &st->n_presence, red);
+    block_emit(lo, hi, base, pred, [&](u64 k, u64 i) {
+        if (k < cap) {
+            pres[k].key = slots[i].key;
+            pres[k].tag = tag;
+        } else {
+            atomicOr(&st->cap_flags, 1u);
         }
-        const u64 b = __ballot(hit);
-        if (!b) continue;
-        const int lane = threadIdx.x & 63;
-        u64 at = 0;
-        if (lane == 0) at = atomicAdd((unsigned long long*)&st->n_presence, (unsigned long long)__popcll(b));
-        at = __shfl(at, 0, 64);
-        if (hit) {
-            const u64 k = at + __popcll(b & ((1ull << lane) - 1ull));
-            if (k < cap) {
-                pres[k].key = g.key;
-                pres[k].tag = tag;
-            } else {
-                atomicOr(&st->cap_flags, 1u);
-            }
-        }
-    }
+    }, red);
 }
 
 hipError_t launch_presence_scan(const GSlot* slots, u64 n, u32 tag, Presence* pres, u64 cap, DevState* st,
                                 hipStream_t s) {
-    const int grid = (int)std::min<u64>((n + 255) / 256, 8192);
-    hipLaunchKernelGGL(presence_scan_kernel, dim3(grid), dim3(256), 0, s, slots, n, tag, pres, cap, st);
+    const int grid = (int)std::max<u64>(1, std::min<u64>((n + 4095) / 4096, 2048));
+    hipLaunchKernelGGL(presence_scan_kernel, dim3(grid), dim3(CWG), 0, s, slots, n, tag, pres, cap, st);
     return hipGetLastError();
 }
 

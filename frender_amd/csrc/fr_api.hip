@@ -25,9 +25,8 @@ struct fr_ctx {
     int grid = 0;
     u32 flush_at = NS * 3 / 4;
     u32 ablate = 0;
-    int kernel = 1;  // 1 chunk kernel (v3), 0 per-tile look-back kernel (v2)
     u64* cold = nullptr;
-    u32 cold_cap = 32768;
+    u32 cold_cap = 8192;
 
     DevState* st = nullptr;
     DevState* h_st = nullptr;      // pinned snapshot
@@ -258,16 +257,11 @@ static int launch_range(fr_ctx* ctx, const u8* dptr, u64 len, u64 avail, int own
         ctx->ev_b.push_back(e2);
     }
     CK(hipEventRecord(ctx->ev_a[ctx->ev_used], ctx->stream));
-    if (ctx->kernel == 1) {
-        a.chunk_tiles = (u32)std::max<u64>(1, (a.num_tiles + ctx->grid - 1) / ctx->grid);
-        a.num_chunks = (a.num_tiles + a.chunk_tiles - 1) / a.chunk_tiles;
-        a.cold_cap = ctx->cold_cap;
-        a.cold = ctx->cold;
-        CK(launch_chunk_scan(a, (int)a.num_chunks, ctx->stream));
-    } else {
-        const int grid = (int)std::min<u64>((u64)ctx->grid, a.num_tiles);
-        CK(launch_scan(a, grid, ctx->stream));
-    }
+    a.chunk_tiles = (u32)std::max<u64>(1, (a.num_tiles + ctx->grid - 1) / ctx->grid);
+    a.num_chunks = (a.num_tiles + a.chunk_tiles - 1) / a.chunk_tiles;
+    a.cold_cap = ctx->cold_cap;
+    a.cold = ctx->cold;
+    CK(launch_chunk_scan(a, (int)a.num_chunks, ctx->stream));
     CK(hipEventRecord(ctx->ev_b[ctx->ev_used], ctx->stream));
     ctx->ev_used++;
     ctx->scan_launches++;
@@ -292,12 +286,11 @@ fr_ctx* fr_create(int device, uint64_t chunk_bytes, uint64_t table_slots) {
     if ((e = hipStreamCreateWithFlags(&ctx->copy, hipStreamNonBlocking)) != hipSuccess) return bad("stream", e);
     hipDeviceProp_t prop;
     if ((e = hipGetDeviceProperties(&prop, device)) != hipSuccess) return bad("props", e);
-    const int per_cu = 2;  // LDS-bound: ~58 KB per workgroup -> 2 per CU
+    const int per_cu = 4;  // ~40 KB LDS and <= 128 VGPRs per workgroup -> 4 per CU
     ctx->grid = prop.multiProcessorCount * per_cu;
     if (const char* g = getenv("FR_GRID")) ctx->grid = std::max(1, atoi(g));
     if (const char* f = getenv("FR_FLUSH_AT")) ctx->flush_at = (u32)atoi(f);
     if (const char* f = getenv("FR_ABLATE")) ctx->ablate = (u32)atoi(f);
-    if (const char* f = getenv("FR_KERNEL")) ctx->kernel = atoi(f);
     if (const char* f = getenv("FR_COLD_CAP")) ctx->cold_cap = (u32)std::max(1024, atoi(f));
     if ((e = dalloc(&ctx->cold, 2ull * ctx->cold_cap * (u64)ctx->grid)) != hipSuccess) return bad("cold lists", e);
 

@@ -17,7 +17,7 @@ constexpr int WG = 256;              // 4 waves of 64
 constexpr int TILE = 16384;          // bytes per tile (one look-back unit)
 constexpr int SEG = TILE / WG;       // 64 contiguous bytes per thread
 constexpr int HALO = 512;            // bytes loaded past the tile for headers that cross it
-constexpr int LOG_NS = 11;
+constexpr int LOG_NS = 10;
 constexpr int NS = 1 << LOG_NS;      // LDS hash slots per workgroup
 constexpr int LPROBE = 32;           // LDS probe bound before going to HBM directly
 constexpr int GPROBE = 256;          // HBM probe bound before the overflow list
@@ -143,7 +143,6 @@ __host__ __device__ inline u64 mix64(u64 x) {
 
 // ---- launchers (fr_kernels.hip) --------------------------------------------------
 hipError_t launch_table_init(GSlot* slots, u64 n, hipStream_t s);
-hipError_t launch_scan(const ScanArgs& a, int grid, hipStream_t s);
 hipError_t launch_chunk_scan(const ScanArgs& a, int grid, hipStream_t s);
 hipError_t launch_reinsert_overflow(Table t, DevState* st, const Overflow* src, u64 n, hipStream_t s);
 hipError_t launch_rehash(Table dst, DevState* st, const GSlot* src, u64 nsrc, hipStream_t s);

@@ -1,6 +1,6 @@
 // fr_kernels.hip — gfx950 kernels for frender's scan hot path.
 //
-//  tally (scan_kernel)  : frender.py:154-181 scan_file + :199-205 merge, one pass over the
+//  tally (chunk_kernel) : frender.py:154-181 scan_file + :199-205 merge, one pass over the
 //                         decoded FASTQ bytes in HBM (R1-R4 of SURVEY.md §8.0)
 //  classify             : frender.py:214-234 (Hamming), :237-291 (classes), :294-351 (rc)
 //  table / order        : the first-occurrence-ordered merged table of :199-203
@@ -139,7 +139,6 @@ __device__ __forceinline__ void add_created(DevState* st, u32 mine) {
 // ------------------------------------------------------------------------------------
 struct ScanShared {
     u8 buf[16 + TILE + HALO + 32];   // [0,16) = the 16 bytes before the tile; +32 pad for word reads
-    u16 hdr[TILE / 4 + 4];
     u64 key[NS];
     u32 cnt[NS];
     u32 mino[NS];
@@ -147,7 +146,6 @@ struct ScanShared {
     u64 tile_excl;
     u32 tile;
     u32 next;
-    u32 nhdr;
     u32 nkeys;        // occupied LDS slots
     u32 created;      // HBM slots this workgroup created (added to n_keys once, at exit)
     u32 flags;
@@ -161,11 +159,10 @@ struct ScanShared {
     u32 chunk;
     int phase;        // guessed line phase (lines before the chunk, mod 4), -1 unsure
     u32 exo_p[EXO_BUF], exo_start[EXO_BUF], exo_len[EXO_BUF];
-    u64 tbits[WG];    // line-terminator bitmap of a chunk's first tile (phase inference)
-    u64 bsp[WG];      // per 64-B segment of the staged tile: ' ' bitmap
+    u64 bsp[WG];      // per 64-B segment of the staged tile: ' ' bitmap (phase inference: the
+                      // line-terminator bitmap of a chunk's first tile)
     u64 bcol[WG];     //                                      ':' bitmap
     u64 beol[WG];     //                                      '\r' | '\n' bitmap
-    u32 hscan[WG / 64];
 };
 
 __device__ __forceinline__ u64 make_ord(const ScanArgs& a, u64 off_in_range) {
@@ -611,12 +608,7 @@ __device__ __forceinline__ TileCount count_tile(ScanShared& sh, const ScanArgs& 
     return tc;
 }
 
-// The tally kernel.  Persistent workgroups draw tiles from a ticket counter; per tile:
-//   look-back (prefix of line terminators) -> every 4th line start -> parse headers (lane per
-//   header) -> count codes in the LDS table (HBM table for the rest).
-// Software pipeline: while tile t is parsed, the next tile's ticket and bytes are already in
-// flight; the next tile is staged and its aggregate published before its own look-back, so
-// look-backs mostly find ready predecessors.
+// per-phase s_memtime stamps (FR_STAMPS diagnostic builds only)
 #ifdef FR_STAMPS
 #define STAMP(i)                                                   \
     do {                                                           \
@@ -632,116 +624,6 @@ __device__ __forceinline__ TileCount count_tile(ScanShared& sh, const ScanArgs& 
     } while (0)
 #endif
 
-__global__ __launch_bounds__(WG) void scan_kernel(ScanArgs a) {
-    __shared__ ScanShared sh;
-#ifdef FR_STAMPS
-    u64 stamps[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    u64 last_ = __builtin_amdgcn_s_memtime();
-#endif
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wid = tid >> 6;
-    for (int i = tid; i < NS; i += WG) {
-        sh.key[i] = 0;
-        sh.cnt[i] = 0;
-        sh.mino[i] = 0xFFFFFFFFu;
-    }
-    if (tid < 2) *(uint4*)(sh.buf + 16 + TILE + HALO + 16 * tid) = make_uint4(0u, 0u, 0u, 0u);
-    if (tid == 0) {
-        sh.nkeys = 0;
-        sh.created = 0;
-        sh.flags = 0;
-        sh.buffered = 0;
-        sh.spec = 0;
-        sh.tile = atomicAdd(&a.st->ticket, 1u);
-    }
-    const u64 base_lines = a.st->lines[a.par];
-    __syncthreads();
-    u32 t = sh.tile;
-    TileRegs r;
-    TileCount tc;
-    if (t < a.num_tiles) {
-        tile_fetch(a, t, r, tid);
-        tile_stage(sh, r, tid);
-        __syncthreads();
-        tc = count_tile(sh, a, t, tid, lane, wid);
-    }
-    STAMP(7);
-    while (t < a.num_tiles) {
-        const u64 tile0 = (u64)t * TILE;
-        const u32 nb = (u32)min((u64)(TILE + HALO), a.avail - tile0);
-        u32 tn = 0;
-        if (tid == 0) tn = atomicAdd(&a.st->ticket, 1u);  // returns during the look-back
-        if (wid == 0) {
-            const u64 ex = lookback(a, t, tc.tot, lane);
-            if (lane == 0) {
-                sh.tile_excl = ex;
-                if (t == a.num_tiles - 1) a.st->lines[a.par ^ 1u] = base_lines + ex + tc.tot;
-                sh.next = tn;
-                sh.nhdr = 0;
-            }
-        }
-        STAMP(0);
-        __syncthreads();
-        STAMP(1);
-        tn = sh.next;
-        tile_fetch(a, tn, r, tid);  // prefetch: lands while this tile is parsed
-
-        // ---- every 4th line is a header (R1); collect their starts -------------------
-        u64 L = base_lines + sh.tile_excl + tc.wexcl + (tc.x - tc.c);
-        u64 m = tc.tmask;
-        const u32 s0 = tid * SEG;
-        while (m) {
-            const int j = __ffsll((long long)m) - 1;
-            m &= m - 1;
-            L += 1;  // index of the line that starts after this terminator
-            if ((L & 3ull) == 0) {
-                const u32 p = s0 + (u32)j + 1u;
-                const u64 gp = tile0 + p;
-                const bool mine = gp < a.len || (a.own_end && gp == a.len && gp < a.avail);
-                if (mine && (a.max_records <= 0 || (i64)(L >> 2) < a.max_records)) {
-                    const u32 slot = atomicAdd(&sh.nhdr, 1u);
-                    sh.hdr[slot] = (u16)p;
-                }
-            }
-        }
-        if (t == 0 && tid == 0 && a.own_start && (base_lines & 3ull) == 0 && a.avail > 0 &&
-            (a.max_records <= 0 || (i64)(base_lines >> 2) < a.max_records)) {
-            const u32 slot = atomicAdd(&sh.nhdr, 1u);
-            sh.hdr[slot] = 0;
-        }
-        __syncthreads();
-        STAMP(2);
-
-        // ---- parse headers (lane per header) and count their codes ------------------
-        const u32 nh = sh.nhdr;
-        if (!(a.ablate & 1u))
-            for (u32 h = tid; h < nh; h += WG) process_header(sh, a, tile0, sh.hdr[h], nb);
-        __syncthreads();
-        STAMP(3);
-        if (tn >= a.num_tiles) break;
-        tile_stage(sh, r, tid);
-        __syncthreads();
-        STAMP(4);
-        tc = count_tile(sh, a, tn, tid, lane, wid);
-        STAMP(5);
-        t = tn;
-    }
-    __syncthreads();
-    lds_flush(sh, a);
-    __syncthreads();
-    STAMP(6);
-#ifdef FR_STAMPS
-    if (tid == 0)
-        for (int i = 0; i < 8; ++i) atomicAdd((unsigned long long*)&a.st->stamp[i], (unsigned long long)stamps[i]);
-#endif
-    if (tid == 0) {
-        if (sh.created) atomicAdd((unsigned long long*)&a.st->n_keys, (unsigned long long)sh.created);
-        if (sh.flags & 1u) atomicOr(&a.st->nonascii, 1u);
-        if (sh.flags & 2u) atomicOr(&a.st->utf8_bad, 1u);
-    }
-}
-
 // =====================================================================================
 // chunk kernel (v3): a workgroup owns a contiguous chunk of tiles and walks it in order, so
 // the line count is local; the chunk's starting line phase is guessed from the FASTQ record
@@ -750,64 +632,6 @@ __global__ __launch_bounds__(WG) void scan_kernel(ScanArgs a) {
 // confirms the guess.  A wrong/unsure guess, a buffer overflow or -s re-runs the chunk with
 // the exact prefix.  Correctness never depends on the guess.
 // =====================================================================================
-
-// every 4th line start of tile t -> sh.hdr (block scan, no shared counter)
-__device__ __forceinline__ void collect_headers(ScanShared& sh, const ScanArgs& a, u32 t, const TileCount& tc, u64 L0, int tid,
-                                int lane, int wid) {
-    const u64 tile0 = (u64)t * TILE;
-    const u32 s0 = tid * SEG;
-    u64 L = L0 + tc.wexcl + (tc.x - tc.c);
-    // pass 1: count this thread's headers
-    u32 n = 0;
-    {
-        u64 m = tc.tmask, l = L;
-        while (m) {
-            const int j = __ffsll((long long)m) - 1;
-            m &= m - 1;
-            l += 1;
-            if ((l & 3ull) == 0) {
-                const u64 gp = tile0 + s0 + (u32)j + 1u;
-                const bool mine = gp < a.len || (a.own_end && gp == a.len && gp < a.avail);
-                n += (mine && (a.max_records <= 0 || (i64)(l >> 2) < a.max_records)) ? 1u : 0u;
-            }
-        }
-    }
-    const bool own0 = t == 0 && tid == 0 && a.own_start && (L0 & 3ull) == 0 && a.avail > 0 &&
-                      (a.max_records <= 0 || (i64)(L0 >> 2) < a.max_records);
-    const u32 mine0 = own0 ? 1u : 0u;
-    u32 x = n + mine0;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const u32 y = __shfl_up(x, d, 64);
-        if (lane >= d) x += y;
-    }
-    if (lane == 63) sh.hscan[wid] = x;
-    __syncthreads();
-    u32 base = 0, tot = 0;
-#pragma unroll
-    for (int w = 0; w < WG / 64; ++w) {
-        const u32 v = sh.hscan[w];
-        base += w < wid ? v : 0u;
-        tot += v;
-    }
-    u32 o = base + x - (n + mine0);
-    if (own0) sh.hdr[o++] = 0;
-    {
-        u64 m = tc.tmask, l = L;
-        while (m) {
-            const int j = __ffsll((long long)m) - 1;
-            m &= m - 1;
-            l += 1;
-            if ((l & 3ull) == 0) {
-                const u32 p = s0 + (u32)j + 1u;
-                const u64 gp = tile0 + p;
-                const bool mine = gp < a.len || (a.own_end && gp == a.len && gp < a.avail);
-                if (mine && (a.max_records <= 0 || (i64)(l >> 2) < a.max_records)) sh.hdr[o++] = (u16)p;
-            }
-        }
-    }
-    if (tid == 0) sh.nhdr = tot;
-}
 
 // Guess P = (lines before the chunk) mod 4 from the first PHASE_LINES complete lines of the
 // staged first tile: with lines indexed P+k+1 after the k-th terminator, a FASTQ record has a
@@ -819,7 +643,7 @@ __device__ __forceinline__ int infer_phase(const ScanShared& sh, u32 tlen) {
     int seqlen[4] = {-1, -1, -1, -1};
     int prev = -1, k = 0;
     for (int w = 0; w < WG && k < PHASE_LINES; ++w) {
-        u64 m = sh.tbits[w];
+        u64 m = sh.bsp[w];
         while (m && k < PHASE_LINES) {
             const int e = w * SEG + (__ffsll((long long)m) - 1);
             m &= m - 1;
@@ -1080,6 +904,38 @@ __device__ __forceinline__ void process_header_bm(ScanShared& sh, const ScanArgs
     else slow_header(sh, a, tile0, p, nb, r, start, n);
 }
 
+// Every 4th line start whose terminator lies in this lane's 64-B segment is a header owned by
+// this lane (the range's first byte by lane 0 of its first tile): parse it where it lies.  No
+// header list, no block scan: the tile's line prefix (count_tile) gives each lane its index.
+__device__ __forceinline__ void parse_own_headers(ScanShared& sh, const ScanArgs& a, u32 t, const TileCount& tc,
+                                                  u64 L0, int tid) {
+    const u64 tile0 = (u64)t * TILE;
+    const u32 nb = (u32)min((u64)(TILE + HALO), a.avail - tile0);
+    const u32 tlen = (u32)min((u64)TILE, a.len - tile0);
+    const u32 s0 = tid * SEG;
+    const bool own0 = t == 0 && tid == 0 && a.own_start && (L0 & 3ull) == 0 && a.avail > 0 &&
+                      (a.max_records <= 0 || (i64)(L0 >> 2) < a.max_records);
+    u64 m = tc.tmask;
+    u64 l = L0 + tc.wexcl + (tc.x - tc.c);
+    int pend = own0 ? 0 : -1;  // the next header position of this lane, -1 none
+    for (;;) {
+        while (pend < 0 && m) {
+            const int j = __ffsll((long long)m) - 1;
+            m &= m - 1;
+            l += 1;
+            if ((l & 3ull) == 0) {
+                const u32 p = s0 + (u32)j + 1u;
+                const u64 gp = tile0 + p;
+                const bool mine = gp < a.len || (a.own_end && gp == a.len && gp < a.avail);
+                if (mine && (a.max_records <= 0 || (i64)(l >> 2) < a.max_records)) pend = (int)p;
+            }
+        }
+        if (pend < 0) break;
+        process_header_bm(sh, a, tile0, (u32)pend, tlen, nb);
+        pend = -1;
+    }
+}
+
 // walk tiles [tb, te) of the range; L0 = line index (absolute, or mod-4 guess) at tile tb.
 // parse = false: count only.  (exact is kept for symmetry: with an exact phase a full cold
 // list falls back to direct HBM inserts inside lds_insert.)
@@ -1100,17 +956,8 @@ __device__ __forceinline__ u64 walk_chunk(ScanShared& sh, const ScanArgs& a, u32
     for (u32 t = tb; t < te; ++t) {
         const bool more = t + 1 < te;
         if (more) tile_fetch(a, t + 1, r, tid);  // lands while this tile is parsed
-        if (parse && !uniform_flag(sh.spec_bad)) {
-            collect_headers(sh, a, t, tc, L0 + lines, tid, lane, wid);
-            __syncthreads();
-            STAMP(0);
-            const u64 tile0 = (u64)t * TILE;
-            const u32 nb = (u32)min((u64)(TILE + HALO), a.avail - tile0);
-            const u32 tlen = (u32)min((u64)TILE, a.len - tile0);
-            const u32 nh = sh.nhdr;
-            if (!(a.ablate & 1u))
-                for (u32 h = tid; h < nh; h += WG) process_header_bm(sh, a, tile0, sh.hdr[h], tlen, nb);
-        }
+        if (parse && !uniform_flag(sh.spec_bad) && !(a.ablate & 1u))
+            parse_own_headers(sh, a, t, tc, L0 + lines, tid);
         __syncthreads();
         STAMP(1);
         lines += tc.tot;
@@ -1130,7 +977,7 @@ __device__ __forceinline__ u64 walk_chunk(ScanShared& sh, const ScanArgs& a, u32
     return lines;
 }
 
-__global__ __launch_bounds__(WG, 2) void chunk_kernel(ScanArgs a) {
+__global__ __launch_bounds__(WG, 4) void chunk_kernel(ScanArgs a) {
     __shared__ ScanShared sh;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -1174,7 +1021,7 @@ __global__ __launch_bounds__(WG, 2) void chunk_kernel(ScanArgs a) {
             tile_stage(sh, r, tid);
             __syncthreads();
             const TileCount tc0 = count_tile(sh, a, tb, tid, lane, wid, false);
-            sh.tbits[tid] = tc0.tmask;
+            sh.bsp[tid] = tc0.tmask;
             __syncthreads();
             if (tid == 0) sh.phase = infer_phase(sh, 0);
             __syncthreads();
@@ -1237,10 +1084,6 @@ hipError_t launch_chunk_scan(const ScanArgs& a, int grid, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_scan(const ScanArgs& a, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(scan_kernel, dim3(grid), dim3(WG), 0, s, a);
-    return hipGetLastError();
-}
 
 // ------------------------------------------------------------------------------------
 // table maintenance

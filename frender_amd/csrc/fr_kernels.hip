@@ -137,11 +137,15 @@ __device__ __forceinline__ void add_created(DevState* st, u32 mine) {
 // ------------------------------------------------------------------------------------
 // the tally kernel
 // ------------------------------------------------------------------------------------
+struct alignas(16) LSlot {  // one ds_read_b128 reads key, count and first offset together
+    u64 key;                 // 0 = empty
+    u32 cnt;
+    u32 mino;                // min range offset of the code's records, ~0 = none
+};
+
 struct ScanShared {
     u8 buf[16 + TILE + HALO + 32];   // [0,16) = the 16 bytes before the tile; +32 pad for word reads
-    u64 key[NS];
-    u32 cnt[NS];
-    u32 mino[NS];
+    LSlot ls[NS];     // LDS hash table of this workgroup's chunk
     u32 wsum[WG / 64];
     u64 tile_excl;
     u32 tile;
@@ -169,38 +173,30 @@ __device__ __forceinline__ u64 make_ord(const ScanArgs& a, u64 off_in_range) {
     return ((u64)a.file_tag << ORD_SHIFT) | (a.file_offset + off_in_range);
 }
 
-__device__ void lds_flush(ScanShared& sh, const ScanArgs& a) {
-    for (int i = threadIdx.x; i < NS; i += WG) {
-        const u64 k = sh.key[i];
-        if (k) {
-            if (global_insert(a.tab, a.st, k, sh.cnt[i], make_ord(a, sh.mino[i]), a.file_tag))
-                atomicAdd(&sh.created, 1u);
-            sh.key[i] = 0;
-            sh.cnt[i] = 0;
-            sh.mino[i] = 0xFFFFFFFFu;
-        }
-    }
-}
-
 __device__ __forceinline__ void lds_insert(ScanShared& sh, const ScanArgs& a, u64 key, u32 off) {
     u32 h = (u32)((key * 0x9E3779B97F4A7C15ull) >> (64 - LOG_NS));
     for (int pr = 0; pr < LPROBE; ++pr) {
-        u64 k = *(volatile u64*)&sh.key[h];
+        typedef u32 u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 sl = *(const volatile u32x4*)&sh.ls[h];
+        u64 k = ((u64)sl.y << 32) | sl.x;
+        u32 mino = sl.w;
         if (k == 0) {
             // a full LDS table stops claiming slots: the code goes to HBM directly; the
             // codes already resident (the hot ones arrive first) keep aggregating here
             if (*(volatile u32*)&sh.nkeys >= a.flush_at) break;
-            const u64 old = atomicCAS((unsigned long long*)&sh.key[h], 0ull, (unsigned long long)key);
+            const u64 old = atomicCAS((unsigned long long*)&sh.ls[h].key, 0ull, (unsigned long long)key);
             if (old == 0) {
                 atomicAdd(&sh.nkeys, 1u);
                 k = key;
             } else {
                 k = old;
             }
+            mino = 0xFFFFFFFFu;
         }
         if (k == key) {
-            atomicAdd(&sh.cnt[h], 1u);
-            atomicMin(&sh.mino[h], off);
+            atomicAdd(&sh.ls[h].cnt, 1u);
+            // mino only decreases, so a stale read can only cause a redundant atomic
+            if (off < mino) atomicMin(&sh.ls[h].mino, off);
             return;
         }
         h = (h + 1) & (NS - 1);
@@ -473,6 +469,9 @@ __device__ void process_header(ScanShared& sh, const ScanArgs& a, u64 tile0, u32
 }
 
 // ---- tile staging: 16-B loads into registers (prefetch), then registers -> LDS ----------
+#ifndef FR_PREFETCH
+#define FR_PREFETCH 1
+#endif
 constexpr int STAGE_VECS = (TILE + HALO + WG * 16 - 1) / (WG * 16);  // 5
 
 struct TileRegs {
@@ -726,10 +725,11 @@ __device__ __forceinline__ void commit_buffers(ScanShared& sh, const ScanArgs& a
 #pragma unroll
             for (int b = 0; b < 2; ++b) {
                 const int i = i0 + b * WG;
-                v[b] = i < NS && sh.key[i] != 0;
-                key[b] = v[b] ? sh.key[i] : 0;
-                cnt[b] = v[b] ? sh.cnt[i] : 0;
-                ord[b] = v[b] ? make_ord(a, sh.mino[i]) : 0;
+                const LSlot e = i < NS ? sh.ls[i] : LSlot{0, 0, 0};
+                v[b] = e.key != 0;
+                key[b] = e.key;
+                cnt[b] = e.cnt;
+                ord[b] = v[b] ? make_ord(a, e.mino) : 0;
             }
             made += insert_many<2>(a, key, cnt, ord, v);
         }
@@ -770,9 +770,7 @@ __device__ __forceinline__ void commit_buffers(ScanShared& sh, const ScanArgs& a
     __syncthreads();
     if (table)
         for (int i = tid; i < NS; i += WG) {
-            sh.key[i] = 0;
-            sh.cnt[i] = 0;
-            sh.mino[i] = 0xFFFFFFFFu;
+            sh.ls[i] = LSlot{0, 0, 0xFFFFFFFFu};
         }
     if (tid == 0) {
         if (table) sh.nkeys = 0;
@@ -787,9 +785,7 @@ __device__ __forceinline__ void commit_buffers(ScanShared& sh, const ScanArgs& a
 __device__ __forceinline__ void discard_buffers(ScanShared& sh, int tid) {
     __syncthreads();
     for (int i = tid; i < NS; i += WG) {
-        sh.key[i] = 0;
-        sh.cnt[i] = 0;
-        sh.mino[i] = 0xFFFFFFFFu;
+        sh.ls[i] = LSlot{0, 0, 0xFFFFFFFFu};
     }
     if (tid == 0) {
         sh.nkeys = 0;
@@ -832,9 +828,7 @@ __device__ __forceinline__ bool encode_perm(const u8* lb, u32 start, u32 n, u64&
     return bad == 0;
 }
 
-// R2 via the tile's ' ' / ':' / line-end bitmaps: first ' ', then the next ' ' or line end,
-// then the last ':' between them.  Lines that reach past the tile's bitmaps fall back to the
-// word-scan parser.
+// the rare header outcomes: word-scan fallback, no ' ' (IndexError), or an exotic code
 __device__ __forceinline__ void slow_header(ScanShared& sh, const ScanArgs& a, u64 tile0, u32 p, u32 nb, int r,
                                          u32 start, u32 n) {
     if (r == 2) process_header(sh, a, tile0, p, nb);
@@ -842,45 +836,51 @@ __device__ __forceinline__ void slow_header(ScanShared& sh, const ScanArgs& a, u
     else exotic_record(a, tile0, p, start, n, sh, nb);
 }
 
-// returns 0 parsed (code at [start, start+n)), 1 no ' ' on the line, 2 fall back to the word scan
+// bits [0, k) of a 128-bit window (k in [0, 128])
+__device__ __forceinline__ void below128(u32 k, u64& lo, u64& hi) {
+    lo = k >= 64u ? ~0ull : ((1ull << k) - 1ull);
+    hi = k <= 64u ? 0ull : (k >= 128u ? ~0ull : ((1ull << (k - 64u)) - 1ull));
+}
+
+__device__ __forceinline__ u32 first128(u64 lo, u64 hi) {  // lowest set bit (window non-empty)
+    return lo ? (u32)__builtin_ctzll(lo) : 64u + (u32)__builtin_ctzll(hi);
+}
+
+// returns 0 parsed (code at [start, start+n)), 1 no ' ' on the line, 2 fall back to the word scan.
+// The line's bitmaps are read as one 128-bit window (two segments, six independent LDS reads,
+// one round trip); lines whose code does not end inside the window take the word scan.
 __device__ __forceinline__ int locate_code_bm(const ScanShared& sh, u32 p, u32 tlen, u32& start, u32& n) {
-    u32 w = p >> 6;
     if (p >= tlen) return 2;
-    const u64 m0 = ~0ull << (p & 63u);
-    u64 sp = sh.bsp[w] & m0, eol = sh.beol[w] & m0;
-    while (!(sp | eol)) {
-        if (++w * 64u >= tlen) return 2;
-        sp = sh.bsp[w];
-        eol = sh.beol[w];
-    }
-    const u32 b = __ffsll((long long)(sp | eol)) - 1;
-    if ((eol >> b) & 1ull) return 1;
-    const u32 sp1 = w * 64u + b;
-    const u64 m1 = b == 63u ? 0ull : (~0ull << (b + 1u));
-    sp &= m1;
-    eol &= m1;
-    while (!(sp | eol)) {
-        if (++w * 64u >= tlen) return 2;
-        sp = sh.bsp[w];
-        eol = sh.beol[w];
-    }
-    const u32 end = w * 64u + (u32)(__ffsll((long long)(sp | eol)) - 1);
-    // last ':' in (sp1, end)
-    u32 wc = end >> 6;
-    u64 cm = sh.bcol[wc] & ((1ull << (end & 63u)) - 1ull);
-    const u32 ws = sp1 >> 6;
-    u32 st = sp1 + 1u;
-    for (;;) {
-        if (wc == ws) cm &= (sp1 & 63u) == 63u ? 0ull : (~0ull << ((sp1 & 63u) + 1u));
-        if (cm) {
-            st = wc * 64u + 64u - (u32)__clzll((long long)cm);
-            break;
-        }
-        if (wc == ws) break;
-        cm = sh.bcol[--wc];
-    }
-    start = st;
-    n = end - st;
+    const u32 w = p >> 6, b = p & 63u;
+    const bool has1 = (w + 1u) * 64u < tlen;
+    const u32 wn = has1 ? w + 1u : w;
+    u64 s0 = sh.bsp[w], s1 = sh.bsp[wn], e0 = sh.beol[w], e1 = sh.beol[wn], c0 = sh.bcol[w], c1 = sh.bcol[wn];
+    if (!has1) s1 = e1 = c1 = 0;
+    // shift the window so that bit 0 is position p
+    const u32 rb = 64u - b;
+    s0 = (s0 >> b) | (b ? s1 << rb : 0ull);
+    s1 >>= b;
+    e0 = (e0 >> b) | (b ? e1 << rb : 0ull);
+    e1 >>= b;
+    c0 = (c0 >> b) | (b ? c1 << rb : 0ull);
+    c1 >>= b;
+    u64 v0 = s0 | e0, v1 = s1 | e1;
+    if (!(v0 | v1)) return 2;
+    const u32 f1 = first128(v0, v1);                       // the first ' ' or line end
+    if ((f1 < 64u ? (e0 >> f1) : (e1 >> (f1 - 64u))) & 1ull) return 1;
+    u64 m0, m1;
+    below128(f1 + 1u, m0, m1);                             // drop bits [0, f1]
+    v0 &= ~m0;
+    v1 &= ~m1;
+    if (!(v0 | v1)) return 2;
+    const u32 f2 = first128(v0, v1);                       // the token's end
+    u64 k0, k1;
+    below128(f2, k0, k1);
+    c0 &= k0 & ~m0;                                        // ':' strictly inside (f1, f2)
+    c1 &= k1 & ~m1;
+    const u32 lastc = c1 ? 127u - (u32)__builtin_clzll(c1) : c0 ? 63u - (u32)__builtin_clzll(c0) : f1;
+    start = p + lastc + 1u;
+    n = f2 - lastc - 1u;
     return 0;
 }
 
@@ -946,12 +946,13 @@ __device__ __forceinline__ u64 walk_chunk(ScanShared& sh, const ScanArgs& a, u32
     u64 stamps[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     u64 last_ = __builtin_amdgcn_s_memtime();
 #endif
+    u64 lines = 0;
+#if FR_PREFETCH
     TileRegs r;
     tile_fetch(a, tb, r, tid);
     tile_stage(sh, r, tid);
     __syncthreads();
     TileCount tc = count_tile(sh, a, tb, tid, lane, wid, false);
-    u64 lines = 0;
     STAMP(4);
     for (u32 t = tb; t < te; ++t) {
         const bool more = t + 1 < te;
@@ -969,6 +970,25 @@ __device__ __forceinline__ u64 walk_chunk(ScanShared& sh, const ScanArgs& a, u32
             STAMP(3);
         }
     }
+#else
+    // no register prefetch: the other workgroups on the CU cover this one's load latency
+    for (u32 t = tb; t < te; ++t) {
+        {
+            TileRegs r;
+            tile_fetch(a, t, r, tid);
+            tile_stage(sh, r, tid);
+        }
+        __syncthreads();
+        STAMP(2);
+        const TileCount tc = count_tile(sh, a, t, tid, lane, wid, false);
+        STAMP(3);
+        if (parse && !uniform_flag(sh.spec_bad) && !(a.ablate & 1u))
+            parse_own_headers(sh, a, t, tc, L0 + lines, tid);
+        __syncthreads();
+        STAMP(1);
+        lines += tc.tot;
+    }
+#endif
 #ifdef FR_STAMPS
     if (tid == 0)
         for (int i = 0; i < 8; ++i)
@@ -983,9 +1003,7 @@ __global__ __launch_bounds__(WG, 4) void chunk_kernel(ScanArgs a) {
     const int lane = tid & 63;
     const int wid = tid >> 6;
     for (int i = tid; i < NS; i += WG) {
-        sh.key[i] = 0;
-        sh.cnt[i] = 0;
-        sh.mino[i] = 0xFFFFFFFFu;
+        sh.ls[i] = LSlot{0, 0, 0xFFFFFFFFu};
     }
     if (tid < 2) *(uint4*)(sh.buf + 16 + TILE + HALO + 16 * tid) = make_uint4(0u, 0u, 0u, 0u);
     if (tid == 0) {

@@ -232,7 +232,7 @@ static int launch_range(fr_ctx* ctx, const u8* dptr, u64 len, u64 avail, int own
     a.file_tag = ctx->file_tag;
     a.par = ctx->par;
     a.epoch = ++ctx->epoch;
-    a.num_tiles = (u32)((len + TILE - 1) / TILE);
+    a.num_tiles = (u32)((len + TSTEP - 1) / TSTEP);
     a.own_start = own_start;
     a.own_end = own_end;
     a.pre_valid = pre_valid;
@@ -296,7 +296,7 @@ fr_ctx* fr_create(int device, uint64_t chunk_bytes, uint64_t table_slots) {
 
     ctx->chunk_bytes = chunk_bytes ? ((chunk_bytes + TILE - 1) / TILE) * TILE : (256ull << 20);
     if (ctx->chunk_bytes > RANGE_MAX) ctx->chunk_bytes = RANGE_MAX;
-    ctx->tiles_cap = RANGE_MAX / TILE + 2;
+    ctx->tiles_cap = RANGE_MAX / TSTEP + 2;
     ctx->nslots = pow2_at_least(std::max<u64>(table_slots, 1024));
     if ((e = hipMalloc((void**)&ctx->st, sizeof(DevState))) != hipSuccess) return bad("state", e);
     if ((e = hipHostMalloc((void**)&ctx->h_st, sizeof(DevState), hipHostMallocDefault)) != hipSuccess)

@@ -481,7 +481,7 @@ struct TileRegs {
 
 __device__ __forceinline__ void tile_fetch(const ScanArgs& a, u32 t, TileRegs& r, int tid) {
     if (t >= a.num_tiles) return;
-    const u64 tile0 = (u64)t * TILE;
+    const u64 tile0 = (u64)t * TSTEP;
     const u32 nb = (u32)min((u64)(TILE + HALO), a.avail - tile0);
 #pragma unroll
     for (int k = 0; k < STAGE_VECS; ++k) {
@@ -523,17 +523,18 @@ struct TileCount {
 // (R1: universal newlines: '\n', '\r\n' and a lone '\r' each end one line)
 __device__ __forceinline__ TileCount count_tile(ScanShared& sh, const ScanArgs& a, u32 t, int tid, int lane, int wid,
                                 bool publish = true) {
-    const u64 tile0 = (u64)t * TILE;
-    const u32 tlen = (u32)min((u64)TILE, a.len - tile0);
+    const u64 tile0 = (u64)t * TSTEP;
+    const u32 tlen = (u32)min((u64)TSTEP, a.len - tile0);   // this tile's own bytes
     const u32 nb = (u32)min((u64)(TILE + HALO), a.avail - tile0);
+    const u32 bl = min((u32)TILE, nb);                        // bytes with bitmaps
     const u32 s0 = tid * SEG;
     TileCount tc;
     tc.tmask = 0;
-    if (s0 >= tlen) {
+    if (s0 >= bl) {
         sh.bsp[tid] = 0;
         sh.bcol[tid] = 0;
         sh.beol[tid] = 0;
-    } else {
+    } else {  // bitmaps for every staged segment; terminators / UTF-8 only for the tile's own bytes
         u64 nl = 0, cr = 0, sp = 0, col = 0;
         u32 hiw = 0;
 #pragma unroll
@@ -552,23 +553,11 @@ __device__ __forceinline__ TileCount count_tile(ScanShared& sh, const ScanArgs& 
             }
         }
         const u64 nxt = (s0 + SEG < nb && sh.buf[16 + s0 + SEG] == '\n') ? 1ull : 0ull;
-        tc.tmask = nl | (cr & ~((nl >> 1) | (nxt << 63)));
+        u64 tm = nl | (cr & ~((nl >> 1) | (nxt << 63)));
         u64 eol = nl | cr;
-        u64 hi = 0;
-        if (hiw & 0x80808080u) {  // rare: exact per-byte high-bit mask for the UTF-8 check
-#pragma unroll
-            for (int qv = 0; qv < SEG / 16; ++qv) {
-                const uint4 v = *(const uint4*)(sh.buf + 16 + s0 + qv * 16);
-                const u32 w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                for (int k = 0; k < 4; ++k) hi |= (u64)hi4(w[k]) << (qv * 16 + k * 4);
-            }
-        }
-        const u32 valid = tlen - s0;
-        if (valid < SEG) {
-            const u64 vm = (1ull << valid) - 1ull;
-            tc.tmask &= vm;
-            hi &= vm;
+        const u32 bvalid = bl - s0;
+        if (bvalid < SEG) {
+            const u64 vm = (1ull << bvalid) - 1ull;
             sp &= vm;
             col &= vm;
             eol &= vm;
@@ -576,9 +565,28 @@ __device__ __forceinline__ TileCount count_tile(ScanShared& sh, const ScanArgs& 
         sh.bsp[tid] = sp;
         sh.bcol[tid] = col;
         sh.beol[tid] = eol;
-        if (hi) {
-            atomicOr(&sh.flags, 1u);
-            if (!utf8_segment_ok(sh, (int)s0, (int)min(valid, (u32)SEG), (int)nb)) atomicOr(&sh.flags, 2u);
+        if (s0 < tlen) {
+            const u32 valid = tlen - s0;
+            u64 hi = 0;
+            if (hiw & 0x80808080u) {  // rare: exact per-byte high-bit mask for the UTF-8 check
+#pragma unroll
+                for (int qv = 0; qv < SEG / 16; ++qv) {
+                    const uint4 v = *(const uint4*)(sh.buf + 16 + s0 + qv * 16);
+                    const u32 w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) hi |= (u64)hi4(w[k]) << (qv * 16 + k * 4);
+                }
+            }
+            if (valid < SEG) {
+                const u64 vm = (1ull << valid) - 1ull;
+                tm &= vm;
+                hi &= vm;
+            }
+            tc.tmask = tm;
+            if (hi) {
+                atomicOr(&sh.flags, 1u);
+                if (!utf8_segment_ok(sh, (int)s0, (int)min(valid, (u32)SEG), (int)nb)) atomicOr(&sh.flags, 2u);
+            }
         }
     }
     tc.c = __popcll(tc.tmask);
@@ -849,10 +857,10 @@ __device__ __forceinline__ u32 first128(u64 lo, u64 hi) {  // lowest set bit (wi
 // returns 0 parsed (code at [start, start+n)), 1 no ' ' on the line, 2 fall back to the word scan.
 // The line's bitmaps are read as one 128-bit window (two segments, six independent LDS reads,
 // one round trip); lines whose code does not end inside the window take the word scan.
-__device__ __forceinline__ int locate_code_bm(const ScanShared& sh, u32 p, u32 tlen, u32& start, u32& n) {
-    if (p >= tlen) return 2;
+__device__ __forceinline__ int locate_code_bm(const ScanShared& sh, u32 p, u32 bl, u32& start, u32& n) {
+    if (p >= bl) return 2;
     const u32 w = p >> 6, b = p & 63u;
-    const bool has1 = (w + 1u) * 64u < tlen;
+    const bool has1 = (w + 1u) * 64u < bl;
     const u32 wn = has1 ? w + 1u : w;
     u64 s0 = sh.bsp[w], s1 = sh.bsp[wn], e0 = sh.beol[w], e1 = sh.beol[wn], c0 = sh.bcol[w], c1 = sh.bcol[wn];
     if (!has1) s1 = e1 = c1 = 0;
@@ -887,10 +895,10 @@ __device__ __forceinline__ int locate_code_bm(const ScanShared& sh, u32 p, u32 t
 // R2 via the tile's ' ' / ':' / line-end bitmaps: first ' ', then the next ' ' or line end,
 // then the last ':' between them.  Lines that reach past the tile's bitmaps fall back to the
 // word-scan parser (process_header).
-__device__ __forceinline__ void process_header_bm(ScanShared& sh, const ScanArgs& a, u64 tile0, u32 p, u32 tlen,
+__device__ __forceinline__ void process_header_bm(ScanShared& sh, const ScanArgs& a, u64 tile0, u32 p, u32 bl,
                                                   u32 nb) {
     u32 start = 0, n = 0;
-    const int r = locate_code_bm(sh, p, tlen, start, n);
+    const int r = locate_code_bm(sh, p, bl, start, n);
     u64 key = 0;
     bool fast = false;
     if (r == 0) {
@@ -900,6 +908,7 @@ __device__ __forceinline__ void process_header_bm(ScanShared& sh, const ScanArgs
         }
         fast = encode_perm(sh.buf + 16, start, n, key);
     }
+    if (a.ablate & 64u) atomicAdd((unsigned long long*)&a.st->stamp[fast ? 3 : r], 1ull);  // diag: outcome counts
     if (fast) count_code(sh, a, tile0, p, key);
     else slow_header(sh, a, tile0, p, nb, r, start, n);
 }
@@ -909,9 +918,9 @@ __device__ __forceinline__ void process_header_bm(ScanShared& sh, const ScanArgs
 // header list, no block scan: the tile's line prefix (count_tile) gives each lane its index.
 __device__ __forceinline__ void parse_own_headers(ScanShared& sh, const ScanArgs& a, u32 t, const TileCount& tc,
                                                   u64 L0, int tid) {
-    const u64 tile0 = (u64)t * TILE;
+    const u64 tile0 = (u64)t * TSTEP;
     const u32 nb = (u32)min((u64)(TILE + HALO), a.avail - tile0);
-    const u32 tlen = (u32)min((u64)TILE, a.len - tile0);
+    const u32 tlen = (u32)min((u64)TSTEP, a.len - tile0);
     const u32 s0 = tid * SEG;
     const bool own0 = t == 0 && tid == 0 && a.own_start && (L0 & 3ull) == 0 && a.avail > 0 &&
                       (a.max_records <= 0 || (i64)(L0 >> 2) < a.max_records);
@@ -931,7 +940,7 @@ __device__ __forceinline__ void parse_own_headers(ScanShared& sh, const ScanArgs
             }
         }
         if (pend < 0) break;
-        process_header_bm(sh, a, tile0, (u32)pend, tlen, nb);
+        process_header_bm(sh, a, tile0, (u32)pend, min((u32)TILE, nb), nb);
         pend = -1;
     }
 }

@@ -286,7 +286,7 @@ fr_ctx* fr_create(int device, uint64_t chunk_bytes, uint64_t table_slots) {
     if ((e = hipStreamCreateWithFlags(&ctx->copy, hipStreamNonBlocking)) != hipSuccess) return bad("stream", e);
     hipDeviceProp_t prop;
     if ((e = hipGetDeviceProperties(&prop, device)) != hipSuccess) return bad("props", e);
-    const int per_cu = 4;  // ~40 KB LDS and <= 128 VGPRs per workgroup -> 4 per CU
+    const int per_cu = chunk_occupancy();  // ~40 KB LDS per workgroup; VGPRs sized by __launch_bounds__
     ctx->grid = prop.multiProcessorCount * per_cu;
     if (const char* g = getenv("FR_GRID")) ctx->grid = std::max(1, atoi(g));
     if (const char* f = getenv("FR_FLUSH_AT")) ctx->flush_at = (u32)atoi(f);

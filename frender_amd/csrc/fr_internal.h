@@ -146,6 +146,7 @@ __host__ __device__ inline u64 mix64(u64 x) {
 // ---- launchers (fr_kernels.hip) --------------------------------------------------
 hipError_t launch_table_init(GSlot* slots, u64 n, hipStream_t s);
 hipError_t launch_chunk_scan(const ScanArgs& a, int grid, hipStream_t s);
+int chunk_occupancy();  // tally workgroups per CU the kernel is built for
 hipError_t launch_reinsert_overflow(Table t, DevState* st, const Overflow* src, u64 n, hipStream_t s);
 hipError_t launch_rehash(Table dst, DevState* st, const GSlot* src, u64 nsrc, hipStream_t s);
 hipError_t launch_compact(const GSlot* slots, u64 nslots, u64* keys, u64* counts, u64* first, u32* pos,

@@ -60,10 +60,18 @@ __device__ __forceinline__ u32 classify4(u32 w) {
     return ch & ((c0 & ~m8) | (c1 & m8)) & ~kill;
 }
 
-// gather bit k of each of the 4 bytes into a 4-bit mask (byte i -> bit i)
+// Class K of 16 bytes (four class words, byte i of word j = position 4j + i) -> a 16-bit mask.
+// v_dot4_u32_u8 gathers the flag bytes at full rate: weights 1,2,4,8 place word 0's bytes at
+// bits 0-3, weights 16..128 word 1's at bits 4-7 (every product is scaled by 2^K, undone at
+// the end); no quarter-rate 32-bit multiplies.
 template <int K>
-__device__ __forceinline__ u32 gather4(u32 c) {
-    return ((((c >> K) & 0x01010101u) * 0x00204081u) >> 21) & 0xFu;
+__device__ __forceinline__ u32 gather16(u32 c0, u32 c1, u32 c2, u32 c3) {
+    constexpr u32 M = 0x01010101u << K;
+    u32 v = __builtin_amdgcn_udot4(c0 & M, 0x08040201u, 0u, false);
+    v = __builtin_amdgcn_udot4(c1 & M, 0x80402010u, v, false);
+    u32 u = __builtin_amdgcn_udot4(c2 & M, 0x08040201u, 0u, false);
+    u = __builtin_amdgcn_udot4(c3 & M, 0x80402010u, u, false);
+    return (v | (u << 8)) >> K;
 }
 
 __device__ __forceinline__ u64 agent_load(const u64* p) {
@@ -194,6 +202,10 @@ __device__ __forceinline__ void lds_insert(ScanShared& sh, const ScanArgs& a, u6
             mino = 0xFFFFFFFFu;
         }
         if (k == key) {
+            if (a.ablate & 256u) {  // ablation: probe only
+                asm volatile("" ::"v"(mino));
+                return;
+            }
             atomicAdd(&sh.ls[h].cnt, 1u);
             // mino only decreases, so a stale read can only cause a redundant atomic
             if (off < mino) atomicMin(&sh.ls[h].mino, off);
@@ -479,36 +491,53 @@ struct TileRegs {
     uint4 pre;  // the 16 bytes before the tile (thread 0; UTF-8 continuation checks)
 };
 
-__device__ __forceinline__ void tile_fetch(const ScanArgs& a, u32 t, TileRegs& r, int tid) {
-    if (t >= a.num_tiles) return;
+// Prefetch: unconditional 16-B loads whose results are not touched until tile_stage, so the
+// loads stay in flight through the parse of the current tile (any select or branch on a loaded
+// value makes the compiler wait for it at once).  Addresses are clamped into the readable
+// range; tile_stage zeroes / re-reads the few vectors at the data end.
+// Branch-free: with want == false (or t past the range) the descriptors hold zero records, so
+// the loads return zeros without touching memory; the caller never branches around a fetch
+// (a conditional fetch makes the compiler copy and wait for the loaded registers at once).
+__device__ __forceinline__ void tile_fetch(const ScanArgs& a, u32 t, TileRegs& r, int tid, bool want = true) {
+    const bool live = want && t < a.num_tiles;
+    const u64 tile0 = live ? (u64)t * TSTEP : 0ull;
+    const u32 nb = live ? (u32)min((u64)(TILE + HALO), a.avail - tile0) : 0u;
+    // wave-uniform buffer descriptors over [tile0, tile0 + nb) and the 16 bytes before the tile:
+    // 32-bit lane offsets (one VGPR for all five loads), hardware range check past the end
+    const u64 base = (u64)(a.buf + tile0);
+    const u32 lo = __builtin_amdgcn_readfirstlane((u32)base), hi = __builtin_amdgcn_readfirstlane((u32)(base >> 32));
+    const u8* ub = (const u8*)(((u64)hi << 32) | lo);
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)ub, (short)0, (int)__builtin_amdgcn_readfirstlane(nb),
+                                                        0x00020000);
+    const bool pre_ok = live && (tile0 >= 16 || a.pre_valid);
+    const auto prsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(pre_ok ? ub - 16 : ub), (short)0, pre_ok ? 16 : 0,
+                                                         0x00020000);
+#pragma unroll
+    for (int k = 0; k < STAGE_VECS; ++k) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, tid * 16, k * WG * 16, 0);
+        r.v[k] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+    const auto pv = __builtin_amdgcn_raw_buffer_load_b128(prsrc, 0, 0, 0);
+    r.pre = make_uint4(pv[0], pv[1], pv[2], pv[3]);
+}
+
+__device__ __forceinline__ void tile_stage(ScanShared& sh, const ScanArgs& a, u32 t, const TileRegs& r, int tid) {
     const u64 tile0 = (u64)t * TSTEP;
     const u32 nb = (u32)min((u64)(TILE + HALO), a.avail - tile0);
 #pragma unroll
     for (int k = 0; k < STAGE_VECS; ++k) {
         const u32 off = tid * 16 + k * WG * 16;
-        uint4 v = make_uint4(0u, 0u, 0u, 0u);
-        if (off + 16 <= nb) {
-            v = *(const uint4*)(a.buf + tile0 + off);
-        } else if (off < nb) {
-            u32 w[4] = {0u, 0u, 0u, 0u};
-            for (u32 j = 0; off + j < nb; ++j) w[j >> 2] |= (u32)a.buf[tile0 + off + j] << (8 * (j & 3));
-            v = make_uint4(w[0], w[1], w[2], w[3]);
+        if (off < (u32)(TILE + HALO)) {
+            uint4 v = r.v[k];
+            if (off + 16u > nb) {  // the data end: bytes past it read as zero (rare, synchronous)
+                u32 w[4] = {0u, 0u, 0u, 0u};
+                for (u32 q = 0; off + q < nb; ++q) w[q >> 2] |= (u32)a.buf[tile0 + off + q] << (8 * (q & 3));
+                v = make_uint4(w[0], w[1], w[2], w[3]);
+            }
+            *(uint4*)(sh.buf + 16 + off) = v;
         }
-        r.v[k] = v;
     }
-    if (tid == 0) {
-        r.pre = make_uint4(0u, 0u, 0u, 0u);
-        if (tile0 >= 16 || a.pre_valid) r.pre = *(const uint4*)(a.buf + tile0 - 16);
-    }
-}
-
-__device__ __forceinline__ void tile_stage(ScanShared& sh, const TileRegs& r, int tid) {
-#pragma unroll
-    for (int k = 0; k < STAGE_VECS; ++k) {
-        const u32 off = tid * 16 + k * WG * 16;
-        if (off < (u32)(TILE + HALO)) *(uint4*)(sh.buf + 16 + off) = r.v[k];
-    }
-    if (tid == 0) *(uint4*)(sh.buf) = r.pre;
+    if (tid == 0) *(uint4*)(sh.buf) = r.pre;  // zeros when not readable (fetch descriptor)
 }
 
 struct TileCount {
@@ -535,23 +564,23 @@ __device__ __forceinline__ TileCount count_tile(ScanShared& sh, const ScanArgs& 
         sh.bcol[tid] = 0;
         sh.beol[tid] = 0;
     } else {  // bitmaps for every staged segment; terminators / UTF-8 only for the tile's own bytes
-        u64 nl = 0, cr = 0, sp = 0, col = 0;
+        u32 nl16[4], cr16[4], sp16[4], col16[4];
         u32 hiw = 0;
 #pragma unroll
         for (int qv = 0; qv < SEG / 16; ++qv) {
             const uint4 v = *(const uint4*)(sh.buf + 16 + s0 + qv * 16);
-            const u32 w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int sh4 = qv * 16 + k * 4;
-                const u32 c = classify4(w[k]);
-                nl |= (u64)gather4<0>(c) << sh4;
-                cr |= (u64)gather4<1>(c) << sh4;
-                sp |= (u64)gather4<2>(c) << sh4;
-                col |= (u64)gather4<3>(c) << sh4;
-                hiw |= w[k];
-            }
+            const u32 c0 = classify4(v.x), c1 = classify4(v.y), c2 = classify4(v.z), c3 = classify4(v.w);
+            nl16[qv] = gather16<0>(c0, c1, c2, c3);
+            cr16[qv] = gather16<1>(c0, c1, c2, c3);
+            sp16[qv] = gather16<2>(c0, c1, c2, c3);
+            col16[qv] = gather16<3>(c0, c1, c2, c3);
+            hiw |= v.x | v.y | v.z | v.w;
         }
+        auto join = [](const u32 (&g)[4]) {
+            return ((u64)(g[2] | (g[3] << 16)) << 32) | (u64)(g[0] | (g[1] << 16));
+        };
+        const u64 nl = join(nl16), cr = join(cr16);
+        u64 sp = join(sp16), col = join(col16);
         const u64 nxt = (s0 + SEG < nb && sh.buf[16 + s0 + SEG] == '\n') ? 1ull : 0ull;
         u64 tm = nl | (cr & ~((nl >> 1) | (nxt << 63)));
         u64 eol = nl | cr;
@@ -862,17 +891,10 @@ __device__ __forceinline__ int locate_code_bm(const ScanShared& sh, u32 p, u32 b
     const u32 w = p >> 6, b = p & 63u;
     const bool has1 = (w + 1u) * 64u < bl;
     const u32 wn = has1 ? w + 1u : w;
-    u64 s0 = sh.bsp[w], s1 = sh.bsp[wn], e0 = sh.beol[w], e1 = sh.beol[wn], c0 = sh.bcol[w], c1 = sh.bcol[wn];
-    if (!has1) s1 = e1 = c1 = 0;
-    // shift the window so that bit 0 is position p
-    const u32 rb = 64u - b;
-    s0 = (s0 >> b) | (b ? s1 << rb : 0ull);
-    s1 >>= b;
-    e0 = (e0 >> b) | (b ? e1 << rb : 0ull);
-    e1 >>= b;
-    c0 = (c0 >> b) | (b ? c1 << rb : 0ull);
-    c1 >>= b;
-    u64 v0 = s0 | e0, v1 = s1 | e1;
+    const u64 s0 = sh.bsp[w], s1 = sh.bsp[wn], e0 = sh.beol[w], e1 = sh.beol[wn];
+    u64 c0 = sh.bcol[w], c1 = sh.bcol[wn];
+    // window positions are relative to segment w: [b, 64) of it, then segment w+1
+    u64 v0 = (s0 | e0) & (~0ull << b), v1 = has1 ? (s1 | e1) : 0ull;
     if (!(v0 | v1)) return 2;
     const u32 f1 = first128(v0, v1);                       // the first ' ' or line end
     if ((f1 < 64u ? (e0 >> f1) : (e1 >> (f1 - 64u))) & 1ull) return 1;
@@ -885,9 +907,9 @@ __device__ __forceinline__ int locate_code_bm(const ScanShared& sh, u32 p, u32 b
     u64 k0, k1;
     below128(f2, k0, k1);
     c0 &= k0 & ~m0;                                        // ':' strictly inside (f1, f2)
-    c1 &= k1 & ~m1;
+    c1 = has1 ? (c1 & k1 & ~m1) : 0ull;
     const u32 lastc = c1 ? 127u - (u32)__builtin_clzll(c1) : c0 ? 63u - (u32)__builtin_clzll(c0) : f1;
-    start = p + lastc + 1u;
+    start = w * 64u + lastc + 1u;
     n = f2 - lastc - 1u;
     return 0;
 }
@@ -920,26 +942,32 @@ __device__ __forceinline__ void parse_own_headers(ScanShared& sh, const ScanArgs
                                                   u64 L0, int tid) {
     const u64 tile0 = (u64)t * TSTEP;
     const u32 nb = (u32)min((u64)(TILE + HALO), a.avail - tile0);
-    const u32 tlen = (u32)min((u64)TSTEP, a.len - tile0);
+    const u32 rem = (u32)min(a.len - tile0, (u64)0xFFFFFFFFu);  // line starts p < rem lie in the range
     const u32 s0 = tid * SEG;
     const bool own0 = t == 0 && tid == 0 && a.own_start && (L0 & 3ull) == 0 && a.avail > 0 &&
                       (a.max_records <= 0 || (i64)(L0 >> 2) < a.max_records);
+    // the i-th terminator (from 0) of this segment starts line lb + i + 1: a header line when
+    // i = 3 - lb (mod 4); skip to the first such terminator, then step four at a time
+    const u64 lb = L0 + tc.wexcl + (tc.x - tc.c);
+    const u32 skip = (3u - (u32)lb) & 3u;
     u64 m = tc.tmask;
-    u64 l = L0 + tc.wexcl + (tc.x - tc.c);
-    int pend = own0 ? 0 : -1;  // the next header position of this lane, -1 none
+#pragma unroll
+    for (u32 q = 0; q < 3; ++q) m = q < skip ? (m & (m - 1)) : m;
+    u64 rec = (lb + skip + 1u) >> 2;  // record index of the next candidate (-s)
+    int pend = own0 ? 0 : -1;
     for (;;) {
-        while (pend < 0 && m) {
-            const int j = __ffsll((long long)m) - 1;
+        if (pend < 0) {
+            if (!m) break;
+            const u32 p = s0 + (u32)__builtin_ctzll(m) + 1u;
             m &= m - 1;
-            l += 1;
-            if ((l & 3ull) == 0) {
-                const u32 p = s0 + (u32)j + 1u;
-                const u64 gp = tile0 + p;
-                const bool mine = gp < a.len || (a.own_end && gp == a.len && gp < a.avail);
-                if (mine && (a.max_records <= 0 || (i64)(l >> 2) < a.max_records)) pend = (int)p;
-            }
+            m &= m - 1;
+            m &= m - 1;
+            m &= m - 1;
+            const bool mine = p < rem || (a.own_end && tile0 + p == a.len && tile0 + p < a.avail);
+            if (!mine || (a.max_records > 0 && (i64)rec >= a.max_records)) break;  // so are all later ones
+            rec += 1;
+            pend = (int)p;
         }
-        if (pend < 0) break;
         process_header_bm(sh, a, tile0, (u32)pend, min((u32)TILE, nb), nb);
         pend = -1;
     }
@@ -959,20 +987,20 @@ __device__ __forceinline__ u64 walk_chunk(ScanShared& sh, const ScanArgs& a, u32
 #if FR_PREFETCH
     TileRegs r;
     tile_fetch(a, tb, r, tid);
-    tile_stage(sh, r, tid);
+    tile_stage(sh, a, tb, r, tid);
     __syncthreads();
     TileCount tc = count_tile(sh, a, tb, tid, lane, wid, false);
     STAMP(4);
     for (u32 t = tb; t < te; ++t) {
         const bool more = t + 1 < te;
-        if (more) tile_fetch(a, t + 1, r, tid);  // lands while this tile is parsed
+        tile_fetch(a, t + 1, r, tid, more);  // lands while this tile is parsed
         if (parse && !uniform_flag(sh.spec_bad) && !(a.ablate & 1u))
             parse_own_headers(sh, a, t, tc, L0 + lines, tid);
         __syncthreads();
         STAMP(1);
         lines += tc.tot;
         if (more) {
-            tile_stage(sh, r, tid);
+            tile_stage(sh, a, t + 1, r, tid);
             __syncthreads();
             STAMP(2);
             tc = count_tile(sh, a, t + 1, tid, lane, wid, false);
@@ -985,7 +1013,7 @@ __device__ __forceinline__ u64 walk_chunk(ScanShared& sh, const ScanArgs& a, u32
         {
             TileRegs r;
             tile_fetch(a, t, r, tid);
-            tile_stage(sh, r, tid);
+            tile_stage(sh, a, t, r, tid);
         }
         __syncthreads();
         STAMP(2);
@@ -1006,7 +1034,10 @@ __device__ __forceinline__ u64 walk_chunk(ScanShared& sh, const ScanArgs& a, u32
     return lines;
 }
 
-__global__ __launch_bounds__(WG, 4) void chunk_kernel(ScanArgs a) {
+#ifndef FR_OCC
+#define FR_OCC 4  // workgroups (= waves per SIMD) per CU; fr_api sizes the grid with fr_chunk_occupancy()
+#endif
+__global__ __launch_bounds__(WG, FR_OCC) void chunk_kernel(ScanArgs a) {
     __shared__ ScanShared sh;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -1045,7 +1076,7 @@ __global__ __launch_bounds__(WG, 4) void chunk_kernel(ScanArgs a) {
         } else if (a.max_records <= 0) {
             TileRegs r;
             tile_fetch(a, tb, r, tid);
-            tile_stage(sh, r, tid);
+            tile_stage(sh, a, tb, r, tid);
             __syncthreads();
             const TileCount tc0 = count_tile(sh, a, tb, tid, lane, wid, false);
             sh.bsp[tid] = tc0.tmask;
@@ -1105,6 +1136,8 @@ __global__ __launch_bounds__(WG, 4) void chunk_kernel(ScanArgs a) {
         if (sh.flags & 2u) atomicOr(&a.st->utf8_bad, 1u);
     }
 }
+
+int chunk_occupancy() { return FR_OCC; }
 
 hipError_t launch_chunk_scan(const ScanArgs& a, int grid, hipStream_t s) {
     hipLaunchKernelGGL(chunk_kernel, dim3(grid), dim3(WG), 0, s, a);

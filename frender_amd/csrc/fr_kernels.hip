@@ -182,7 +182,8 @@ __device__ __forceinline__ u64 make_ord(const ScanArgs& a, u64 off_in_range) {
 }
 
 __device__ __forceinline__ void lds_insert(ScanShared& sh, const ScanArgs& a, u64 key, u32 off) {
-    u32 h = (u32)((key * 0x9E3779B97F4A7C15ull) >> (64 - LOG_NS));
+    // one 32-bit multiply (keys hold <= 63 bits: fold the top down first)
+    u32 h = (((u32)key ^ (u32)(key >> 27)) * 0x9E3779B1u) >> (32 - LOG_NS);
     for (int pr = 0; pr < LPROBE; ++pr) {
         typedef u32 u32x4 __attribute__((ext_vector_type(4)));
         const u32x4 sl = *(const volatile u32x4*)&sh.ls[h];
@@ -202,10 +203,6 @@ __device__ __forceinline__ void lds_insert(ScanShared& sh, const ScanArgs& a, u6
             mino = 0xFFFFFFFFu;
         }
         if (k == key) {
-            if (a.ablate & 256u) {  // ablation: probe only
-                asm volatile("" ::"v"(mino));
-                return;
-            }
             atomicAdd(&sh.ls[h].cnt, 1u);
             // mino only decreases, so a stale read can only cause a redundant atomic
             if (off < mino) atomicMin(&sh.ls[h].mino, off);

@@ -30,6 +30,7 @@ struct fr_ctx {
 
     DevState* st = nullptr;
     DevState* h_st = nullptr;      // pinned snapshot
+    bool st_fresh = false;         // h_st equals the device state (no device work on it since)
     hipEvent_t st_ev = nullptr;
     bool st_pending = false;
     u64* tiles = nullptr;
@@ -138,13 +139,17 @@ static int state_reset_counts(fr_ctx* ctx) {
     *ctx->h_st = z;
     CK(hipMemcpyAsync(ctx->st, ctx->h_st, sizeof(DevState), hipMemcpyHostToDevice, ctx->stream));
     CK(hipStreamSynchronize(ctx->stream));
+    ctx->st_pending = false;
+    ctx->st_fresh = true;
     return FR_OK;
 }
 
-static int read_state(fr_ctx* ctx) {  // synchronous exact snapshot
+static int read_state(fr_ctx* ctx) {  // exact snapshot (a host round trip only when stale)
+    if (ctx->st_fresh && !ctx->st_pending) return FR_OK;
     CK(hipMemcpyAsync(ctx->h_st, ctx->st, sizeof(DevState), hipMemcpyDeviceToHost, ctx->stream));
     CK(hipStreamSynchronize(ctx->stream));
     ctx->st_pending = false;
+    ctx->st_fresh = true;
     return FR_OK;
 }
 
@@ -177,6 +182,7 @@ static int grow_table(fr_ctx* ctx, bool force_bigger) {
         ctx->tab.ovf = fresh;
         CK(hipMemsetAsync(&ctx->st->n_overflow, 0, sizeof(u64), ctx->stream));
         CK(launch_reinsert_overflow(ctx->tab, ctx->st, old, novf, ctx->stream));
+        ctx->st_fresh = false;
         CK(hipStreamSynchronize(ctx->stream));
         CK(hipFree(old));
     }
@@ -249,6 +255,7 @@ static int launch_range(fr_ctx* ctx, const u8* dptr, u64 len, u64 avail, int own
         a.epoch = 1;
     }
     CK(hipMemsetAsync(&ctx->st->ticket, 0, sizeof(u32), ctx->stream));
+    ctx->st_fresh = false;
     if (ctx->ev_used == ctx->ev_a.size()) {
         hipEvent_t e1, e2;
         CK(hipEventCreate(&e1));
@@ -492,6 +499,9 @@ int fr_begin_file(fr_ctx* ctx, int64_t max_records) {
     CK(hipMemsetAsync(&ctx->st->lines[0], 0, 2 * sizeof(u64), ctx->stream));
     CK(hipMemsetAsync(&ctx->st->err_nospace, 0xFF, sizeof(u64), ctx->stream));
     CK(hipMemsetAsync(&ctx->st->nonascii, 0, 2 * sizeof(u32), ctx->stream));
+    ctx->h_st->lines[0] = ctx->h_st->lines[1] = 0;  // the snapshot stays exact
+    ctx->h_st->err_nospace = ~0ull;
+    ctx->h_st->nonascii = ctx->h_st->utf8_bad = 0;
     ctx->file_tag++;
     ctx->file_offset = 0;
     ctx->max_records = max_records > 0 ? max_records : 0;
@@ -574,6 +584,10 @@ int fr_feed_device(fr_ctx* ctx, const uint8_t* dev_data, uint64_t len) {
         CK(hipMemcpyAsync(&b, dev_data + len - 1, 1, hipMemcpyDeviceToHost, ctx->stream));
         CK(hipStreamSynchronize(ctx->stream));
         ctx->last_byte = b;
+        if (ctx->st_pending) {  // the snapshot queued after the last launch has landed
+            ctx->st_pending = false;
+            ctx->st_fresh = true;
+        }
     }
     ctx->carry.clear();
     return FR_OK;
@@ -597,6 +611,7 @@ int fr_end_file(fr_ctx* ctx, fr_file_stats* out) {
     if (rc) return rc;
     rc = ensure_presence_cap(ctx);
     if (rc) return rc;
+    ctx->st_fresh = false;
     CK(launch_presence_scan(ctx->tab.slots, ctx->nslots, ctx->file_tag, ctx->tab.pres, ctx->tab.pres_cap, ctx->st,
                             ctx->stream));
     rc = read_state(ctx);
@@ -894,6 +909,7 @@ int fr_merge_unique_device(fr_ctx* ctx, const void* dev_keys, const void* dev_co
         rc = grow_table(ctx, true);
         if (rc) return rc;
     }
+    ctx->st_fresh = false;
     CK(launch_merge(ctx->tab, ctx->st, (const u64*)dev_keys, (const u64*)dev_counts, (const u64*)dev_first, n,
                     ctx->stream));
     return grow_table(ctx, false);

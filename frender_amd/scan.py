@@ -69,39 +69,71 @@ class UniqueTable:
         return {c: int(n) for c, n in zip(self.codes, self.counts)}
 
 
-def _gz_chunks(path, chunk=READ_CHUNK, depth=2):
-    """Inflate in a helper thread (zlib releases the GIL) while the GPU consumes."""
-    q: queue.Queue = queue.Queue(maxsize=depth)
-    stop = threading.Event()
+class _GzReader:
+    """Inflate one .gz file in a helper thread (zlib releases the GIL) into a bounded queue of
+    decoded chunks.  tally_barcodes keeps up to `cores` of these running ahead of the file the
+    GPU is consuming: the reference parallelises over files with a Pool (frender.py:189-193);
+    here the files inflate in parallel and the GPU tallies them in order."""
 
-    def work():
+    def __init__(self, path, chunk=READ_CHUNK, depth=2):
+        self.q: queue.Queue = queue.Queue(maxsize=depth)
+        self.stop = threading.Event()
+        self.t = threading.Thread(target=self._work, args=(path, chunk), daemon=True)
+        self.t.start()
+
+    def _work(self, path, chunk):
         try:
             with gzip.open(path, "rb") as g:
-                while not stop.is_set():
+                while not self.stop.is_set():
                     b = g.read(chunk)
-                    q.put(b)
+                    self.q.put(b)
                     if not b:
                         return
         except BaseException as e:  # noqa: BLE001 - re-raised in the consumer
-            q.put(e)
+            self.q.put(e)
 
-    t = threading.Thread(target=work, daemon=True)
-    t.start()
-    try:
+    def __iter__(self):
         while True:
-            item = q.get()
+            item = self.q.get()
             if isinstance(item, BaseException):
                 raise item
             if not item:
                 return
             yield item
-    finally:
-        stop.set()
-        while t.is_alive():
+
+    def close(self):
+        self.stop.set()
+        while self.t.is_alive():
             try:
-                q.get_nowait()
+                self.q.get_nowait()
             except queue.Empty:
-                t.join(0.01)
+                self.t.join(0.01)
+
+
+def _file_done(ctx, st, fi, exo, exo_seen):
+    """Per-file epilogue of scan_file (frender.py:160-181): the reference's exceptions for bad
+    input, and the exotic codes of this file merged by string.  Returns (exo_seen, new_here)."""
+    if st.error == _lib.FR_SCAN_NO_SPACE:  # frender.py:169 split(" ")[1]
+        raise IndexError("list index out of range")
+    if st.error == _lib.FR_SCAN_UTF8:  # gzip.open(..., "rt") decode (frender.py:159)
+        raise UnicodeDecodeError("utf-8", b"", 0, 1, "invalid start byte")
+    new_here = int(st.new_keys)
+    if st.exotic:
+        ords, lens, offs, pool = ctx.exotic(exo_seen, int(st.exotic))
+        for k in range(len(ords)):
+            code = bytes(pool[int(offs[k]):int(offs[k]) + int(lens[k])]).decode("utf-8")
+            e = exo.get(code)
+            if e is None:
+                exo[code] = [1, int(ords[k]), {fi}]
+                new_here += 1
+            else:
+                e[0] += 1
+                e[1] = min(e[1], int(ords[k]))
+                if fi not in e[2]:
+                    e[2].add(fi)
+                    new_here += 1
+        exo_seen += len(ords)
+    return exo_seen, new_here
 
 
 def tally_barcodes(cores, files, sample=None, ctx=None) -> UniqueTable:
@@ -115,37 +147,31 @@ def tally_barcodes(cores, files, sample=None, ctx=None) -> UniqueTable:
     names, records = [], []
     exo: dict = {}
     exo_seen = 0
-    for fi, path in enumerate(files):
-        name = str(os.path.basename(path))
-        names.append(name)
-        print(f"Tallying barcodes from {name}...", end="")
-        ctx.begin_file(sample)
-        for chunk in _gz_chunks(path):
-            if ctx.feed(chunk):
-                break
-        st = ctx.end_file()
-        if st.error == _lib.FR_SCAN_NO_SPACE:  # frender.py:169 split(" ")[1]
-            raise IndexError("list index out of range")
-        if st.error == _lib.FR_SCAN_UTF8:  # gzip.open(..., "rt") decode (frender.py:159)
-            raise UnicodeDecodeError("utf-8", b"", 0, 1, "invalid start byte")
-        new_here = int(st.new_keys)
-        if st.exotic:
-            ords, lens, offs, pool = ctx.exotic(exo_seen, int(st.exotic))
-            for k in range(len(ords)):
-                code = bytes(pool[int(offs[k]):int(offs[k]) + int(lens[k])]).decode("utf-8")
-                e = exo.get(code)
-                if e is None:
-                    exo[code] = [1, int(ords[k]), {fi}]
-                    new_here += 1
-                else:
-                    e[0] += 1
-                    e[1] = min(e[1], int(ords[k]))
-                    if fi not in e[2]:
-                        e[2].add(fi)
-                        new_here += 1
-            exo_seen += len(ords)
-        records.append(int(st.records))
-        print(f"found {new_here} new barcode{'' if new_here == 1 else 's'} in {st.records} reads.")
+    ahead = max(1, int(cores))
+    readers: dict = {}
+    try:
+        for fi, path in enumerate(files):
+            for j in range(fi, min(len(files), fi + ahead)):
+                if j not in readers:
+                    readers[j] = _GzReader(files[j])
+            name = str(os.path.basename(path))
+            names.append(name)
+            print(f"Tallying barcodes from {name}...", end="")
+            ctx.begin_file(sample)
+            rd = readers.pop(fi)
+            try:
+                for chunk in rd:
+                    if ctx.feed(chunk):
+                        break
+            finally:
+                rd.close()
+            st = ctx.end_file()
+            exo_seen, new_here = _file_done(ctx, st, fi, exo, exo_seen)
+            records.append(int(st.records))
+            print(f"found {new_here} new barcode{'' if new_here == 1 else 's'} in {st.records} reads.")
+    finally:
+        for rd in readers.values():
+            rd.close()
     print(type([]), len(files))
     ctx.finalize()
     keys, counts, first = ctx.unique()

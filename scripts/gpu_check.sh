@@ -12,8 +12,38 @@ if [[ $STAGE == all || $STAGE == test ]]; then
       > gpurun_out/pytest_gpu.log 2>&1
   rc=$?
   tail -30 gpurun_out/pytest_gpu.log
-  echo "pytest exit $rc"
-  if [[ $rc -ne 0 && $rc -ne 1 ]]; then exit $rc; fi
+  echo "pytest if [[ $STAGE == dist ]]; then  # multi-rank rehearsal on this box's GPU (gloo): merged table == one-GPU table
+  timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+      --master-port 29511 bench.py --gpus 2 --steps 2 --warmup 1 --reads 10000000 --no-cpu --dist-backend gloo \
+      ${DIST_ARGS:-} > gpurun_out/dist2.log 2>&1 || { echo "dist run failed"; tail -5 gpurun_out/dist2.log; exit 1; }
+  timeout -k 10 300 python bench.py --steps 2 --warmup 1 --reads 20000000 --no-cpu ${DIST_ARGS:-} \
+      > gpurun_out/dist1.log 2>&1 || { echo "single run failed"; exit 1; }
+  python - <<'PY'
+import json
+a = [json.loads(l) for l in open("gpurun_out/dist2.log") if l.startswith("{")][0]
+b = [json.loads(l) for l in open("gpurun_out/dist1.log") if l.startswith("{")][0]
+print("merged uniques", a["config"]["unique_codes"], "single", b["config"]["unique_codes"])
+assert a["config"]["unique_codes"] == b["config"]["unique_codes"]
+PY
+  rc=$?
+fi
+exit $rc"
+  if [[ $rc -ne 0 && $rc -ne 1 ]]; then if [[ $STAGE == dist ]]; then  # multi-rank rehearsal on this box's GPU (gloo): merged table == one-GPU table
+  timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+      --master-port 29511 bench.py --gpus 2 --steps 2 --warmup 1 --reads 10000000 --no-cpu --dist-backend gloo \
+      ${DIST_ARGS:-} > gpurun_out/dist2.log 2>&1 || { echo "dist run failed"; tail -5 gpurun_out/dist2.log; exit 1; }
+  timeout -k 10 300 python bench.py --steps 2 --warmup 1 --reads 20000000 --no-cpu ${DIST_ARGS:-} \
+      > gpurun_out/dist1.log 2>&1 || { echo "single run failed"; exit 1; }
+  python - <<'PY'
+import json
+a = [json.loads(l) for l in open("gpurun_out/dist2.log") if l.startswith("{")][0]
+b = [json.loads(l) for l in open("gpurun_out/dist1.log") if l.startswith("{")][0]
+print("merged uniques", a["config"]["unique_codes"], "single", b["config"]["unique_codes"])
+assert a["config"]["unique_codes"] == b["config"]["unique_codes"]
+PY
+  rc=$?
+fi
+exit $rc; fi
 fi
 if [[ $STAGE == all || $STAGE == bench ]]; then
   timeout -k 10 400 python bench.py --steps 5 --warmup 2 ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1
@@ -28,5 +58,20 @@ if [[ $STAGE == all || $STAGE == prof ]]; then
   p=$?; tail -3 "$GRAFT_REPO_ROOT/gpurun_out/prof.log"; echo "prof exit $p"
   cd "$GRAFT_REPO_ROOT"
   find gpurun_out/prof -name "*kernel_stats.csv" -exec head -20 {} \;
+fi
+if [[ $STAGE == dist ]]; then  # multi-rank rehearsal on this box's GPU (gloo): merged table == one-GPU table
+  timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+      --master-port 29511 bench.py --gpus 2 --steps 2 --warmup 1 --reads 10000000 --no-cpu --dist-backend gloo \
+      ${DIST_ARGS:-} > gpurun_out/dist2.log 2>&1 || { echo "dist run failed"; tail -5 gpurun_out/dist2.log; exit 1; }
+  timeout -k 10 300 python bench.py --steps 2 --warmup 1 --reads 20000000 --no-cpu ${DIST_ARGS:-} \
+      > gpurun_out/dist1.log 2>&1 || { echo "single run failed"; exit 1; }
+  python - <<'PY'
+import json
+a = [json.loads(l) for l in open("gpurun_out/dist2.log") if l.startswith("{")][0]
+b = [json.loads(l) for l in open("gpurun_out/dist1.log") if l.startswith("{")][0]
+print("merged uniques", a["config"]["unique_codes"], "single", b["config"]["unique_codes"])
+assert a["config"]["unique_codes"] == b["config"]["unique_codes"]
+PY
+  rc=$?
 fi
 exit $rc

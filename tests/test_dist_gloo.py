@@ -74,3 +74,50 @@ def test_tree_merge_gloo(world, seed):
             want[k] = (c0 + c, min(f0, f))
     assert got == sorted(want.items())
     assert n == len(want)
+
+
+def _worker_a2a(rank, world, port, seed, out):
+    from frender_amd.dist import owner_of, partition_exchange, reduce_sum
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    table = _table(rank, seed)
+    rows = torch.tensor([[k, c, f] for k, (c, f) in sorted(table.items())], dtype=torch.int64).reshape(-1, 3)
+    mine = partition_exchange(dist, "cpu", rows)
+    part = {}
+    for k, c, f in mine.tolist():
+        assert int(owner_of(torch.tensor([k]), world)[0]) == rank  # only codes this rank owns
+        c0, f0 = part.get(k, (0, 1 << 62))
+        part[k] = (c0 + c, min(f0, f))
+    total = reduce_sum(dist, "cpu", [len(part)])[0]
+    out.put((rank, sorted(part.items()), total))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,seed", [(2, 5), (3, 6), (4, 7)])
+def test_partition_exchange_gloo(world, seed):
+    """The hash-partitioned all-to-all merge: every code lands on exactly one owner and the
+    union of the merged partitions equals the merged table (count = sum, first = min)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_a2a, args=(r, world, port, seed, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    union = {}
+    for _, items, _ in got:
+        for k, v in items:
+            assert k not in union
+            union[k] = v
+    want = {}
+    for r in range(world):
+        for k, (c, f) in _table(r, seed).items():
+            c0, f0 = want.get(k, (0, 1 << 62))
+            want[k] = (c0 + c, min(f0, f))
+    assert union == want
+    assert all(t == len(want) for _, _, t in got)

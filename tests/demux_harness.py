@@ -1,0 +1,62 @@
+"""Shared runner for the demux golden cases (tests/golden/demux/*, made by the reference)."""
+import argparse
+import contextlib
+import gzip
+import io
+import json
+import os
+import shutil
+import tempfile
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CASES = os.path.join(HERE, "golden", "demux")
+
+
+def case_names():
+    return sorted(os.listdir(CASES)) if os.path.isdir(CASES) else []
+
+
+def run_case(name, demux_fn):
+    """Run demux_fn(args) on the case's inputs; return a list of differences (empty = parity)."""
+    case = os.path.join(CASES, name)
+    flags = json.load(open(os.path.join(case, "spec.json")))["flags"]
+    exp_dir = os.path.join(case, "expected")
+    diffs = []
+    with tempfile.TemporaryDirectory() as tmp:
+        shutil.copytree(os.path.join(case, "inputs"), os.path.join(tmp, "inputs"))
+        inp = os.path.join(tmp, "inputs")
+        args = argparse.Namespace(r=os.path.join(inp, "results.csv"), d=os.path.join(tmp, "out"), o=flags.get("o"),
+                                  no_index_hop=flags.get("no_index_hop", False),
+                                  no_ambiguous=flags.get("no_ambiguous", False),
+                                  no_undeter=flags.get("no_undeter", False),
+                                  no_samples=flags.get("no_samples", False),
+                                  files=[os.path.join(inp, f) for f in sorted(os.listdir(inp)) if f.endswith(".gz")])
+        buf = io.StringIO()
+        err = None
+        with contextlib.redirect_stdout(buf):
+            try:
+                demux_fn(args)
+            except BaseException as e:  # noqa: BLE001
+                err = {"type": type(e).__name__, "message": str(e).replace(tmp, "<case>")}
+        want_err = None
+        if os.path.exists(os.path.join(exp_dir, "error.json")):
+            want_err = json.load(open(os.path.join(exp_dir, "error.json")))
+        if err != want_err:
+            diffs.append(f"error: got {err} want {want_err}")
+        want_out = open(os.path.join(exp_dir, "stdout.txt")).read()
+        if buf.getvalue().replace(tmp, "<case>") != want_out:
+            diffs.append(f"stdout: got {buf.getvalue()!r} want {want_out!r}")
+        if want_err is None:
+            outd = os.path.join(tmp, "out")
+            got = sorted(os.listdir(outd)) if os.path.isdir(outd) else []
+            want = sorted(f[:-len(".content.gz")] for f in os.listdir(exp_dir) if f.endswith(".content.gz"))
+            if got != want:
+                diffs.append(f"output files: got {got} want {want}")
+            for fn in set(got) & set(want):
+                with gzip.open(os.path.join(outd, fn), "rb") as g:
+                    a = g.read()
+                with gzip.open(os.path.join(exp_dir, fn + ".content.gz"), "rb") as g:
+                    b = g.read()
+                if a != b:
+                    diffs.append(f"{fn}: content differs ({len(a)} vs {len(b)} bytes)")
+    return diffs

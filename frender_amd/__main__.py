@@ -1,6 +1,7 @@
-"""`python -m frender_amd scan ...` — the reference's CLI (frender.py:817-930), scan on MI355X."""
+"""`python -m frender_amd scan|demux ...` — the reference's CLI (frender.py:817-930) on MI355X."""
 import argparse
 import sys
+from datetime import datetime, timezone
 
 
 def main(argv=None):
@@ -22,13 +23,35 @@ def main(argv=None):
                    help=".csv barcode association table; required unless a directory holding one is given")
     p.add_argument("files", nargs="+", help="Fastq file(s) or a directory of fastq files")
     p.set_defaults(cmd="scan")
+    d = sub.add_parser("demux", help="Demultiplex paired fastq files using a frender scan result file")
+    d.add_argument("-i", "--no-index-hop", action="store_true",
+                   help="don't split index hop reads into their own file (will be included in undetermined file "
+                        "unless -u is set)")
+    d.add_argument("-a", "--no-ambiguous", action="store_true",
+                   help="don't split ambiguous reads into their own file (will be included in undetermined file "
+                        "unless -u is set)")
+    d.add_argument("-u", "--no-undeter", action="store_true", help="do NOT produce undetermined files")
+    d.add_argument("-s", "--no-samples", action="store_true", help="do NOT produce individual sample files")
+    d.add_argument("-o", metavar="output_name", help="name infix for output files")
+    d.add_argument("-d", metavar="output_dir",
+                   default=f"./frender-demux-output_{datetime.strftime(datetime.now(timezone.utc), '%Y-%M-%d_%H%M_%Z')}/",
+                   help="output directory (default: ./frender-demux-output_{date_time}/)")
+    d.add_argument("-r", metavar="result_file", required=True, help="REQUIRED: frender scan result file")
+    d.add_argument("--gz-level", type=int, default=9,
+                   help="gzip level of the outputs (the reference writes gzip.open's default, 9)")
+    d.add_argument("files", nargs="+", help="Fastq file, list of fastq files, or directory path")
+    d.set_defaults(cmd="demux")
     args = parser.parse_args(argv)
-    if getattr(args, "cmd", None) != "scan":
-        parser.print_help()
-        return 2
-    from .scan import frender_scan
-    frender_scan(args)
-    return 0
+    if getattr(args, "cmd", None) == "scan":
+        from .scan import frender_scan
+        frender_scan(args)
+        return 0
+    if getattr(args, "cmd", None) == "demux":
+        from .demux import frender_demux
+        frender_demux(args)
+        return 0
+    parser.print_help()
+    return 2
 
 
 if __name__ == "__main__":

@@ -78,6 +78,17 @@ _SIGS = {
     "fr_copy_to_device": (C.c_int, [P, P, P, C.c_uint64]),
     "fr_synth_device": (C.c_int, [P, P, C.c_uint64, C.c_uint64, C.c_int, C.c_uint64, C.c_char_p, C.c_char_p,
                                   C.c_int, C.c_int, C.c_int]),
+    # demux (row f-1)
+    "fr_dmx_create": (P, [C.c_int]),
+    "fr_dmx_destroy": (None, [P]),
+    "fr_dmx_last_error": (C.c_char_p, [P]),
+    "fr_dmx_set_table": (C.c_int, [P, P, P, C.c_uint64]),
+    "fr_dmx_load": (C.c_int, [P, C.c_int, P, C.c_uint64, u64p]),
+    "fr_dmx_records": (C.c_int, [P, C.c_int, P, C.c_uint64, P, P]),
+    "fr_dmx_exotic": (C.c_int, [P, C.c_uint64, P, C.c_uint64, u64p]),
+    "fr_dmx_patch": (C.c_int, [P, P, P, C.c_uint64]),
+    "fr_dmx_route": (C.c_int, [P, C.c_int, C.c_uint64, C.POINTER(C.c_int64), C.POINTER(C.c_int32), P, P]),
+    "fr_dmx_fetch": (C.c_int, [P, C.c_int, P, C.c_uint64]),
 }
 for _name, (_res, _args) in _SIGS.items():
     _f = getattr(lib, _name)
@@ -112,6 +123,90 @@ def pack_lower(s: str) -> int:
     for i, ch in enumerate(s):
         v |= {"a": 1, "c": 2, "g": 3, "t": 4, "n": 5}.get(ch, 7) << (3 * i)
     return v
+
+
+FR_DMX_MISSING, FR_DMX_BADTYPE, FR_DMX_EXOTIC = -1, -2, -3
+
+
+def pack_fast(codes) -> tuple:
+    """Codes over {A,C,G,T,N,+} of 1..21 chars -> (3-bit packed keys, mask of the packable codes)."""
+    keys = np.zeros(len(codes), dtype=np.uint64)
+    ok = np.zeros(len(codes), dtype=bool)
+    sym = {"A": 1, "C": 2, "G": 3, "T": 4, "N": 5, "+": 6}
+    for i, c in enumerate(codes):
+        if not 1 <= len(c) <= 21:
+            continue
+        v = 0
+        for j, ch in enumerate(c):
+            s = sym.get(ch)
+            if s is None:
+                break
+            v |= s << (3 * j)
+        else:
+            keys[i] = v
+            ok[i] = True
+    return keys, ok
+
+
+class Demux:
+    """One GPU's demux state (fr_dmx): see include/frender_amd.h."""
+
+    def __init__(self, device: int = 0):
+        self.h = lib.fr_dmx_create(device)
+        err = lib.fr_dmx_last_error(self.h) if self.h else b"fr_dmx_create returned NULL"
+        if err:
+            raise FrenderError(f"fr_dmx_create: {err.decode()}")
+
+    def _ck(self, rc, what):
+        if rc != FR_OK:
+            raise FrenderError(f"{what}: {lib.fr_dmx_last_error(self.h).decode()} (rc={rc})")
+
+    def close(self):
+        if self.h:
+            lib.fr_dmx_destroy(self.h)
+            self.h = None
+
+    def set_table(self, keys: np.ndarray, vals: np.ndarray):
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        vals = np.ascontiguousarray(vals, dtype=np.int32)
+        self._ck(lib.fr_dmx_set_table(self.h, _ptr(keys), _ptr(vals), keys.size), "fr_dmx_set_table")
+
+    def load(self, mate: int, data) -> int:
+        a = np.frombuffer(data, dtype=np.uint8)
+        n = C.c_uint64()
+        self._ck(lib.fr_dmx_load(self.h, mate, _ptr(a), a.size, C.byref(n)), "fr_dmx_load")
+        return n.value
+
+    def records(self, mate: int, recs) -> tuple:
+        r = np.ascontiguousarray(recs, dtype=np.uint64)
+        s, e = np.empty(r.size, np.uint64), np.empty(r.size, np.uint64)
+        self._ck(lib.fr_dmx_records(self.h, mate, _ptr(r), r.size, _ptr(s), _ptr(e)), "fr_dmx_records")
+        return s, e
+
+    def exotic(self, n_pairs: int) -> np.ndarray:
+        n = C.c_uint64()
+        self._ck(lib.fr_dmx_exotic(self.h, n_pairs, None, 0, C.byref(n)), "fr_dmx_exotic")
+        out = np.empty(n.value, np.uint64)
+        if n.value:
+            self._ck(lib.fr_dmx_exotic(self.h, n_pairs, _ptr(out), n.value, C.byref(n)), "fr_dmx_exotic")
+        return out
+
+    def patch(self, recs, dest):
+        r = np.ascontiguousarray(recs, dtype=np.uint64)
+        d = np.ascontiguousarray(dest, dtype=np.int32)
+        self._ck(lib.fr_dmx_patch(self.h, _ptr(r), _ptr(d), r.size), "fr_dmx_patch")
+
+    def route(self, n_dest: int, n_pairs: int):
+        fe, ev = C.c_int64(), C.c_int32()
+        b1, b2 = np.zeros(n_dest, np.uint64), np.zeros(n_dest, np.uint64)
+        self._ck(lib.fr_dmx_route(self.h, n_dest, n_pairs, C.byref(fe), C.byref(ev), _ptr(b1), _ptr(b2)),
+                 "fr_dmx_route")
+        return fe.value, ev.value, b1, b2
+
+    def fetch(self, mate: int, nbytes: int) -> bytes:
+        out = np.empty(nbytes, np.uint8)
+        self._ck(lib.fr_dmx_fetch(self.h, mate, _ptr(out), nbytes), "fr_dmx_fetch")
+        return out.tobytes()
 
 
 class Context:

@@ -1,0 +1,528 @@
+// fr_demux.hip — SURVEY.md §8.1 row (f-1): `demux` (frender.py:733-814) on the GPU.
+//
+// The reference's hot loop walks R1/R2 record pairs in lockstep, takes the code after the last
+// ':' of the R2 header line (frender.py:778), looks it up in the scan results and appends both
+// records to the writer pair of the result's read type / sample (frender.py:779-810).  Here one
+// pair of decoded files is resident in HBM and:
+//   dmx_count  newline count per 16-KiB tile (HBM-bound streaming read)
+//   scan       exclusive prefix of the tile counts (rocprim)
+//   dmx_index  record starts (every 4th line start) and, for R2, the code -> destination lookup
+//              in an open-addressing table of the results' fast codes
+//   route      stable partition of the record pairs by destination (rocprim radix sort on the
+//              destination, record index as payload), output offsets (rocprim scans) and a
+//              gather-copy of both mates' record bytes into destination-major buffers
+// The host inflates, normalises universal newlines (frender.py:776 reads in text mode), resolves
+// the rare codes outside the fast alphabet, raises the reference's errors, and gzips each
+// destination's bytes into its writer pair.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include <rocprim/rocprim.hpp>
+
+#include "../../include/frender_amd.h"
+#include "fr_internal.h"
+
+namespace fr {
+namespace {
+
+constexpr int DT = 16384;        // tile bytes
+constexpr int DWG = 256;         // lanes per workgroup: 64 B each
+constexpr int DSEG = DT / DWG;
+constexpr int DHALO = 1024;      // bytes staged past the tile for headers that cross it
+constexpr int DMAXSYM = MAXSYM;  // fast key: <= 21 symbols
+
+__device__ __forceinline__ u32 nl_mask4(u32 w) {  // exact '\n' bytes -> bits 0..3
+    const u32 t = w ^ 0x0A0A0A0Au;
+    const u32 z = ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;
+    return __builtin_amdgcn_udot4(z >> 7, 0x08040201u, 0u, false);
+}
+
+__device__ __forceinline__ u32 sym_byte(u32 c) {  // A1 C2 G3 T4 N5 +6, else 0
+    switch (c) {
+        case 'A': return 1;
+        case 'C': return 2;
+        case 'G': return 3;
+        case 'T': return 4;
+        case 'N': return 5;
+        case '+': return 6;
+        default: return 0;
+    }
+}
+
+struct DmxTable {
+    const u64* keys;  // 0 = empty
+    const int32_t* vals;
+    u64 mask;
+};
+
+__device__ __forceinline__ int32_t table_get(const DmxTable& t, u64 key) {
+    if (!t.keys) return FR_DMX_MISSING;
+    u64 h = mix64(key) & t.mask;
+    for (;;) {
+        const u64 k = t.keys[h];
+        if (k == key) return t.vals[h];
+        if (k == 0) return FR_DMX_MISSING;
+        h = (h + 1) & t.mask;
+    }
+}
+
+__global__ void dmx_table_insert(u64* keys, int32_t* vals, u64 mask, const u64* in_k, const int32_t* in_v, u64 n) {
+    for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
+        const u64 key = in_k[i];
+        u64 h = mix64(key) & mask;
+        for (;;) {
+            const u64 old = atomicCAS((unsigned long long*)&keys[h], 0ull, (unsigned long long)key);
+            if (old == 0 || old == key) {
+                vals[h] = in_v[i];
+                break;
+            }
+            h = (h + 1) & mask;
+        }
+    }
+}
+
+// 64 bytes of lane `tid` of tile t (zeros past len) -> '\n' bitmap
+__device__ __forceinline__ u64 lane_nl(const u8* buf, u64 len, u64 tile0, int tid) {
+    const u64 base = tile0 + (u64)tid * DSEG;
+    u64 m = 0;
+    if (base + DSEG <= len) {
+#pragma unroll
+        for (int q = 0; q < DSEG / 16; ++q) {
+            const uint4 v = *(const uint4*)(buf + base + q * 16);
+            m |= (u64)(nl_mask4(v.x) | (nl_mask4(v.y) << 4) | (nl_mask4(v.z) << 8) | (nl_mask4(v.w) << 12)) << (16 * q);
+        }
+    } else if (base < len) {
+        for (u64 j = 0; base + j < len; ++j) m |= (u64)(buf[base + j] == '\n') << j;
+    }
+    return m;
+}
+
+__global__ __launch_bounds__(DWG) void dmx_count(const u8* buf, u64 len, u32 ntiles, u32* tile_cnt) {
+    __shared__ u32 ws[DWG / 64];
+    for (u32 t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        u32 c = __popcll(lane_nl(buf, len, (u64)t * DT, threadIdx.x));
+        for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+        if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
+        __syncthreads();
+        if (threadIdx.x == 0) tile_cnt[t] = ws[0] + ws[1] + ws[2] + ws[3];
+        __syncthreads();
+    }
+}
+
+// the code of the header line starting at p: text after the line's last ':' up to its '\n'
+// (frender.py:778) -> destination; bytes come from the staged tile when inside it
+__device__ int32_t header_dest(const u8* buf, u64 len, u64 p, const u8* lds, u64 lds0, u32 lds_n,
+                               const DmxTable& tab) {
+    auto rd = [&](u64 q) -> u32 { return (q >= lds0 && q - lds0 < lds_n) ? (u32)lds[q - lds0] : (u32)buf[q]; };
+    u64 e = p, lastc = ~0ull;
+    while (e < len) {
+        const u32 c = rd(e);
+        if (c == '\n') break;
+        if (c == ':') lastc = e;
+        ++e;
+    }
+    const u64 s = lastc == ~0ull ? p : lastc + 1;
+    const u64 n = e - s;
+    if (n == 0 || n > (u64)DMAXSYM) return FR_DMX_EXOTIC;
+    u64 key = 0;
+    for (u64 i = 0; i < n; ++i) {
+        const u32 sy = sym_byte(rd(s + i));
+        if (!sy) return FR_DMX_EXOTIC;
+        key |= (u64)sy << (3 * i);
+    }
+    return table_get(tab, key);
+}
+
+__global__ __launch_bounds__(DWG) void dmx_index(const u8* buf, u64 len, u32 ntiles, const u64* tile_base,
+                                                 u64* rec_start, int32_t* rec_dest, DmxTable tab) {
+    __shared__ u8 lds[DT + DHALO];
+    __shared__ u32 ws[DWG / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    for (u32 t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const u64 tile0 = (u64)t * DT;
+        const u32 lds_n = (u32)min((u64)(DT + DHALO), len - tile0);
+        if (rec_dest) {
+            for (u32 i = tid * 16; i < lds_n; i += DWG * 16) {
+                if (i + 16 <= lds_n) *(uint4*)(lds + i) = *(const uint4*)(buf + tile0 + i);
+                else
+                    for (u32 j = i; j < lds_n; ++j) lds[j] = buf[tile0 + j];
+            }
+        }
+        const u64 m = lane_nl(buf, len, tile0, tid);
+        const u32 c = __popcll(m);
+        u32 x = c;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const u32 y = __shfl_up(x, d, 64);
+            if (lane >= d) x += y;
+        }
+        if (lane == 63) ws[wid] = x;
+        __syncthreads();
+        u64 L = tile_base[t] + (x - c);
+        for (int w = 0; w < wid; ++w) L += ws[w];
+        // line start after each '\n' of this lane's segment: line index L + rank + 1
+        u64 mm = m;
+        while (mm) {
+            const u32 j = __builtin_ctzll(mm);
+            mm &= mm - 1;
+            L += 1;
+            const u64 p = tile0 + (u64)tid * DSEG + j + 1;
+            if ((L & 3ull) == 0 && p < len) {
+                rec_start[L >> 2] = p;
+                if (rec_dest) rec_dest[L >> 2] = header_dest(buf, len, p, lds, tile0, lds_n, tab);
+            }
+        }
+        if (t == 0 && tid == 0 && len > 0) {  // the first line of the file
+            rec_start[0] = 0;
+            if (rec_dest) rec_dest[0] = header_dest(buf, len, 0, lds, tile0, lds_n, tab);
+        }
+        __syncthreads();
+    }
+}
+
+__global__ void dmx_first_error(const int32_t* dest, u64 n, unsigned long long* first) {
+    for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x)
+        if (dest[i] < 0) atomicMin(first, (unsigned long long)i);
+}
+
+__global__ void dmx_keys(const int32_t* dest, u64 n, u32* keys, u32* idx) {
+    for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
+        keys[i] = (u32)dest[i];
+        idx[i] = (u32)i;
+    }
+}
+
+// lengths of both mates' records in partition order
+__global__ void dmx_lengths(const u32* perm, u64 n, const u64* rs1, const u64* rs2, u64* len1, u64* len2) {
+    for (u64 j = blockIdx.x * (u64)blockDim.x + threadIdx.x; j < n; j += (u64)gridDim.x * blockDim.x) {
+        const u32 i = perm[j];
+        len1[j] = rs1[i + 1] - rs1[i];
+        len2[j] = rs2[i + 1] - rs2[i];
+    }
+}
+
+// first partition position of every destination present (sorted keys: one boundary each, no atomics)
+__global__ void dmx_bounds(const u32* sk, u64 n, u32* first) {
+    for (u64 j = blockIdx.x * (u64)blockDim.x + threadIdx.x; j < n; j += (u64)gridDim.x * blockDim.x)
+        if (j == 0 || sk[j] != sk[j - 1]) first[sk[j]] = (u32)j;
+}
+
+// byte offset of every destination's first record (n_dest entries, + the total at [n_dest])
+__global__ void dmx_dest_offsets(const u32* first, int n_dest, u64 n, const u64* o1, const u64* l1, const u64* o2,
+                                 const u64* l2, u64* off1, u64* off2) {
+    const int d = blockIdx.x * blockDim.x + threadIdx.x;
+    if (d > n_dest) return;
+    const u64 tot1 = o1[n - 1] + l1[n - 1], tot2 = o2[n - 1] + l2[n - 1];
+    // an absent destination starts where the next present one does
+    int e = d;
+    while (e < n_dest && first[e] == 0xFFFFFFFFu) ++e;
+    off1[d] = e < n_dest ? o1[first[e]] : tot1;
+    off2[d] = e < n_dest ? o2[first[e]] : tot2;
+}
+
+// one wave per output record: coalesced byte copies
+__global__ void dmx_copy(const u32* perm, u64 n, const u64* rs, const u8* src, const u64* off, u8* dst) {
+    const int lane = threadIdx.x & 63;
+    const u64 waves = (u64)gridDim.x * (blockDim.x / 64);
+    for (u64 j = blockIdx.x * (u64)(blockDim.x / 64) + (threadIdx.x >> 6); j < n; j += waves) {
+        const u32 i = perm[j];
+        const u64 s = rs[i], e = rs[i + 1], o = off[j];
+        for (u64 q = s + lane; q < e; q += 64) dst[o + (q - s)] = src[q];
+    }
+}
+
+int grid_for(u64 n, int per = 256, int cap = 8192) {
+    return (int)std::max<u64>(1, std::min<u64>((n + per - 1) / per, (u64)cap));
+}
+
+}  // namespace
+}  // namespace fr
+
+using namespace fr;
+
+struct fr_dmx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    // results table
+    u64* tkeys = nullptr;
+    int32_t* tvals = nullptr;
+    u64 tmask = 0;
+    // per mate: data, record starts (+ sentinel), destinations (R2)
+    u8* data[2] = {nullptr, nullptr};
+    u64 cap[2] = {0, 0};
+    u64 len[2] = {0, 0};
+    u64* rs[2] = {nullptr, nullptr};
+    u64 rs_cap[2] = {0, 0};
+    u64 nrec[2] = {0, 0};
+    int32_t* dest = nullptr;
+    u64 dest_cap = 0;
+    // route outputs
+    u8* out[2] = {nullptr, nullptr};
+    u64 out_cap[2] = {0, 0};
+    u64 out_len[2] = {0, 0};
+};
+
+#define DK(x)                                                                  \
+    do {                                                                       \
+        hipError_t e_ = (x);                                                   \
+        if (e_ != hipSuccess) {                                                \
+            d->err = std::string(#x) + ": " + hipGetErrorString(e_);           \
+            return FR_ERR_HIP;                                                 \
+        }                                                                      \
+    } while (0)
+
+template <class T>
+static hipError_t ensure(T** p, u64& cap, u64 n) {
+    if (n <= cap && *p) return hipSuccess;
+    if (*p) {
+        hipError_t e = hipFree(*p);
+        if (e != hipSuccess) return e;
+        *p = nullptr;
+    }
+    cap = std::max<u64>(n + n / 4, 1024);
+    return hipMalloc((void**)p, cap * sizeof(T));
+}
+
+extern "C" {
+
+fr_dmx* fr_dmx_create(int device) {
+    fr_dmx* d = new fr_dmx();
+    d->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess)
+        d->err = "fr_dmx_create: no usable HIP device";
+    return d;
+}
+
+void fr_dmx_destroy(fr_dmx* d) {
+    if (!d) return;
+    (void)hipSetDevice(d->device);
+    if (d->stream) (void)hipStreamSynchronize(d->stream);
+    void* p[] = {d->tkeys, d->tvals, d->data[0], d->data[1], d->rs[0], d->rs[1], d->dest, d->out[0], d->out[1]};
+    for (void* x : p)
+        if (x) (void)hipFree(x);
+    if (d->stream) (void)hipStreamDestroy(d->stream);
+    delete d;
+}
+
+const char* fr_dmx_last_error(const fr_dmx* d) { return d ? d->err.c_str() : "null context"; }
+
+int fr_dmx_set_table(fr_dmx* d, const uint64_t* keys, const int32_t* vals, uint64_t n) {
+    DK(hipSetDevice(d->device));
+    if (d->tkeys) DK(hipFree(d->tkeys));
+    if (d->tvals) DK(hipFree(d->tvals));
+    d->tkeys = nullptr;
+    d->tvals = nullptr;
+    u64 slots = 1024;
+    while (slots < 2 * n) slots <<= 1;
+    d->tmask = slots - 1;
+    DK(hipMalloc(&d->tkeys, slots * 8));
+    DK(hipMalloc(&d->tvals, slots * 4));
+    DK(hipMemsetAsync(d->tkeys, 0, slots * 8, d->stream));
+    if (n) {
+        u64* k = nullptr;
+        int32_t* v = nullptr;
+        DK(hipMalloc(&k, n * 8));
+        DK(hipMalloc(&v, n * 4));
+        DK(hipMemcpyAsync(k, keys, n * 8, hipMemcpyHostToDevice, d->stream));
+        DK(hipMemcpyAsync(v, vals, n * 4, hipMemcpyHostToDevice, d->stream));
+        hipLaunchKernelGGL(dmx_table_insert, dim3(grid_for(n)), dim3(256), 0, d->stream, d->tkeys, d->tvals, d->tmask,
+                           k, v, n);
+        DK(hipGetLastError());
+        DK(hipStreamSynchronize(d->stream));
+        DK(hipFree(k));
+        DK(hipFree(v));
+    }
+    return FR_OK;
+}
+
+int fr_dmx_load(fr_dmx* d, int mate, const uint8_t* data, uint64_t len, uint64_t* n_records) {
+    if (mate < 0 || mate > 1) return d->err = "mate must be 0 (R1) or 1 (R2)", FR_ERR_INVALID;
+    DK(hipSetDevice(d->device));
+    DK(ensure(&d->data[mate], d->cap[mate], len + 16));
+    if (len) DK(hipMemcpyAsync(d->data[mate], data, len, hipMemcpyHostToDevice, d->stream));
+    d->len[mate] = len;
+    const u32 ntiles = (u32)((len + DT - 1) / DT);
+    u32* cnt = nullptr;
+    u64* base = nullptr;
+    DK(hipMalloc(&cnt, std::max<u64>(ntiles, 1) * 4));
+    DK(hipMalloc(&base, (u64)(ntiles + 1) * 8));
+    if (ntiles) {
+        hipLaunchKernelGGL(dmx_count, dim3(std::min<u32>(ntiles, 8192)), dim3(DWG), 0, d->stream, d->data[mate], len,
+                           ntiles, cnt);
+        DK(hipGetLastError());
+        size_t tb = 0;
+        DK(rocprim::exclusive_scan(nullptr, tb, cnt, base, (u64)0, (size_t)ntiles + 0, rocprim::plus<u64>(), d->stream));
+        void* tmp = nullptr;
+        DK(hipMalloc(&tmp, std::max<size_t>(tb, 1)));
+        DK(rocprim::exclusive_scan(tmp, tb, cnt, base, (u64)0, (size_t)ntiles, rocprim::plus<u64>(), d->stream));
+        DK(hipStreamSynchronize(d->stream));
+        DK(hipFree(tmp));
+    }
+    // lines = '\n' count + a last line without one
+    u64 nl = 0;
+    if (ntiles) {
+        u64 last_base = 0;
+        u32 last_cnt = 0;
+        DK(hipMemcpy(&last_base, base + ntiles - 1, 8, hipMemcpyDeviceToHost));
+        DK(hipMemcpy(&last_cnt, cnt + ntiles - 1, 4, hipMemcpyDeviceToHost));
+        nl = last_base + last_cnt;
+    }
+    u8 lastb = '\n';
+    if (len) DK(hipMemcpy(&lastb, d->data[mate] + len - 1, 1, hipMemcpyDeviceToHost));
+    const u64 lines = nl + ((len && lastb != '\n') ? 1 : 0);
+    const u64 nrec = (lines + 3) / 4;
+    DK(ensure(&d->rs[mate], d->rs_cap[mate], nrec + 1));
+    if (mate == 1) DK(ensure(&d->dest, d->dest_cap, nrec + 1));
+    DK(hipMemcpyAsync(d->rs[mate] + nrec, &len, 8, hipMemcpyHostToDevice, d->stream));  // sentinel
+    if (ntiles) {
+        DmxTable tab{d->tkeys, d->tvals, d->tmask};
+        hipLaunchKernelGGL(dmx_index, dim3(std::min<u32>(ntiles, 4096)), dim3(DWG), 0, d->stream, d->data[mate], len,
+                           ntiles, base, d->rs[mate], mate == 1 ? d->dest : nullptr, tab);
+        DK(hipGetLastError());
+    }
+    DK(hipStreamSynchronize(d->stream));
+    DK(hipFree(cnt));
+    DK(hipFree(base));
+    d->nrec[mate] = nrec;
+    *n_records = nrec;
+    return FR_OK;
+}
+
+int fr_dmx_records(fr_dmx* d, int mate, const uint64_t* recs, uint64_t n, uint64_t* starts, uint64_t* ends) {
+    DK(hipSetDevice(d->device));
+    std::vector<u64> all;
+    for (u64 k = 0; k < n; ++k) {
+        if (recs[k] >= d->nrec[mate]) return d->err = "record index out of range", FR_ERR_INVALID;
+        u64 se[2];
+        DK(hipMemcpy(se, d->rs[mate] + recs[k], 16, hipMemcpyDeviceToHost));
+        starts[k] = se[0];
+        ends[k] = se[1];
+    }
+    return FR_OK;
+}
+
+int fr_dmx_exotic(fr_dmx* d, uint64_t n_pairs, uint64_t* recs, uint64_t cap, uint64_t* n) {
+    DK(hipSetDevice(d->device));
+    n_pairs = std::min<u64>(n_pairs, d->nrec[1]);
+    std::vector<int32_t> h(n_pairs);
+    if (n_pairs) DK(hipMemcpy(h.data(), d->dest, n_pairs * 4, hipMemcpyDeviceToHost));
+    u64 k = 0;
+    for (u64 i = 0; i < n_pairs; ++i)
+        if (h[i] == FR_DMX_EXOTIC) {
+            if (k < cap) recs[k] = i;
+            ++k;
+        }
+    *n = k;
+    return FR_OK;
+}
+
+int fr_dmx_patch(fr_dmx* d, const uint64_t* recs, const int32_t* dest, uint64_t n) {
+    DK(hipSetDevice(d->device));
+    for (u64 k = 0; k < n; ++k) {
+        if (recs[k] >= d->nrec[1]) return d->err = "record index out of range", FR_ERR_INVALID;
+        DK(hipMemcpyAsync(d->dest + recs[k], dest + k, 4, hipMemcpyHostToDevice, d->stream));
+    }
+    DK(hipStreamSynchronize(d->stream));
+    return FR_OK;
+}
+
+int fr_dmx_route(fr_dmx* d, int n_dest, uint64_t n_pairs, int64_t* first_error, int32_t* error_val,
+                 uint64_t* bytes_r1, uint64_t* bytes_r2) {
+    DK(hipSetDevice(d->device));
+    const u64 P = std::min<u64>({n_pairs, d->nrec[0], d->nrec[1]});
+    if (P >= 0xFFFFFFFFull) return d->err = "too many records in one file pair", FR_ERR_CAPACITY;
+    *first_error = -1;
+    *error_val = 0;
+    for (int k = 0; k < n_dest; ++k) bytes_r1[k] = bytes_r2[k] = 0;
+    d->out_len[0] = d->out_len[1] = 0;
+    if (!P) return FR_OK;
+    unsigned long long* fe = nullptr;
+    DK(hipMalloc(&fe, 8));
+    DK(hipMemsetAsync(fe, 0xFF, 8, d->stream));
+    hipLaunchKernelGGL(dmx_first_error, dim3(grid_for(P)), dim3(256), 0, d->stream, d->dest, P, fe);
+    DK(hipGetLastError());
+    u64 first = 0;
+    DK(hipMemcpyAsync(&first, fe, 8, hipMemcpyDeviceToHost, d->stream));
+    DK(hipStreamSynchronize(d->stream));
+    DK(hipFree(fe));
+    if (first != ~0ull) {
+        int32_t v = 0;
+        DK(hipMemcpy(&v, d->dest + first, 4, hipMemcpyDeviceToHost));
+        *first_error = (int64_t)first;
+        *error_val = v;
+        return FR_OK;
+    }
+    // stable partition by destination
+    u32 *k_in = nullptr, *k_out = nullptr, *i_in = nullptr, *perm = nullptr;
+    u64 *l1 = nullptr, *l2 = nullptr, *o1 = nullptr, *o2 = nullptr;
+    u32* first_pos = nullptr;
+    u64 *off1 = nullptr, *off2 = nullptr;
+    DK(hipMalloc(&k_in, P * 4));
+    DK(hipMalloc(&k_out, P * 4));
+    DK(hipMalloc(&i_in, P * 4));
+    DK(hipMalloc(&perm, P * 4));
+    DK(hipMalloc(&l1, P * 8));
+    DK(hipMalloc(&l2, P * 8));
+    DK(hipMalloc(&o1, P * 8));
+    DK(hipMalloc(&o2, P * 8));
+    DK(hipMalloc(&first_pos, (u64)std::max(n_dest, 1) * 4));
+    DK(hipMalloc(&off1, (u64)(n_dest + 1) * 8));
+    DK(hipMalloc(&off2, (u64)(n_dest + 1) * 8));
+    DK(hipMemsetAsync(first_pos, 0xFF, (u64)std::max(n_dest, 1) * 4, d->stream));
+    hipLaunchKernelGGL(dmx_keys, dim3(grid_for(P)), dim3(256), 0, d->stream, d->dest, P, k_in, i_in);
+    DK(hipGetLastError());
+    int bits = 1;
+    while ((1 << bits) < n_dest) ++bits;
+    size_t tb = 0;
+    DK(rocprim::radix_sort_pairs(nullptr, tb, k_in, k_out, i_in, perm, (size_t)P, 0, (unsigned)bits, d->stream));
+    void* tmp = nullptr;
+    size_t tb2 = 0;
+    DK(rocprim::exclusive_scan(nullptr, tb2, l1, o1, (u64)0, (size_t)P, rocprim::plus<u64>(), d->stream));
+    DK(hipMalloc(&tmp, std::max<size_t>(std::max(tb, tb2), 1)));
+    DK(rocprim::radix_sort_pairs(tmp, tb, k_in, k_out, i_in, perm, (size_t)P, 0, (unsigned)bits, d->stream));
+    hipLaunchKernelGGL(dmx_lengths, dim3(grid_for(P)), dim3(256), 0, d->stream, perm, P, d->rs[0], d->rs[1], l1, l2);
+    DK(hipGetLastError());
+    hipLaunchKernelGGL(dmx_bounds, dim3(grid_for(P)), dim3(256), 0, d->stream, k_out, P, first_pos);
+    DK(hipGetLastError());
+    DK(rocprim::exclusive_scan(tmp, tb2, l1, o1, (u64)0, (size_t)P, rocprim::plus<u64>(), d->stream));
+    DK(rocprim::exclusive_scan(tmp, tb2, l2, o2, (u64)0, (size_t)P, rocprim::plus<u64>(), d->stream));
+    hipLaunchKernelGGL(dmx_dest_offsets, dim3((n_dest + 256) / 256), dim3(256), 0, d->stream, first_pos, n_dest, P,
+                       o1, l1, o2, l2, off1, off2);
+    DK(hipGetLastError());
+    std::vector<u64> h1(n_dest + 1), h2(n_dest + 1);
+    DK(hipMemcpyAsync(h1.data(), off1, (n_dest + 1) * 8, hipMemcpyDeviceToHost, d->stream));
+    DK(hipMemcpyAsync(h2.data(), off2, (n_dest + 1) * 8, hipMemcpyDeviceToHost, d->stream));
+    DK(hipStreamSynchronize(d->stream));
+    for (int k = 0; k < n_dest; ++k) {
+        bytes_r1[k] = h1[k + 1] - h1[k];
+        bytes_r2[k] = h2[k + 1] - h2[k];
+    }
+    const u64 s1 = h1[n_dest], s2 = h2[n_dest];
+    DK(ensure(&d->out[0], d->out_cap[0], s1 + 16));
+    DK(ensure(&d->out[1], d->out_cap[1], s2 + 16));
+    const int cg = grid_for(P, 4, 16384);
+    hipLaunchKernelGGL(dmx_copy, dim3(cg), dim3(256), 0, d->stream, perm, P, d->rs[0], d->data[0], o1, d->out[0]);
+    DK(hipGetLastError());
+    hipLaunchKernelGGL(dmx_copy, dim3(cg), dim3(256), 0, d->stream, perm, P, d->rs[1], d->data[1], o2, d->out[1]);
+    DK(hipGetLastError());
+    DK(hipStreamSynchronize(d->stream));
+    void* fr[] = {k_in, k_out, i_in, perm, l1, l2, o1, o2, first_pos, off1, off2, tmp};
+    for (void* x : fr) DK(hipFree(x));
+    d->out_len[0] = s1;
+    d->out_len[1] = s2;
+    return FR_OK;
+}
+
+int fr_dmx_fetch(fr_dmx* d, int mate, uint8_t* out, uint64_t len) {
+    if (mate < 0 || mate > 1 || len > d->out_len[mate]) return d->err = "fr_dmx_fetch: bad mate or length", FR_ERR_INVALID;
+    DK(hipSetDevice(d->device));
+    if (len) DK(hipMemcpy(out, d->out[mate], len, hipMemcpyDeviceToHost));
+    return FR_OK;
+}
+
+}  // extern "C"

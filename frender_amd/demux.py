@@ -1,0 +1,188 @@
+"""frender `demux` with the record routing on the GPU.
+
+Mirrors frender.py:645-814: the same results-file check, writer names, R1/R2 pairing, stdout
+lines and failure modes.  Per file pair, the decoded R1 and R2 text goes to the GPU
+(libfrender_hip.so, fr_dmx_* in include/frender_amd.h), which finds every record, resolves the
+R2 code of each pair against the results and gathers both mates' records destination-major;
+the host inflates, resolves the rare codes outside the fast alphabet, raises the reference's
+errors and gzips each destination's bytes into its writer pair (threads: zlib releases the GIL).
+"""
+from __future__ import annotations
+
+import csv
+import gzip
+import os
+import re
+import threading
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+
+import numpy as np
+
+from . import _lib
+from .host import parse_files
+
+RESULTS_HEADER = ["idx1", "idx2", "reads", "matched_idx1", "matched_idx2", "read_type", "sample_name"]
+
+
+def parse_results_file(result_file) -> dict:
+    """frender.py:645-664 (asserts the README column order): code -> (read_type, sample_id)."""
+    with open(result_file, newline="") as f:
+        rd = csv.reader(f)
+        header = next(rd)
+        assert header[0:7] == RESULTS_HEADER, f"${result_file} does not appear to be a valid frender result file!"
+        return {line[0] + "+" + line[1]: (line[5], line[6]) for line in rd}
+
+
+def open_files(name, out_dir, infix, level):
+    """frender.py:667-676."""
+    if not out_dir.endswith("/"):
+        out_dir += "/"
+    return {read: gzip.open(f"{out_dir}{name}_frender-demux_{infix + '_' if infix else ''}{read}.fq.gz", "wb",
+                            compresslevel=level) for read in ("R1", "R2")}
+
+
+def is_read_mate(str1, str2) -> bool:
+    """frender.py:685-693."""
+    if len([0 for a, b in zip(str1, str2) if a != b]) != 1:
+        return False
+    r1 = int(re.search("_R[12]_", str1)[0].replace("_", "").replace("R", ""))
+    r2 = int(re.search("_R[12]_", str2)[0].replace("_", "").replace("R", ""))
+    return {r1, r2} == {1, 2}
+
+
+def get_paired_files(files_list) -> list:
+    """frender.py:696-716."""
+    pairs = []
+    for path in [p for p in files_list if re.search("_R1_", str(p), re.IGNORECASE)]:
+        mates = [i for i, f in enumerate(files_list) if is_read_mate(str(path), str(f))]
+        if len(mates) > 1:
+            raise SystemExit(f"Found more than one potential read 2 file for {path}")
+        if not mates:
+            raise SystemExit(f"Couldn't find a read 2 file for {path}")
+        pairs.append((path, files_list[mates[0]]))
+    return pairs
+
+
+def read_text(path) -> bytes:
+    """The decoded bytes as the reference's text-mode reader sees them (frender.py:776): strict
+    UTF-8 (UnicodeDecodeError otherwise) and universal newlines folded to '\\n'."""
+    with gzip.open(path, "rb") as g:
+        data = g.read()
+    if np.frombuffer(data, dtype=np.uint8).max(initial=0) >= 0x80:
+        data.decode("utf-8")  # raises like gzip.open(..., "rt")
+    if b"\r" in data:
+        data = data.replace(b"\r\n", b"\n").replace(b"\r", b"\n")
+    return data
+
+
+def _line_at(data: bytes, start: int) -> bytes:
+    e = data.find(b"\n", start)
+    return data[start:] if e < 0 else data[start:e]
+
+
+def frender_demux(args, dev=None) -> None:
+    """frender.py:733-814 with the per-record loop on the GPU."""
+    index_hop = not args.no_index_hop
+    ambiguous = not args.no_ambiguous
+    undeter = not args.no_undeter
+    samples = not args.no_samples
+    level = getattr(args, "gz_level", None) or 9  # gzip.open's default, as the reference writes
+    infix = args.o
+    undeter_name = f"Undetermined{'-ambiguous' if ambiguous else ''}{'-index-hop' if index_hop else ''}"
+
+    result_file = Path(args.r)
+    if not Path.is_file(result_file):
+        raise SystemExit(f"File {result_file} not found")
+    results = parse_results_file(result_file)
+    ids = sorted({sid for _, sid in results.values()} - {""})
+    if (not ids) & samples:
+        print("Warning: no demuxable sample ids found in the supplied frender result file!")
+
+    os.mkdir(args.d)
+    writers = []  # destination id -> writer pair
+
+    def new_writers(name):
+        writers.append(open_files(name, args.d, infix, level))
+        return len(writers) - 1
+
+    sample_dest = {sid: new_writers(sid) for sid in ids} if samples else None
+    undeter_dest = new_writers(undeter_name) if undeter else None
+    hop_dest = new_writers("Index-hop") if index_hop else undeter_dest
+    amb_dest = new_writers("Ambiguous") if ambiguous else undeter_dest
+
+    def route_of(row) -> int:  # frender.py:779-810
+        rtype, sid = row
+        if rtype == "demuxable" and sample_dest:
+            return sample_dest.get(sid, _lib.FR_DMX_MISSING)  # KeyError -> "Couldn't find barcode"
+        if rtype == "index_hop" and hop_dest is not None:
+            return hop_dest
+        if rtype == "ambiguous" and amb_dest is not None:
+            return amb_dest
+        if rtype == "undetermined" and undeter_dest is not None:
+            return undeter_dest
+        return _lib.FR_DMX_BADTYPE
+
+    codes = list(results.keys())
+    keys, fast = _lib.pack_fast(codes)
+    vals = np.array([route_of(results[c]) for c in codes], dtype=np.int32)
+
+    if len(args.files) == 1:
+        file = Path(args.files[0])
+        if Path.is_dir(file):
+            spec = {"dir": file}
+        elif Path.is_file(file):
+            spec = {"file": file}
+        else:
+            raise SystemExit("Specified directory or file path doesn't seem to exist!")
+    else:
+        spec = {"file": [Path(f) for f in args.files]}
+    pairs = get_paired_files(parse_files(spec, just_r1=False))
+
+    dmx = dev or _lib.Demux(int(os.environ.get("LOCAL_RANK", "0")))
+    pool = ThreadPoolExecutor(max_workers=max(2, min(32, len(writers) * 2)))
+    try:
+        dmx.set_table(keys[fast], vals[fast])
+        for read1_file, read2_file in pairs:
+            print(f"Demultiplexing {read1_file.name}...")
+            f1 = pool.submit(read_text, read1_file)
+            d2 = read_text(read2_file)
+            d1 = f1.result()
+            n1 = dmx.load(0, d1)
+            n2 = dmx.load(1, d2)
+            n_pairs = min(n1, n2)  # zip() stops at the shorter file
+            ex = dmx.exotic(n_pairs)
+            if ex.size:  # codes outside the fast alphabet: resolve by string
+                starts, _ = dmx.records(1, ex)
+                dest = []
+                for s in starts.tolist():
+                    code = _line_at(d2, s).split(b":")[-1].decode("utf-8")
+                    row = results.get(code)
+                    dest.append(_lib.FR_DMX_MISSING if row is None else route_of(row))
+                dmx.patch(ex, np.array(dest, dtype=np.int32))
+            first, val, b1, b2 = dmx.route(len(writers), n_pairs)
+            if first >= 0:
+                s, _ = dmx.records(1, [first])
+                code = _line_at(d2, int(s[0])).split(b":")[-1].decode("utf-8")
+                if val == _lib.FR_DMX_MISSING:
+                    raise SystemExit(f"Couldn't find barcode {code} in supplied frender result file!")
+                raise SystemExit("Unrecognized read type found in supplied frender result file!")
+            o1 = dmx.fetch(0, int(b1.sum()))
+            o2 = dmx.fetch(1, int(b2.sum()))
+            c1 = np.concatenate([[0], np.cumsum(b1)]).astype(np.int64)
+            c2 = np.concatenate([[0], np.cumsum(b2)]).astype(np.int64)
+            jobs = []
+            for k, w in enumerate(writers):
+                if b1[k]:
+                    jobs.append(pool.submit(w["R1"].write, memoryview(o1)[c1[k]:c1[k + 1]]))
+                if b2[k]:
+                    jobs.append(pool.submit(w["R2"].write, memoryview(o2)[c2[k]:c2[k + 1]]))
+            for j in jobs:
+                j.result()
+    finally:
+        pool.shutdown(wait=True)
+        for w in writers:
+            for f in w.values():
+                f.close()
+        if dev is None:
+            dmx.close()

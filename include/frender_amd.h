@@ -153,6 +153,39 @@ int fr_copy_to_device(fr_ctx* ctx, void* dev_dst, const void* src, uint64_t byte
 int fr_synth_device(fr_ctx* ctx, uint8_t* dev_out, uint64_t r0, uint64_t n, int R, uint64_t seed,
                     const char* idx1_ascii, const char* idx2_ascii, int S, int L1, int L2);
 
+/* ---- demux: replaces the hot loop of frender_demux (frender.py:776-810)
+ * One file pair at a time.  The caller hands over decoded text with universal newlines already
+ * normalised to '\n' (the reference reads in text mode, :776).  Records are groups of 4 lines
+ * (grouper, :719-723); the R2 record's code is the text after the last ':' of its first line
+ * (:778).  Destinations are small non-negative ids chosen by the caller (one per writer pair). */
+#define FR_DMX_MISSING (-1) /* code not in the results: SystemExit "Couldn't find barcode ..." (:807-810) */
+#define FR_DMX_BADTYPE (-2) /* read type with no writers: SystemExit "Unrecognized read type ..." (:803-806) */
+#define FR_DMX_EXOTIC (-3)  /* code outside the fast alphabet / > 21 chars: the host resolves it */
+
+typedef struct fr_dmx fr_dmx;
+fr_dmx* fr_dmx_create(int device);
+void fr_dmx_destroy(fr_dmx* d);
+const char* fr_dmx_last_error(const fr_dmx* d);
+/* results table: fast-alphabet codes (3-bit packed like fr_get_unique keys) -> destination or
+ * FR_DMX_BADTYPE; codes absent from the table resolve to FR_DMX_MISSING */
+int fr_dmx_set_table(fr_dmx* d, const uint64_t* keys, const int32_t* vals, uint64_t n);
+/* mate 0 = R1, 1 = R2 (R2 also resolves every record's destination); returns the record count */
+int fr_dmx_load(fr_dmx* d, int mate, const uint8_t* data, uint64_t len, uint64_t* n_records);
+/* byte span [start, end) of the given records of a mate (host error messages, exotic codes) */
+int fr_dmx_records(fr_dmx* d, int mate, const uint64_t* recs, uint64_t n, uint64_t* starts, uint64_t* ends);
+/* R2 records < n_pairs whose destination is FR_DMX_EXOTIC (first cap written; *n = total) */
+int fr_dmx_exotic(fr_dmx* d, uint64_t n_pairs, uint64_t* recs, uint64_t cap, uint64_t* n);
+/* set the destinations of the given R2 records (the host's resolution of exotic codes) */
+int fr_dmx_patch(fr_dmx* d, const uint64_t* recs, const int32_t* dest, uint64_t n);
+/* route the first n_pairs record pairs: if some pair has a negative destination, *first_error is
+ * the first such pair and *error_val its value (nothing routed); otherwise both mates' records
+ * are gathered destination-major (record order kept within a destination) and the byte count
+ * of every destination is returned per mate */
+int fr_dmx_route(fr_dmx* d, int n_dest, uint64_t n_pairs, int64_t* first_error, int32_t* error_val,
+                 uint64_t* bytes_r1, uint64_t* bytes_r2);
+/* the routed bytes of a mate (destination-major) */
+int fr_dmx_fetch(fr_dmx* d, int mate, uint8_t* out, uint64_t len);
+
 #ifdef __cplusplus
 }
 #endif

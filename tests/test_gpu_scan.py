@@ -316,3 +316,64 @@ def test_merge_unique_device(lib):
         ref.close()
         for c in ranks:
             c.close()
+
+
+# ---------------------------------------------------------------------------------------
+# demux (row f-1): the GPU path against the reference's own outputs
+# ---------------------------------------------------------------------------------------
+from demux_harness import case_names as demux_case_names  # noqa: E402
+from demux_harness import run_case as run_demux_case  # noqa: E402
+
+
+@pytest.mark.parametrize("name", demux_case_names())
+def test_demux_golden_on_gpu(name):
+    from frender_amd.demux import frender_demux
+    diffs = run_demux_case(name, frender_demux)
+    assert not diffs, "\n".join(diffs)
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_demux_random_vs_oracle(seed, tmp_path):
+    """Random paired inputs with mixed codes, CRLF/CR, long headers and a short R2 against
+    the demux oracle (content of every writer)."""
+    import argparse
+    import gzip
+    from frender_amd.demux import frender_demux
+    from oracle import demux_oracle
+    rng = random.Random(seed)
+    codes = ["AAAA+CCCC", "GGGG+TTTT", "AAAA+TTTT", "ACGT+ACGT", "NNNN+CCCC", "acgt+TTTT", "ACG+GT"]
+    kinds = {"AAAA+CCCC": ("demuxable", "S1"), "GGGG+TTTT": ("demuxable", "S2"), "AAAA+TTTT": ("index_hop", ""),
+             "ACGT+ACGT": ("undetermined", ""), "NNNN+CCCC": ("ambiguous", ""), "acgt+TTTT": ("demuxable", "S1"),
+             "ACG+GT": ("undetermined", "")}
+    inp = tmp_path / "in"
+    inp.mkdir()
+    r1, r2 = [], []
+    for i in range(rng.randint(3000, 6000)):
+        c = rng.choice(codes)
+        nl = rng.choice(["\n"] * 8 + ["\r\n", "\r"])
+        pad = "x" * (rng.randint(0, 900) if rng.random() < 0.02 else rng.randint(0, 20))
+        seq = "".join(rng.choice("ACGT") for _ in range(rng.randint(0, 60)))
+        r1.append(f"@r{i}:{pad}:1:FC 1:N:0:{c}{nl}{seq}{nl}+{nl}{'F' * len(seq)}{nl}")
+        r2.append(f"@r{i}:{pad}:1:FC 2:N:0:{c}{nl}{seq[::-1]}{nl}+{nl}{'F' * len(seq)}{nl}")
+    t2 = "".join(r2)[:-rng.randint(1, 40)]
+    with gzip.open(inp / "x_R1_001.fastq.gz", "wb") as f:
+        f.write("".join(r1).encode())
+    with gzip.open(inp / "x_R2_001.fastq.gz", "wb") as f:
+        f.write(t2.encode())
+    with open(inp / "results.csv", "w") as f:
+        f.write("idx1,idx2,reads,matched_idx1,matched_idx2,read_type,sample_name,demux_ok\r\n")
+        for c, (t, s) in kinds.items():
+            a, b = c.split("+")[0:2]
+            f.write(f"{a},{b},1,,,{t},{s},True\r\n")
+    files = [str(inp / "x_R1_001.fastq.gz"), str(inp / "x_R2_001.fastq.gz")]
+
+    def ns(d):
+        return argparse.Namespace(r=str(inp / "results.csv"), d=str(d), o=None, no_index_hop=False,
+                                  no_ambiguous=False, no_undeter=False, no_samples=False, files=files)
+
+    want = demux_oracle.demux(ns(tmp_path / "o_ref"))
+    frender_demux(ns(tmp_path / "o_gpu"))
+    for p, data in want.items():
+        q = p.replace("o_ref", "o_gpu")
+        with gzip.open(q, "rb") as g:
+            assert g.read() == data, q

@@ -84,6 +84,7 @@ _SIGS = {
     "fr_dmx_last_error": (C.c_char_p, [P]),
     "fr_dmx_set_table": (C.c_int, [P, P, P, C.c_uint64]),
     "fr_dmx_load": (C.c_int, [P, C.c_int, P, C.c_uint64, u64p]),
+    "fr_dmx_load_device": (C.c_int, [P, C.c_int, P, C.c_uint64, u64p]),
     "fr_dmx_records": (C.c_int, [P, C.c_int, P, C.c_uint64, P, P]),
     "fr_dmx_exotic": (C.c_int, [P, C.c_uint64, P, C.c_uint64, u64p]),
     "fr_dmx_patch": (C.c_int, [P, P, P, C.c_uint64]),
@@ -175,6 +176,11 @@ class Demux:
         a = np.frombuffer(data, dtype=np.uint8)
         n = C.c_uint64()
         self._ck(lib.fr_dmx_load(self.h, mate, _ptr(a), a.size, C.byref(n)), "fr_dmx_load")
+        return n.value
+
+    def load_device(self, mate: int, dev_ptr: int, nbytes: int) -> int:
+        n = C.c_uint64()
+        self._ck(lib.fr_dmx_load_device(self.h, mate, P(dev_ptr), nbytes, C.byref(n)), "fr_dmx_load_device")
         return n.value
 
     def records(self, mate: int, recs) -> tuple:

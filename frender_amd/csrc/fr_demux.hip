@@ -113,16 +113,39 @@ __global__ __launch_bounds__(DWG) void dmx_count(const u8* buf, u64 len, u32 nti
     }
 }
 
-// the code of the header line starting at p: text after the line's last ':' up to its '\n'
-// (frender.py:778) -> destination; bytes come from the staged tile when inside it
-__device__ int32_t header_dest(const u8* buf, u64 len, u64 p, const u8* lds, u64 lds0, u32 lds_n,
-                               const DmxTable& tab) {
-    auto rd = [&](u64 q) -> u32 { return (q >= lds0 && q - lds0 < lds_n) ? (u32)lds[q - lds0] : (u32)buf[q]; };
+__device__ __forceinline__ u32 eq_mask4(u32 w, u32 rep) {  // exact byte equality -> bits 0..3
+    const u32 t = w ^ rep;
+    const u32 z = ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;
+    return __builtin_amdgcn_udot4(z >> 7, 0x08040201u, 0u, false);
+}
+
+// fast key of the code bytes [s, s+n) in LDS: v_perm lookups 4 bytes per step (A1 C2 G3 T4 N5 +6);
+// false when a byte is outside the fast alphabet
+__device__ __forceinline__ bool encode_fast(const u8* lds, u32 s, u32 n, u64& key) {
+    u64 kk = 0;
+    u32 bad = 0;
+    for (u32 k = 0; 4 * k < n; ++k) {
+        const u32 p = s + 4 * k;
+        const u32 lo = *(const u32*)(lds + (p & ~3u)), hi = *(const u32*)(lds + (p & ~3u) + 4);
+        const u32 a = __builtin_amdgcn_alignbyte(hi, lo, p & 3u);
+        const u32 idx = (a >> 1) & 0x07070707u;
+        const u32 expect = __builtin_amdgcn_perm(0x4E002B00u, 0x47544341u, idx);
+        const u32 sym = __builtin_amdgcn_perm(0x05000600u, 0x03040201u, idx);
+        const u32 left = n - 4 * k;
+        const u32 vm = left >= 4 ? 0xFFFFFFFFu : (0xFFFFFFFFu >> (32 - 8 * left));
+        bad |= (expect ^ a) & vm;
+        const u32 sv = sym & vm;
+        kk |= (u64)((sv & 0x7u) | ((sv >> 5) & 0x38u) | ((sv >> 10) & 0x1C0u) | ((sv >> 15) & 0xE00u)) << (12 * k);
+    }
+    key = kk;
+    return bad == 0;
+}
+
+// slow path: the header line runs past the staged bytes -> byte loop over global memory
+__device__ __noinline__ int32_t header_dest_global(const u8* buf, u64 len, u64 p, const DmxTable& tab) {
     u64 e = p, lastc = ~0ull;
-    while (e < len) {
-        const u32 c = rd(e);
-        if (c == '\n') break;
-        if (c == ':') lastc = e;
+    while (e < len && buf[e] != '\n') {
+        if (buf[e] == ':') lastc = e;
         ++e;
     }
     const u64 s = lastc == ~0ull ? p : lastc + 1;
@@ -130,26 +153,70 @@ __device__ int32_t header_dest(const u8* buf, u64 len, u64 p, const u8* lds, u64
     if (n == 0 || n > (u64)DMAXSYM) return FR_DMX_EXOTIC;
     u64 key = 0;
     for (u64 i = 0; i < n; ++i) {
-        const u32 sy = sym_byte(rd(s + i));
+        const u32 sy = sym_byte(buf[s + i]);
         if (!sy) return FR_DMX_EXOTIC;
         key |= (u64)sy << (3 * i);
     }
     return table_get(tab, key);
 }
 
+// the code of the header line starting at tile position q: the text after the line's last ':'
+// up to its '\n' (frender.py:778) -> destination.  Word-at-a-time over the staged tile (LDS,
+// zero-padded past lds_n); '\n' and ':' found with exact SWAR byte masks.
+__device__ __forceinline__ int32_t header_dest(const u8* buf, u64 len, u64 tile0, u32 q, const u8* lds, u32 lds_n,
+                                               const DmxTable& tab) {
+    int lastc = -1, e = -1;
+    u32 w = q & ~3u;
+    u32 keep = (0xFu << (q & 3u)) & 0xFu;
+    for (; w < lds_n; w += 4) {
+        const u32 v = *(const u32*)(lds + w);
+        u32 nl = eq_mask4(v, 0x0A0A0A0Au) & keep, col = eq_mask4(v, 0x3A3A3A3Au) & keep;
+        keep = 0xFu;
+        if (w + 4 > lds_n) {
+            const u32 vm = (1u << (lds_n - w)) - 1u;
+            nl &= vm;
+            col &= vm;
+        }
+        if (nl) {
+            const u32 b = __builtin_ctz(nl);
+            col &= (1u << b) - 1u;
+            if (col) lastc = (int)(w + 31u - __builtin_clz(col));
+            e = (int)(w + b);
+            break;
+        }
+        if (col) lastc = (int)(w + 31u - __builtin_clz(col));
+    }
+    if (e < 0) {
+        if (tile0 + lds_n < len) return header_dest_global(buf, len, tile0 + q, tab);
+        e = (int)lds_n;  // the line ends with the data
+    }
+    const u32 s = lastc >= 0 ? (u32)lastc + 1u : q;
+    const u32 n = (u32)e - s;
+    if (n == 0 || n > (u32)DMAXSYM) return FR_DMX_EXOTIC;
+    u64 key;
+    if (!encode_fast(lds, s, n, key)) return FR_DMX_EXOTIC;
+    return table_get(tab, key);
+}
+
 __global__ __launch_bounds__(DWG) void dmx_index(const u8* buf, u64 len, u32 ntiles, const u64* tile_base,
                                                  u64* rec_start, int32_t* rec_dest, DmxTable tab) {
-    __shared__ u8 lds[DT + DHALO];
+    __shared__ __attribute__((aligned(16))) u8 lds[DT + DHALO + 32];  // +32: zero pad for word reads
     __shared__ u32 ws[DWG / 64];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     for (u32 t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const u64 tile0 = (u64)t * DT;
         const u32 lds_n = (u32)min((u64)(DT + DHALO), len - tile0);
         if (rec_dest) {
-            for (u32 i = tid * 16; i < lds_n; i += DWG * 16) {
-                if (i + 16 <= lds_n) *(uint4*)(lds + i) = *(const uint4*)(buf + tile0 + i);
-                else
-                    for (u32 j = i; j < lds_n; ++j) lds[j] = buf[tile0 + j];
+            for (u32 i = tid * 16; i < lds_n + 32; i += DWG * 16) {
+                uint4 v = make_uint4(0u, 0u, 0u, 0u);
+                if (i + 16 <= lds_n) {
+                    v = *(const uint4*)(buf + tile0 + i);
+                } else if (i < lds_n) {
+                    u32 b[4] = {0u, 0u, 0u, 0u};
+                    for (u32 j = i; j < lds_n; ++j) b[(j - i) >> 2] |= (u32)buf[tile0 + j] << (8 * ((j - i) & 3));
+                    v = make_uint4(b[0], b[1], b[2], b[3]);
+                }
+                if (i < DT + DHALO + 32) *(uint4*)(lds + i) = v;
             }
         }
         const u64 m = lane_nl(buf, len, tile0, tid);
@@ -173,12 +240,12 @@ __global__ __launch_bounds__(DWG) void dmx_index(const u8* buf, u64 len, u32 nti
             const u64 p = tile0 + (u64)tid * DSEG + j + 1;
             if ((L & 3ull) == 0 && p < len) {
                 rec_start[L >> 2] = p;
-                if (rec_dest) rec_dest[L >> 2] = header_dest(buf, len, p, lds, tile0, lds_n, tab);
+                if (rec_dest) rec_dest[L >> 2] = header_dest(buf, len, tile0, (u32)(p - tile0), lds, lds_n, tab);
             }
         }
         if (t == 0 && tid == 0 && len > 0) {  // the first line of the file
             rec_start[0] = 0;
-            if (rec_dest) rec_dest[0] = header_dest(buf, len, 0, lds, tile0, lds_n, tab);
+            if (rec_dest) rec_dest[0] = header_dest(buf, len, tile0, 0u, lds, lds_n, tab);
         }
         __syncthreads();
     }
@@ -224,14 +291,29 @@ __global__ void dmx_dest_offsets(const u32* first, int n_dest, u64 n, const u64*
     off2[d] = e < n_dest ? o2[first[e]] : tot2;
 }
 
-// one wave per output record: coalesced byte copies
+// one wave per output record: a byte head up to the destination's 4-byte alignment, then
+// aligned dword stores, each assembled from the two source dwords it straddles
+// (v_alignbyte_b32), then a byte tail.  Source reads may run up to 3 bytes past the record
+// inside the same aligned dword (allocations are 256-B granular).
 __global__ void dmx_copy(const u32* perm, u64 n, const u64* rs, const u8* src, const u64* off, u8* dst) {
     const int lane = threadIdx.x & 63;
     const u64 waves = (u64)gridDim.x * (blockDim.x / 64);
     for (u64 j = blockIdx.x * (u64)(blockDim.x / 64) + (threadIdx.x >> 6); j < n; j += waves) {
         const u32 i = perm[j];
-        const u64 s = rs[i], e = rs[i + 1], o = off[j];
-        for (u64 q = s + lane; q < e; q += 64) dst[o + (q - s)] = src[q];
+        const u64 s = rs[i], len = rs[i + 1] - s, o = off[j];
+        const u64 head = min((u64)((4u - (u32)(o & 3u)) & 3u), len);
+        if ((u64)lane < head) dst[o + lane] = src[s + lane];
+        const u64 s1 = s + head, o1 = o + head, words = (len - head) >> 2;
+        const u32 sh = (u32)(s1 & 3u);
+        const u32* sw = (const u32*)(src + (s1 & ~3ull));
+        u32* dw = (u32*)(dst + o1);
+        for (u64 k = lane; k < words; k += 64) {
+            const u32 lo = sw[k];
+            const u32 hi = sh ? sw[k + 1] : 0u;
+            dw[k] = sh ? __builtin_amdgcn_alignbyte(hi, lo, sh) : lo;
+        }
+        const u64 t0 = head + (words << 2);
+        if (t0 + lane < len) dst[o + t0 + lane] = src[s + t0 + lane];
     }
 }
 
@@ -255,13 +337,25 @@ struct fr_dmx {
     // per mate: data, record starts (+ sentinel), destinations (R2)
     u8* data[2] = {nullptr, nullptr};
     u64 cap[2] = {0, 0};
+    const u8* src[2] = {nullptr, nullptr};  // the bytes indexed: data[m] or a caller's device buffer
     u64 len[2] = {0, 0};
     u64* rs[2] = {nullptr, nullptr};
     u64 rs_cap[2] = {0, 0};
     u64 nrec[2] = {0, 0};
     int32_t* dest = nullptr;
     u64 dest_cap = 0;
-    // route outputs
+    // route temporaries (grow-only) and outputs
+    u32 *k_in = nullptr, *k_out = nullptr, *i_in = nullptr, *perm = nullptr, *first_pos = nullptr;
+    u64 *l1 = nullptr, *l2 = nullptr, *o1 = nullptr, *o2 = nullptr, *off1 = nullptr, *off2 = nullptr;
+    u64 c_k_in = 0, c_k_out = 0, c_i_in = 0, c_perm = 0, c_first = 0, c_l1 = 0, c_l2 = 0, c_o1 = 0, c_o2 = 0,
+        c_off1 = 0, c_off2 = 0;
+    void* tmp = nullptr;
+    u64 c_tmp = 0;
+    u32* cnt = nullptr;
+    u64* base = nullptr;
+    u64 c_cnt = 0, c_base = 0;
+    unsigned long long* fe = nullptr;
+    u64 c_fe = 0;
     u8* out[2] = {nullptr, nullptr};
     u64 out_cap[2] = {0, 0};
     u64 out_len[2] = {0, 0};
@@ -302,7 +396,9 @@ void fr_dmx_destroy(fr_dmx* d) {
     if (!d) return;
     (void)hipSetDevice(d->device);
     if (d->stream) (void)hipStreamSynchronize(d->stream);
-    void* p[] = {d->tkeys, d->tvals, d->data[0], d->data[1], d->rs[0], d->rs[1], d->dest, d->out[0], d->out[1]};
+    void* p[] = {d->tkeys, d->tvals, d->data[0], d->data[1], d->rs[0], d->rs[1], d->dest, d->out[0], d->out[1],
+                 d->k_in, d->k_out, d->i_in, d->perm, d->first_pos, d->l1, d->l2, d->o1, d->o2, d->off1, d->off2,
+                 d->tmp, d->cnt, d->base, d->fe};
     for (void* x : p)
         if (x) (void)hipFree(x);
     if (d->stream) (void)hipStreamDestroy(d->stream);
@@ -340,57 +436,59 @@ int fr_dmx_set_table(fr_dmx* d, const uint64_t* keys, const int32_t* vals, uint6
     return FR_OK;
 }
 
+static int dmx_index_mate(fr_dmx* d, int mate, const u8* buf, u64 len, u64* n_records) {
+    d->src[mate] = buf;
+    d->len[mate] = len;
+    const u32 ntiles = (u32)((len + DT - 1) / DT);
+    DK(ensure(&d->cnt, d->c_cnt, (u64)ntiles + 1));
+    DK(ensure(&d->base, d->c_base, (u64)ntiles + 1));
+    u64 nl = 0;
+    if (ntiles) {
+        hipLaunchKernelGGL(dmx_count, dim3(std::min<u32>(ntiles, 8192)), dim3(DWG), 0, d->stream, buf, len, ntiles,
+                           d->cnt);
+        DK(hipGetLastError());
+        size_t tb = 0;
+        DK(rocprim::exclusive_scan(nullptr, tb, d->cnt, d->base, (u64)0, (size_t)ntiles + 1, rocprim::plus<u64>(),
+                                   d->stream));
+        DK(ensure((u8**)&d->tmp, d->c_tmp, tb + 1));
+        DK(hipMemsetAsync(d->cnt + ntiles, 0, 4, d->stream));
+        DK(rocprim::exclusive_scan(d->tmp, tb, d->cnt, d->base, (u64)0, (size_t)ntiles + 1, rocprim::plus<u64>(),
+                                   d->stream));
+        DK(hipMemcpyAsync(&nl, d->base + ntiles, 8, hipMemcpyDeviceToHost, d->stream));  // total '\n'
+    }
+    u8 lastb = '\n';
+    if (len) DK(hipMemcpyAsync(&lastb, buf + len - 1, 1, hipMemcpyDeviceToHost, d->stream));
+    DK(hipStreamSynchronize(d->stream));
+    const u64 lines = nl + ((len && lastb != '\n') ? 1 : 0);  // a last line without '\n'
+    const u64 nrec = (lines + 3) / 4;
+    DK(ensure(&d->rs[mate], d->rs_cap[mate], nrec + 1));
+    if (mate == 1) DK(ensure(&d->dest, d->dest_cap, nrec + 1));
+    d->nrec[mate] = nrec;
+    *n_records = nrec;
+    DK(hipMemcpyAsync(d->rs[mate] + nrec, &d->len[mate], 8, hipMemcpyHostToDevice, d->stream));  // sentinel
+    if (ntiles) {
+        DmxTable tab{d->tkeys, d->tvals, d->tmask};
+        hipLaunchKernelGGL(dmx_index, dim3(std::min<u32>(ntiles, 4096)), dim3(DWG), 0, d->stream, buf, len, ntiles,
+                           d->base, d->rs[mate], mate == 1 ? d->dest : nullptr, tab);
+        DK(hipGetLastError());
+    }
+    DK(hipStreamSynchronize(d->stream));
+    return FR_OK;
+}
+
 int fr_dmx_load(fr_dmx* d, int mate, const uint8_t* data, uint64_t len, uint64_t* n_records) {
     if (mate < 0 || mate > 1) return d->err = "mate must be 0 (R1) or 1 (R2)", FR_ERR_INVALID;
     DK(hipSetDevice(d->device));
     DK(ensure(&d->data[mate], d->cap[mate], len + 16));
     if (len) DK(hipMemcpyAsync(d->data[mate], data, len, hipMemcpyHostToDevice, d->stream));
-    d->len[mate] = len;
-    const u32 ntiles = (u32)((len + DT - 1) / DT);
-    u32* cnt = nullptr;
-    u64* base = nullptr;
-    DK(hipMalloc(&cnt, std::max<u64>(ntiles, 1) * 4));
-    DK(hipMalloc(&base, (u64)(ntiles + 1) * 8));
-    if (ntiles) {
-        hipLaunchKernelGGL(dmx_count, dim3(std::min<u32>(ntiles, 8192)), dim3(DWG), 0, d->stream, d->data[mate], len,
-                           ntiles, cnt);
-        DK(hipGetLastError());
-        size_t tb = 0;
-        DK(rocprim::exclusive_scan(nullptr, tb, cnt, base, (u64)0, (size_t)ntiles + 0, rocprim::plus<u64>(), d->stream));
-        void* tmp = nullptr;
-        DK(hipMalloc(&tmp, std::max<size_t>(tb, 1)));
-        DK(rocprim::exclusive_scan(tmp, tb, cnt, base, (u64)0, (size_t)ntiles, rocprim::plus<u64>(), d->stream));
-        DK(hipStreamSynchronize(d->stream));
-        DK(hipFree(tmp));
-    }
-    // lines = '\n' count + a last line without one
-    u64 nl = 0;
-    if (ntiles) {
-        u64 last_base = 0;
-        u32 last_cnt = 0;
-        DK(hipMemcpy(&last_base, base + ntiles - 1, 8, hipMemcpyDeviceToHost));
-        DK(hipMemcpy(&last_cnt, cnt + ntiles - 1, 4, hipMemcpyDeviceToHost));
-        nl = last_base + last_cnt;
-    }
-    u8 lastb = '\n';
-    if (len) DK(hipMemcpy(&lastb, d->data[mate] + len - 1, 1, hipMemcpyDeviceToHost));
-    const u64 lines = nl + ((len && lastb != '\n') ? 1 : 0);
-    const u64 nrec = (lines + 3) / 4;
-    DK(ensure(&d->rs[mate], d->rs_cap[mate], nrec + 1));
-    if (mate == 1) DK(ensure(&d->dest, d->dest_cap, nrec + 1));
-    DK(hipMemcpyAsync(d->rs[mate] + nrec, &len, 8, hipMemcpyHostToDevice, d->stream));  // sentinel
-    if (ntiles) {
-        DmxTable tab{d->tkeys, d->tvals, d->tmask};
-        hipLaunchKernelGGL(dmx_index, dim3(std::min<u32>(ntiles, 4096)), dim3(DWG), 0, d->stream, d->data[mate], len,
-                           ntiles, base, d->rs[mate], mate == 1 ? d->dest : nullptr, tab);
-        DK(hipGetLastError());
-    }
-    DK(hipStreamSynchronize(d->stream));
-    DK(hipFree(cnt));
-    DK(hipFree(base));
-    d->nrec[mate] = nrec;
-    *n_records = nrec;
-    return FR_OK;
+    return dmx_index_mate(d, mate, d->data[mate], len, n_records);
+}
+
+int fr_dmx_load_device(fr_dmx* d, int mate, const uint8_t* dev_data, uint64_t len, uint64_t* n_records) {
+    if (mate < 0 || mate > 1) return d->err = "mate must be 0 (R1) or 1 (R2)", FR_ERR_INVALID;
+    if (((uintptr_t)dev_data & 15u) != 0) return d->err = "device data must be 16-byte aligned", FR_ERR_INVALID;
+    DK(hipSetDevice(d->device));
+    return dmx_index_mate(d, mate, dev_data, len, n_records);
 }
 
 int fr_dmx_records(fr_dmx* d, int mate, const uint64_t* recs, uint64_t n, uint64_t* starts, uint64_t* ends) {
@@ -441,15 +539,14 @@ int fr_dmx_route(fr_dmx* d, int n_dest, uint64_t n_pairs, int64_t* first_error, 
     for (int k = 0; k < n_dest; ++k) bytes_r1[k] = bytes_r2[k] = 0;
     d->out_len[0] = d->out_len[1] = 0;
     if (!P) return FR_OK;
-    unsigned long long* fe = nullptr;
-    DK(hipMalloc(&fe, 8));
+    DK(ensure(&d->fe, d->c_fe, 1));
+    unsigned long long* fe = d->fe;
     DK(hipMemsetAsync(fe, 0xFF, 8, d->stream));
     hipLaunchKernelGGL(dmx_first_error, dim3(grid_for(P)), dim3(256), 0, d->stream, d->dest, P, fe);
     DK(hipGetLastError());
     u64 first = 0;
     DK(hipMemcpyAsync(&first, fe, 8, hipMemcpyDeviceToHost, d->stream));
     DK(hipStreamSynchronize(d->stream));
-    DK(hipFree(fe));
     if (first != ~0ull) {
         int32_t v = 0;
         DK(hipMemcpy(&v, d->dest + first, 4, hipMemcpyDeviceToHost));
@@ -457,22 +554,20 @@ int fr_dmx_route(fr_dmx* d, int n_dest, uint64_t n_pairs, int64_t* first_error, 
         *error_val = v;
         return FR_OK;
     }
-    // stable partition by destination
-    u32 *k_in = nullptr, *k_out = nullptr, *i_in = nullptr, *perm = nullptr;
-    u64 *l1 = nullptr, *l2 = nullptr, *o1 = nullptr, *o2 = nullptr;
-    u32* first_pos = nullptr;
-    u64 *off1 = nullptr, *off2 = nullptr;
-    DK(hipMalloc(&k_in, P * 4));
-    DK(hipMalloc(&k_out, P * 4));
-    DK(hipMalloc(&i_in, P * 4));
-    DK(hipMalloc(&perm, P * 4));
-    DK(hipMalloc(&l1, P * 8));
-    DK(hipMalloc(&l2, P * 8));
-    DK(hipMalloc(&o1, P * 8));
-    DK(hipMalloc(&o2, P * 8));
-    DK(hipMalloc(&first_pos, (u64)std::max(n_dest, 1) * 4));
-    DK(hipMalloc(&off1, (u64)(n_dest + 1) * 8));
-    DK(hipMalloc(&off2, (u64)(n_dest + 1) * 8));
+    // stable partition by destination (temporaries cached in the context, grow-only)
+    DK(ensure(&d->k_in, d->c_k_in, P));
+    DK(ensure(&d->k_out, d->c_k_out, P));
+    DK(ensure(&d->i_in, d->c_i_in, P));
+    DK(ensure(&d->perm, d->c_perm, P));
+    DK(ensure(&d->l1, d->c_l1, P));
+    DK(ensure(&d->l2, d->c_l2, P));
+    DK(ensure(&d->o1, d->c_o1, P));
+    DK(ensure(&d->o2, d->c_o2, P));
+    DK(ensure(&d->first_pos, d->c_first, (u64)std::max(n_dest, 1)));
+    DK(ensure(&d->off1, d->c_off1, (u64)n_dest + 1));
+    DK(ensure(&d->off2, d->c_off2, (u64)n_dest + 1));
+    u32 *k_in = d->k_in, *k_out = d->k_out, *i_in = d->i_in, *perm = d->perm, *first_pos = d->first_pos;
+    u64 *l1 = d->l1, *l2 = d->l2, *o1 = d->o1, *o2 = d->o2, *off1 = d->off1, *off2 = d->off2;
     DK(hipMemsetAsync(first_pos, 0xFF, (u64)std::max(n_dest, 1) * 4, d->stream));
     hipLaunchKernelGGL(dmx_keys, dim3(grid_for(P)), dim3(256), 0, d->stream, d->dest, P, k_in, i_in);
     DK(hipGetLastError());
@@ -480,10 +575,10 @@ int fr_dmx_route(fr_dmx* d, int n_dest, uint64_t n_pairs, int64_t* first_error, 
     while ((1 << bits) < n_dest) ++bits;
     size_t tb = 0;
     DK(rocprim::radix_sort_pairs(nullptr, tb, k_in, k_out, i_in, perm, (size_t)P, 0, (unsigned)bits, d->stream));
-    void* tmp = nullptr;
     size_t tb2 = 0;
     DK(rocprim::exclusive_scan(nullptr, tb2, l1, o1, (u64)0, (size_t)P, rocprim::plus<u64>(), d->stream));
-    DK(hipMalloc(&tmp, std::max<size_t>(std::max(tb, tb2), 1)));
+    DK(ensure((u8**)&d->tmp, d->c_tmp, std::max<size_t>(std::max(tb, tb2), 1)));
+    void* tmp = d->tmp;
     DK(rocprim::radix_sort_pairs(tmp, tb, k_in, k_out, i_in, perm, (size_t)P, 0, (unsigned)bits, d->stream));
     hipLaunchKernelGGL(dmx_lengths, dim3(grid_for(P)), dim3(256), 0, d->stream, perm, P, d->rs[0], d->rs[1], l1, l2);
     DK(hipGetLastError());
@@ -506,13 +601,11 @@ int fr_dmx_route(fr_dmx* d, int n_dest, uint64_t n_pairs, int64_t* first_error, 
     DK(ensure(&d->out[0], d->out_cap[0], s1 + 16));
     DK(ensure(&d->out[1], d->out_cap[1], s2 + 16));
     const int cg = grid_for(P, 4, 16384);
-    hipLaunchKernelGGL(dmx_copy, dim3(cg), dim3(256), 0, d->stream, perm, P, d->rs[0], d->data[0], o1, d->out[0]);
+    hipLaunchKernelGGL(dmx_copy, dim3(cg), dim3(256), 0, d->stream, perm, P, d->rs[0], d->src[0], o1, d->out[0]);
     DK(hipGetLastError());
-    hipLaunchKernelGGL(dmx_copy, dim3(cg), dim3(256), 0, d->stream, perm, P, d->rs[1], d->data[1], o2, d->out[1]);
+    hipLaunchKernelGGL(dmx_copy, dim3(cg), dim3(256), 0, d->stream, perm, P, d->rs[1], d->src[1], o2, d->out[1]);
     DK(hipGetLastError());
     DK(hipStreamSynchronize(d->stream));
-    void* fr[] = {k_in, k_out, i_in, perm, l1, l2, o1, o2, first_pos, off1, off2, tmp};
-    for (void* x : fr) DK(hipFree(x));
     d->out_len[0] = s1;
     d->out_len[1] = s2;
     return FR_OK;

@@ -78,9 +78,63 @@ def gz_scan(n, files=4):
             "M_reads_per_s": round(n / dt / 1e6, 3)}
 
 
+def gz_demux(n, files=2, level=9):
+    """The whole `demux` command over `files` R1/R2 .fastq.gz pairs of n/files pairs each."""
+    import csv
+
+    import numpy as np
+
+    from frender_amd.demux import frender_demux
+
+    sheet = synth.make_sheet(96, 8, 8)
+    with tempfile.TemporaryDirectory() as d:
+        per = n // files
+        codes_total = {}
+        for f in range(files):
+            t1 = synth.generate_bytes(sheet, f * per, per, R=150, seed=1)
+            t2 = t1.replace(b" 1:N:0:", b" 2:N:0:")
+            synth.write_fastq_gz(os.path.join(d, f"syn_L{f + 1:03d}_R1_001.fastq.gz"), t1, level=1)
+            synth.write_fastq_gz(os.path.join(d, f"syn_L{f + 1:03d}_R2_001.fastq.gz"), t2, level=1)
+            ctx = _lib.Context(device=0, chunk_bytes=256 << 20, table_slots=1 << 20)
+            ctx.reset()
+            ctx.begin_file(None)
+            ctx.feed(t1)
+            ctx.end_file()
+            ctx.finalize()
+            keys, counts, _ = ctx.unique()
+            names, nid = _sheet_names(sheet.ids)
+            ctx.set_sheet(sheet.idx1, sheet.idx2, [reverse_complement(x) for x in sheet.idx2], nid, len(names))
+            c = ctx.classify(1, False)
+            ctx.close()
+            kinds = ("undetermined", "index_hop", "demuxable", "ambiguous")
+            for code, cls, row in zip(_lib.decode_keys(keys), c["cls"].tolist(), c["row"].tolist()):
+                codes_total[code] = (kinds[cls], sheet.ids[row] if cls == 2 else "")
+        res = os.path.join(d, "results.csv")
+        with open(res, "w", newline="") as f:
+            w = csv.writer(f)
+            w.writerow(["idx1", "idx2", "reads", "matched_idx1", "matched_idx2", "read_type", "sample_name", "demux_ok"])
+            for code, (t, sid) in codes_total.items():
+                a, b = code.split("+")[0:2]
+                w.writerow([a, b, 1, "", "", t, sid, True])
+        ins = sorted(os.path.join(d, x) for x in os.listdir(d) if x.endswith(".gz"))
+        args = types.SimpleNamespace(r=res, d=os.path.join(d, "out"), o=None, no_index_hop=False, no_ambiguous=False,
+                                     no_undeter=False, no_samples=False, files=ins, gz_level=level)
+        t0 = time.perf_counter()
+        frender_demux(args)
+        dt = time.perf_counter() - t0
+        out_bytes = sum(os.path.getsize(os.path.join(args.d, x)) for x in os.listdir(args.d))
+    return {"path": "gz_demux", "read_pairs": per * files, "files": files, "gz_level": level, "s": round(dt, 3),
+            "M_pairs_per_s": round(per * files / dt / 1e6, 3), "out_gz_bytes": out_bytes}
+
+
 if __name__ == "__main__":
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 50_000_000
     gzn = int(sys.argv[2]) if len(sys.argv) > 2 else 8_000_000
     if n:
         print(json.dumps(host_feed(n)), flush=True)
-    print(json.dumps(gz_scan(gzn)), flush=True)
+    if gzn:
+        print(json.dumps(gz_scan(gzn)), flush=True)
+    dmn = int(sys.argv[3]) if len(sys.argv) > 3 else 2_000_000
+    if dmn:
+        for lvl in (9, 1):
+            print(json.dumps(gz_demux(dmn, level=lvl)), flush=True)

@@ -18,7 +18,7 @@ constexpr int TILE = 16384;          // bytes per tile (one look-back unit)
 constexpr int SEG = TILE / WG;       // 64 contiguous bytes per thread
 constexpr int TSTEP = TILE - SEG;    // tile stride: tiles overlap by one segment, so the bitmaps
                                      // of a tile's last own segment always have a successor
-constexpr int HALO = 512;            // bytes loaded past the tile for headers that cross it
+constexpr int HALO = 0;              // bytes staged past the tile (lines past it are read from HBM)
 constexpr int LOG_NS = 10;
 constexpr int NS = 1 << LOG_NS;      // LDS hash slots per workgroup
 constexpr int LPROBE = 32;           // LDS probe bound before going to HBM directly

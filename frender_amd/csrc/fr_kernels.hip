@@ -152,7 +152,7 @@ struct alignas(16) LSlot {  // one ds_read_b128 reads key, count and first offse
 };
 
 struct ScanShared {
-    u8 buf[16 + TILE + HALO + 32];   // [0,16) = the 16 bytes before the tile; +32 pad for word reads
+    u8 buf[16 + TILE + HALO + 32];   // tile at [16, 16+TILE); +32 zero pad for word reads
     LSlot ls[NS];     // LDS hash table of this workgroup's chunk
     u32 wsum[WG / 64];
     u64 tile_excl;
@@ -291,10 +291,16 @@ __device__ __forceinline__ u64 lookback(const ScanArgs& a, u32 t, u32 agg, int l
 }
 
 // validate UTF-8 for the bytes [s0, s0+n) of the tile (only called when a byte >= 0x80
-// is present).  Byte at tile position q is sh.buf[16 + q]; positions < 0 are the 16 bytes
-// before the tile (zero when not readable), positions >= nb are past the readable end.
-__device__ bool utf8_segment_ok(const ScanShared& sh, int s0, int n, int nb) {
-    auto byte_at = [&](int q) -> int { return (q < nb && q >= -16) ? (int)sh.buf[16 + q] : -1; };
+// is present).  Bytes inside the staged tile come from LDS, others (before the tile or past
+// the staged bytes) from HBM when readable, -1 otherwise.
+__device__ bool utf8_segment_ok(const ScanShared& sh, const ScanArgs& a, u64 tile0, int s0, int n, int nb) {
+    auto byte_at = [&](int q) -> int {
+        if (q >= 0 && q < nb) return (int)sh.buf[16 + q];
+        const i64 g = (i64)tile0 + q;
+        if (q < 0 && g < 0 && !a.pre_valid) return -1;
+        if (g >= (i64)a.avail) return -1;
+        return (int)a.buf[g];
+    };
     for (int q = s0; q < s0 + n; ++q) {
         const int b = byte_at(q);
         if (b < 0x80) continue;
@@ -481,11 +487,10 @@ __device__ void process_header(ScanShared& sh, const ScanArgs& a, u64 tile0, u32
 #ifndef FR_PREFETCH
 #define FR_PREFETCH 1
 #endif
-constexpr int STAGE_VECS = (TILE + HALO + WG * 16 - 1) / (WG * 16);  // 5
+constexpr int STAGE_VECS = (TILE + HALO + WG * 16 - 1) / (WG * 16);  // 4
 
 struct TileRegs {
     uint4 v[STAGE_VECS];
-    uint4 pre;  // the 16 bytes before the tile (thread 0; UTF-8 continuation checks)
 };
 
 // Prefetch: unconditional 16-B loads whose results are not touched until tile_stage, so the
@@ -506,16 +511,11 @@ __device__ __forceinline__ void tile_fetch(const ScanArgs& a, u32 t, TileRegs& r
     const u8* ub = (const u8*)(((u64)hi << 32) | lo);
     const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)ub, (short)0, (int)__builtin_amdgcn_readfirstlane(nb),
                                                         0x00020000);
-    const bool pre_ok = live && (tile0 >= 16 || a.pre_valid);
-    const auto prsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(pre_ok ? ub - 16 : ub), (short)0, pre_ok ? 16 : 0,
-                                                         0x00020000);
 #pragma unroll
     for (int k = 0; k < STAGE_VECS; ++k) {
         const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, tid * 16, k * WG * 16, 0);
         r.v[k] = make_uint4(v[0], v[1], v[2], v[3]);
     }
-    const auto pv = __builtin_amdgcn_raw_buffer_load_b128(prsrc, 0, 0, 0);
-    r.pre = make_uint4(pv[0], pv[1], pv[2], pv[3]);
 }
 
 __device__ __forceinline__ void tile_stage(ScanShared& sh, const ScanArgs& a, u32 t, const TileRegs& r, int tid) {
@@ -534,7 +534,6 @@ __device__ __forceinline__ void tile_stage(ScanShared& sh, const ScanArgs& a, u3
             *(uint4*)(sh.buf + 16 + off) = v;
         }
     }
-    if (tid == 0) *(uint4*)(sh.buf) = r.pre;  // zeros when not readable (fetch descriptor)
 }
 
 struct TileCount {
@@ -611,7 +610,8 @@ __device__ __forceinline__ TileCount count_tile(ScanShared& sh, const ScanArgs& 
             tc.tmask = tm;
             if (hi) {
                 atomicOr(&sh.flags, 1u);
-                if (!utf8_segment_ok(sh, (int)s0, (int)min(valid, (u32)SEG), (int)nb)) atomicOr(&sh.flags, 2u);
+                if (!utf8_segment_ok(sh, a, tile0, (int)s0, (int)min(valid, (u32)SEG), (int)nb))
+                    atomicOr(&sh.flags, 2u);
             }
         }
     }

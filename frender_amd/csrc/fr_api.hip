@@ -31,6 +31,8 @@ struct fr_ctx {
     DevState* st = nullptr;
     DevState* h_st = nullptr;      // pinned snapshot
     bool st_fresh = false;         // h_st equals the device state (no device work on it since)
+    Table* d_tab = nullptr;        // device copy of tab for the tally kernel
+    Table* h_tab = nullptr;        // pinned staging of that copy (last uploaded value)
     hipEvent_t st_ev = nullptr;
     bool st_pending = false;
     u64* tiles = nullptr;
@@ -247,7 +249,12 @@ static int launch_range(fr_ctx* ctx, const u8* dptr, u64 len, u64 avail, int own
     a.max_records = ctx->max_records;
     a.st = ctx->st;
     a.tiles = ctx->tiles;
-    a.tab = ctx->tab;
+    if (std::memcmp(&ctx->tab, ctx->h_tab, sizeof(Table)) != 0) {  // the table moved: refresh its device copy
+        CK(hipStreamSynchronize(ctx->stream));  // the previous copy from h_tab has landed
+        std::memcpy(ctx->h_tab, &ctx->tab, sizeof(Table));
+        CK(hipMemcpyAsync(ctx->d_tab, ctx->h_tab, sizeof(Table), hipMemcpyHostToDevice, ctx->stream));
+    }
+    a.tab = ctx->d_tab;
     if (a.num_tiles > ctx->tiles_cap) return fail(ctx, FR_ERR_INVALID, "range larger than the look-back array");
     if (ctx->epoch >= 0x7FFFFFFFu) {  // tag wrap: restart epochs on a cleared descriptor array
         CK(hipMemsetAsync(ctx->tiles, 0, ctx->tiles_cap * sizeof(u64), ctx->stream));
@@ -306,6 +313,10 @@ fr_ctx* fr_create(int device, uint64_t chunk_bytes, uint64_t table_slots) {
     ctx->tiles_cap = RANGE_MAX / TSTEP + 2;
     ctx->nslots = pow2_at_least(std::max<u64>(table_slots, 1024));
     if ((e = hipMalloc((void**)&ctx->st, sizeof(DevState))) != hipSuccess) return bad("state", e);
+    if ((e = hipMalloc((void**)&ctx->d_tab, sizeof(Table))) != hipSuccess) return bad("table copy", e);
+    if ((e = hipHostMalloc((void**)&ctx->h_tab, sizeof(Table), hipHostMallocDefault)) != hipSuccess)
+        return bad("table staging", e);
+    std::memset(ctx->h_tab, 0, sizeof(Table));
     if ((e = hipHostMalloc((void**)&ctx->h_st, sizeof(DevState), hipHostMallocDefault)) != hipSuccess)
         return bad("pinned state", e);
     if ((e = hipEventCreateWithFlags(&ctx->st_ev, hipEventDisableTiming)) != hipSuccess) return bad("event", e);
@@ -343,7 +354,7 @@ void fr_destroy(fr_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->copy) (void)hipStreamSynchronize(ctx->copy);
-    void* dev[] = {ctx->st, ctx->tiles, ctx->tab.slots, ctx->tab.ovf, ctx->tab.pres, ctx->tab.exo_ord,
+    void* dev[] = {ctx->st, ctx->d_tab, ctx->tiles, ctx->tab.slots, ctx->tab.ovf, ctx->tab.pres, ctx->tab.exo_ord,
                    ctx->tab.exo_off, ctx->tab.exo_len, ctx->tab.exo_pool, ctx->dbuf[0], ctx->dbuf[1], ctx->d_sheet,
                    ctx->d_keys, ctx->d_counts, ctx->d_first, ctx->d_keys_s, ctx->d_counts_s,
                    ctx->d_first_s, ctx->d_pos, ctx->d_perm, ctx->d_rank, ctx->d_counter, ctx->d_temp, ctx->d_pres_u,
@@ -353,6 +364,7 @@ void fr_destroy(fr_ctx* ctx) {
         if (p) (void)hipFree(p);
     if (ctx->h_st) (void)hipHostFree(ctx->h_st);
     if (ctx->h_sheet) (void)hipHostFree(ctx->h_sheet);
+    if (ctx->h_tab) (void)hipHostFree(ctx->h_tab);
     for (int i = 0; i < 2; ++i) {
         if (ctx->pin[i]) (void)hipHostFree(ctx->pin[i]);
         if (ctx->copied[i]) (void)hipEventDestroy(ctx->copied[i]);

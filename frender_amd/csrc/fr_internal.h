@@ -104,7 +104,8 @@ struct ScanArgs {
     u64* cold;           // chunk kernel: cold lists, [grid][cold_cap] x {key, ordinal}
     DevState* st;
     u64* tiles;          // look-back descriptors
-    Table tab;
+    const Table* tab;    // device copy: read where used (rare paths), so the tile loop holds no
+                         // table fields in scalar registers
 };
 
 struct SheetArgs {

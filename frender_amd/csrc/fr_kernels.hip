@@ -184,6 +184,7 @@ __device__ __forceinline__ u64 make_ord(const ScanArgs& a, u64 off_in_range) {
 __device__ __forceinline__ void lds_insert(ScanShared& sh, const ScanArgs& a, u64 key, u32 off) {
     // one 32-bit multiply (keys hold <= 63 bits: fold the top down first)
     u32 h = (((u32)key ^ (u32)(key >> 27)) * 0x9E3779B1u) >> (32 - LOG_NS);
+#pragma unroll 2
     for (int pr = 0; pr < LPROBE; ++pr) {
         typedef u32 u32x4 __attribute__((ext_vector_type(4)));
         const u32x4 sl = *(const volatile u32x4*)&sh.ls[h];
@@ -224,7 +225,7 @@ __device__ __forceinline__ void lds_insert(ScanShared& sh, const ScanArgs& a, u6
         }
         // exact phase and a full cold list: insert directly
     }
-    if (global_insert(a.tab, a.st, key, 1, make_ord(a, off), a.file_tag)) atomicAdd(&sh.created, 1u);
+    if (global_insert(*a.tab, a.st, key, 1, make_ord(a, off), a.file_tag)) atomicAdd(&sh.created, 1u);
 }
 
 // Decoupled look-back over the launch's tile descriptors {tag = 2*epoch + inclusive, value}.
@@ -358,13 +359,13 @@ __device__ void exotic_record(const ScanArgs& a, u64 tile0, u32 p, u64 start, u6
     }
     const u64 i = atomicAdd((unsigned long long*)&a.st->n_exotic, 1ull);
     const u64 po = atomicAdd((unsigned long long*)&a.st->exo_pool_used, (unsigned long long)n);
-    if (i < a.tab.exo_cap && po + n <= a.tab.exo_pool_cap) {
-        a.tab.exo_ord[i] = make_ord(a, tile0 + p);
-        a.tab.exo_off[i] = po;
-        a.tab.exo_len[i] = (u32)n;
+    if (i < a.tab->exo_cap && po + n <= a.tab->exo_pool_cap) {
+        a.tab->exo_ord[i] = make_ord(a, tile0 + p);
+        a.tab->exo_off[i] = po;
+        a.tab->exo_len[i] = (u32)n;
         for (u64 k = 0; k < n; ++k) {
             const u64 q = start + k;
-            a.tab.exo_pool[po + k] = q < nb ? sh.buf[16 + q] : a.buf[tile0 + q];
+            a.tab->exo_pool[po + k] = q < nb ? sh.buf[16 + q] : a.buf[tile0 + q];
         }
     } else {
         atomicOr(&a.st->cap_flags, 4u);
@@ -718,7 +719,7 @@ __device__ __forceinline__ int infer_phase(const ScanShared& sh, u32 tlen) {
 template <int B>
 __device__ __forceinline__ u32 insert_many(const ScanArgs& a, const u64 (&key)[B], const u64 (&cnt)[B],
                                            const u64 (&ord)[B], const bool (&valid)[B]) {
-    const Table& T = a.tab;
+    const Table T = *a.tab;
     uint4 w0[B], w1[B];
     u64 h[B];
 #pragma unroll
@@ -790,11 +791,11 @@ __device__ __forceinline__ void commit_buffers(ScanShared& sh, const ScanArgs& a
         const u64 n = sh.exo_len[k];
         const u64 i = atomicAdd((unsigned long long*)&a.st->n_exotic, 1ull);
         const u64 po = atomicAdd((unsigned long long*)&a.st->exo_pool_used, (unsigned long long)n);
-        if (i < a.tab.exo_cap && po + n <= a.tab.exo_pool_cap) {
-            a.tab.exo_ord[i] = make_ord(a, sh.exo_p[k]);
-            a.tab.exo_off[i] = po;
-            a.tab.exo_len[i] = (u32)n;
-            for (u64 q = 0; q < n; ++q) a.tab.exo_pool[po + q] = a.buf[sh.exo_start[k] + q];
+        if (i < a.tab->exo_cap && po + n <= a.tab->exo_pool_cap) {
+            a.tab->exo_ord[i] = make_ord(a, sh.exo_p[k]);
+            a.tab->exo_off[i] = po;
+            a.tab->exo_len[i] = (u32)n;
+            for (u64 q = 0; q < n; ++q) a.tab->exo_pool[po + q] = a.buf[sh.exo_start[k] + q];
         } else {
             atomicOr(&a.st->cap_flags, 4u);
         }

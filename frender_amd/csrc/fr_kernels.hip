@@ -617,14 +617,18 @@ __device__ __forceinline__ TileCount count_tile(ScanShared& sh, const ScanArgs& 
         }
     }
     tc.c = __popcll(tc.tmask);
-    u32 x = tc.c;
+    // inclusive wave scan of c (<= 64, 7 bits) without LDS round trips: bit-sliced ballots,
+    // each lane counting the set bits of the lanes at or below it (v_mbcnt)
+    u32 x = 0, wtot = 0;
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const u32 y = __shfl_up(x, d, 64);
-        if (lane >= d) x += y;
+    for (int b = 0; b < 7; ++b) {
+        const u64 m = __ballot((tc.c >> b) & 1u);
+        x += (__builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u)) +
+              ((tc.c >> b) & 1u)) << b;
+        wtot += (u32)__popcll(m) << b;
     }
     tc.x = x;
-    if (lane == 63) sh.wsum[wid] = x;
+    if (lane == 0) sh.wsum[wid] = wtot;
     __syncthreads();
     u32 wexcl = 0, tot = 0;
 #pragma unroll

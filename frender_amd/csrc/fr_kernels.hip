@@ -1409,22 +1409,41 @@ __device__ __forceinline__ int mism(u64 q, u64 s) {  // Hamming distance of two 
 }
 
 constexpr int CLS_WG = 256;
-constexpr int CLS_LDS_ROWS = 2048;
-constexpr int RC_LDS_NAMES = 1024;
+constexpr int CLS_LDS_BYTES = 48 * 1024;  // dynamic LDS cap: sheet images + per-name rc sums
 
-__device__ __forceinline__ void class_of(u64 q1, u64 q2, const u64* s1, const u64* s2, int S, int nsubs, int& m1,
-                                         int& m2, int& cls, int& row) {
+__device__ __forceinline__ int mism32(u32 q, u32 s) {  // <= 10 symbols: 30 bits
+    const u32 x = q ^ s;
+    return __popc((x | (x >> 1) | (x >> 2)) & 0x09249249u);
+}
+
+template <typename W>
+__device__ __forceinline__ int mism_w(W q, W s) {
+    if constexpr (sizeof(W) == 4) return mism32(q, s);
+    else return mism(q, s);
+}
+
+// R7/R8 for one unique over every sheet row, forward idx2 and (rc) rc(idx2) in the same pass
+// (idx1's distances are shared): the first matching row of each list, |M1 ∩ M2| and its first row.
+template <typename W>
+__device__ __forceinline__ void class_pair(W q1, W q2, const W* s1, const W* s2, const W* s2rc, int S, int nsubs,
+                                           bool rc, int& m1, int& m2, int& cls, int& row, int& rm2, int& rcls,
+                                           int& rrow) {
     m1 = -1;
     m2 = -1;
-    int both = 0, r = -1;
+    rm2 = -1;
+    int both = 0, r = -1, rboth = 0, rr = -1;
     for (int i = 0; i < S; ++i) {
-        const bool a = mism(q1, s1[i]) <= nsubs;
-        const bool b = mism(q2, s2[i]) <= nsubs;
-        if (a && m1 < 0) m1 = i;
-        if (b && m2 < 0) m2 = i;
-        if (a && b) {
-            if (!both) r = i;
-            ++both;
+        const bool a = mism_w<W>(q1, s1[i]) <= nsubs;
+        const bool b = mism_w<W>(q2, s2[i]) <= nsubs;
+        m1 = (a && m1 < 0) ? i : m1;
+        m2 = (b && m2 < 0) ? i : m2;
+        r = (a && b && both == 0) ? i : r;
+        both += (a && b) ? 1 : 0;
+        if (rc) {
+            const bool c = mism_w<W>(q2, s2rc[i]) <= nsubs;
+            rm2 = (c && rm2 < 0) ? i : rm2;
+            rr = (a && c && rboth == 0) ? i : rr;
+            rboth += (a && c) ? 1 : 0;
         }
     }
     if (m1 >= 0 && m2 >= 0) {
@@ -1432,31 +1451,49 @@ __device__ __forceinline__ void class_of(u64 q1, u64 q2, const u64* s1, const u6
         row = both == 1 ? r : -1;
     } else {
         cls = CLS_UNDET;
+        row = -1;
+    }
+    if (m1 >= 0 && rm2 >= 0) {
+        rcls = rboth == 0 ? CLS_HOP : rboth == 1 ? CLS_DEMUX : CLS_AMBIG;
+        rrow = rboth == 1 ? rr : -1;
+    } else {
+        rcls = CLS_UNDET;
+        rm2 = -1;
+        rrow = -1;
+    }
+    if (cls == CLS_UNDET) {
         m1 = -1;
         m2 = -1;
-        row = -1;
     }
 }
 
+// One lane per unique code.  The sheet images (u32 when every entry has <= 10 symbols, else
+// u64) and the per-name rc sums live in dynamic LDS sized to the sheet; sheets too large for it
+// are read from HBM.
+template <typename W>
 __global__ __launch_bounds__(CLS_WG) void classify_kernel(const u64* keys, const u64* counts, u64 n, SheetArgs sh,
-                                                          int nsubs, int rc, ClassOut o) {
-    __shared__ u64 s1[CLS_LDS_ROWS], s2[CLS_LDS_ROWS], s2rc[CLS_LDS_ROWS];
-    __shared__ unsigned long long lf[RC_LDS_NAMES], lr[RC_LDS_NAMES];
-    const bool in_lds = sh.S <= CLS_LDS_ROWS;
-    const bool rc_lds = sh.n_names <= RC_LDS_NAMES;
-    if (in_lds) {
+                                                          int nsubs, int rc, ClassOut o, int sheet_in_lds,
+                                                          int names_in_lds) {
+    extern __shared__ __attribute__((aligned(16))) u8 cls_lds[];
+    unsigned long long* lf = (unsigned long long*)cls_lds;
+    unsigned long long* lr = lf + (names_in_lds ? sh.n_names : 0);
+    W* s1 = (W*)(lr + (names_in_lds ? sh.n_names : 0));
+    W* s2 = s1 + sh.S;
+    W* s2rc = s2 + sh.S;
+    if (sheet_in_lds) {
         for (int i = threadIdx.x; i < sh.S; i += CLS_WG) {
-            s1[i] = sh.i1[i];
-            s2[i] = sh.i2[i];
-            s2rc[i] = rc ? sh.i2rc[i] : 0;
+            s1[i] = (W)sh.i1[i];
+            s2[i] = (W)sh.i2[i];
+            s2rc[i] = rc ? (W)sh.i2rc[i] : (W)0;
         }
     }
-    if (rc && rc_lds)
+    if (rc && names_in_lds)
         for (int i = threadIdx.x; i < sh.n_names; i += CLS_WG) lf[i] = lr[i] = 0;
     __syncthreads();
-    const u64* S1 = in_lds ? s1 : sh.i1;
-    const u64* S2 = in_lds ? s2 : sh.i2;
-    const u64* S2rc = in_lds ? s2rc : sh.i2rc;
+    // sheets outside LDS: W is u64 then (the launcher guarantees it)
+    const W* S1 = sheet_in_lds ? s1 : (const W*)sh.i1;
+    const W* S2 = sheet_in_lds ? s2 : (const W*)sh.i2;
+    const W* S2rc = sheet_in_lds ? s2rc : (const W*)sh.i2rc;
 
     const u64 u = blockIdx.x * (u64)CLS_WG + threadIdx.x;
     if (u < n) {
@@ -1487,17 +1524,13 @@ __global__ __launch_bounds__(CLS_WG) void classify_kernel(const u64* keys, const
             else {
                 const u64 q1 = n1 ? (key & ((1ull << (3 * n1)) - 1ull)) : 0ull;
                 const u64 q2 = n2 ? ((key >> (3 * (p1 + 1))) & ((1ull << (3 * n2)) - 1ull)) : 0ull;
-                class_of(q1, q2, S1, S2, sh.S, nsubs, m1, m2, cls, row);
-                if (rc) {
-                    int rm1;
-                    class_of(q1, q2, S1, S2rc, sh.S, nsubs, rm1, rm2, rcls, rrow);
-                    // both calls demuxable to different sample NAMES -> ambiguous (frender.py:336-349)
-                    if (cls == CLS_DEMUX && rcls == CLS_DEMUX && sh.name[row] != sh.name[rrow]) {
-                        cls = CLS_AMBIG;
-                        row = -1;
-                        rcls = CLS_AMBIG;
-                        rrow = -1;
-                    }
+                class_pair<W>((W)q1, (W)q2, S1, S2, S2rc, sh.S, nsubs, rc != 0, m1, m2, cls, row, rm2, rcls, rrow);
+                // both calls demuxable to different sample NAMES -> ambiguous (frender.py:336-349)
+                if (rc && cls == CLS_DEMUX && rcls == CLS_DEMUX && sh.name[row] != sh.name[rrow]) {
+                    cls = CLS_AMBIG;
+                    row = -1;
+                    rcls = CLS_AMBIG;
+                    rrow = -1;
                 }
             }
         }
@@ -1518,17 +1551,17 @@ __global__ __launch_bounds__(CLS_WG) void classify_kernel(const u64* keys, const
             const u64 cnt = counts[u];
             if (cls == CLS_DEMUX) {
                 const int nm = sh.name[row];
-                if (rc_lds) atomicAdd(&lf[nm], (unsigned long long)cnt);
+                if (names_in_lds) atomicAdd(&lf[nm], (unsigned long long)cnt);
                 else atomicAdd((unsigned long long*)&o.rc_f[nm], (unsigned long long)cnt);
             }
             if (rcls == CLS_DEMUX) {
                 const int nm = sh.name[rrow];
-                if (rc_lds) atomicAdd(&lr[nm], (unsigned long long)cnt);
+                if (names_in_lds) atomicAdd(&lr[nm], (unsigned long long)cnt);
                 else atomicAdd((unsigned long long*)&o.rc_r[nm], (unsigned long long)cnt);
             }
         }
     }
-    if (rc && rc_lds) {
+    if (rc && names_in_lds) {
         __syncthreads();
         for (int i = threadIdx.x; i < sh.n_names; i += CLS_WG) {
             if (lf[i]) atomicAdd((unsigned long long*)&o.rc_f[i], lf[i]);
@@ -1541,7 +1574,21 @@ hipError_t launch_classify(const u64* keys, const u64* counts, u64 n, SheetArgs 
                            hipStream_t s) {
     if (!n) return hipSuccess;
     const u64 grid = (n + CLS_WG - 1) / CLS_WG;
-    hipLaunchKernelGGL(classify_kernel, dim3((u32)grid), dim3(CLS_WG), 0, s, keys, counts, n, sh, nsubs, rc, o);
+    // u32 images when every sheet entry (and so every matching query) has <= 10 symbols
+    const bool narrow = sh.S > 0 && sh.L1u >= 0 && sh.L1u <= 10 && sh.L2u >= 0 && sh.L2u <= 10;
+    const size_t wb = narrow ? 4 : 8;
+    const size_t names_bytes = rc ? 2ull * 8 * sh.n_names : 0;
+    const size_t sheet_bytes = 3 * wb * (size_t)std::max(sh.S, 0);
+    const int names_in_lds = (rc && names_bytes <= CLS_LDS_BYTES / 2) ? 1 : 0;
+    const size_t nb = names_in_lds ? names_bytes : 0;
+    const int sheet_in_lds = (nb + sheet_bytes <= CLS_LDS_BYTES) ? 1 : 0;
+    const size_t lds = nb + (sheet_in_lds ? sheet_bytes : 0) + 16;
+    if (narrow && sheet_in_lds)
+        hipLaunchKernelGGL(classify_kernel<u32>, dim3((u32)grid), dim3(CLS_WG), lds, s, keys, counts, n, sh, nsubs, rc,
+                           o, sheet_in_lds, names_in_lds);
+    else
+        hipLaunchKernelGGL(classify_kernel<u64>, dim3((u32)grid), dim3(CLS_WG), lds, s, keys, counts, n, sh, nsubs, rc,
+                           o, sheet_in_lds, names_in_lds);
     return hipGetLastError();
 }
 

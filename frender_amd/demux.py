@@ -64,21 +64,123 @@ def get_paired_files(files_list) -> list:
     return pairs
 
 
+def text_chunks(path, chunk=64 << 20):
+    """Decoded bytes of a .gz file as the reference's text-mode reader sees them (frender.py:776),
+    streamed: strict UTF-8 (UnicodeDecodeError otherwise, sequences may straddle chunks) and
+    universal newlines folded to '\n' (a '\r' ending a chunk waits for the next one)."""
+    import codecs
+
+    from .scan import _GzReader
+
+    rd = _GzReader(path, chunk)
+    dec = None
+    hold = b""
+    try:
+        for raw in rd:
+            data = hold + raw
+            hold = b""
+            if data.endswith(b"\r"):
+                hold, data = b"\r", data[:-1]
+            if np.frombuffer(data, dtype=np.uint8).max(initial=0) >= 0x80 or dec is not None:
+                dec = dec or codecs.getincrementaldecoder("utf-8")()
+                dec.decode(data)  # raises like gzip.open(..., "rt")
+            if b"\r" in data:
+                data = data.replace(b"\r\n", b"\n").replace(b"\r", b"\n")
+            if data:
+                yield data
+        if dec is not None:
+            dec.decode(b"", final=True)
+        if hold:
+            yield b"\n"
+    finally:
+        rd.close()
+
+
 def read_text(path) -> bytes:
-    """The decoded bytes as the reference's text-mode reader sees them (frender.py:776): strict
-    UTF-8 (UnicodeDecodeError otherwise) and universal newlines folded to '\\n'."""
-    with gzip.open(path, "rb") as g:
-        data = g.read()
-    if np.frombuffer(data, dtype=np.uint8).max(initial=0) >= 0x80:
-        data.decode("utf-8")  # raises like gzip.open(..., "rt")
-    if b"\r" in data:
-        data = data.replace(b"\r\n", b"\n").replace(b"\r", b"\n")
-    return data
+    """The whole decoded file (text-mode view): see text_chunks."""
+    return b"".join(text_chunks(path))
 
 
 def _line_at(data: bytes, start: int) -> bytes:
     e = data.find(b"\n", start)
     return data[start:] if e < 0 else data[start:e]
+
+
+def _demux_pair(dmx, pool, read1_file, read2_file, results, route_of, writers, window):
+    """One R1/R2 pair in record-aligned windows: the GPU indexes both windows, the complete
+    record pairs are routed, and the bytes after the last routed record carry into the next
+    window.  Pairing stops when either mate runs out of records (zip, frender.py:777)."""
+    streams = [text_chunks(read1_file), text_chunks(read2_file)]
+    bufs = [b"", b""]
+    eof = [False, False]
+    pending = []  # the previous window's gzip jobs: overlap with this window's inflate and GPU work
+    try:
+        while True:
+            for m in (0, 1):
+                parts = [bufs[m]]
+                size = len(bufs[m])
+                while size < window and not eof[m]:
+                    try:
+                        c = next(streams[m])
+                    except StopIteration:
+                        eof[m] = True
+                        break
+                    parts.append(c)
+                    size += len(c)
+                bufs[m] = b"".join(parts)
+            n = [dmx.load(0, bufs[0]), dmx.load(1, bufs[1])]
+            # the last record of a window may continue in the next one unless its file ended
+            done = [n[m] if eof[m] else max(n[m] - 1, 0) for m in (0, 1)]
+            n_pairs = min(done)
+            if n_pairs == 0:
+                if eof[0] or eof[1] or (not n[0] and not n[1]):
+                    break
+                window *= 2  # a record longer than the window: widen it
+                continue
+            ex = dmx.exotic(n_pairs)
+            if ex.size:  # codes outside the fast alphabet: resolve by string
+                starts, _ = dmx.records(1, ex)
+                dest = []
+                for s in starts.tolist():
+                    code = _line_at(bufs[1], s).split(b":")[-1].decode("utf-8")
+                    row = results.get(code)
+                    dest.append(_lib.FR_DMX_MISSING if row is None else route_of(row))
+                dmx.patch(ex, np.array(dest, dtype=np.int32))
+            first, val, b1, b2 = dmx.route(len(writers), n_pairs)
+            if first >= 0:
+                s, _ = dmx.records(1, [first])
+                code = _line_at(bufs[1], int(s[0])).split(b":")[-1].decode("utf-8")
+                if val == _lib.FR_DMX_MISSING:
+                    raise SystemExit(f"Couldn't find barcode {code} in supplied frender result file!")
+                raise SystemExit("Unrecognized read type found in supplied frender result file!")
+            o1 = dmx.fetch(0, int(b1.sum()))
+            o2 = dmx.fetch(1, int(b2.sum()))
+            for j in pending:
+                j.result()
+            c1 = np.concatenate([[0], np.cumsum(b1)]).astype(np.int64)
+            c2 = np.concatenate([[0], np.cumsum(b2)]).astype(np.int64)
+            pending = []
+            for k, w in enumerate(writers):
+                if b1[k]:
+                    pending.append(pool.submit(w["R1"].write, memoryview(o1)[c1[k]:c1[k + 1]]))
+                if b2[k]:
+                    pending.append(pool.submit(w["R2"].write, memoryview(o2)[c2[k]:c2[k + 1]]))
+            # carry the bytes after the routed records
+            cut = []
+            for m in (0, 1):
+                if n_pairs < n[m]:
+                    s, _ = dmx.records(m, [n_pairs])
+                    cut.append(int(s[0]))
+                else:
+                    cut.append(len(bufs[m]))
+            bufs = [bufs[0][cut[0]:], bufs[1][cut[1]:]]
+            if (eof[0] and n_pairs == n[0]) or (eof[1] and n_pairs == n[1]):
+                break
+    finally:
+        for j in pending:
+            j.result()
+        for st in streams:
+            st.close()
 
 
 def frender_demux(args, dev=None) -> None:
@@ -139,46 +241,14 @@ def frender_demux(args, dev=None) -> None:
         spec = {"file": [Path(f) for f in args.files]}
     pairs = get_paired_files(parse_files(spec, just_r1=False))
 
+    window = int(getattr(args, "window", None) or (512 << 20))  # decoded bytes per mate per GPU pass
     dmx = dev or _lib.Demux(int(os.environ.get("LOCAL_RANK", "0")))
     pool = ThreadPoolExecutor(max_workers=max(2, min(32, len(writers) * 2)))
     try:
         dmx.set_table(keys[fast], vals[fast])
         for read1_file, read2_file in pairs:
             print(f"Demultiplexing {read1_file.name}...")
-            f1 = pool.submit(read_text, read1_file)
-            d2 = read_text(read2_file)
-            d1 = f1.result()
-            n1 = dmx.load(0, d1)
-            n2 = dmx.load(1, d2)
-            n_pairs = min(n1, n2)  # zip() stops at the shorter file
-            ex = dmx.exotic(n_pairs)
-            if ex.size:  # codes outside the fast alphabet: resolve by string
-                starts, _ = dmx.records(1, ex)
-                dest = []
-                for s in starts.tolist():
-                    code = _line_at(d2, s).split(b":")[-1].decode("utf-8")
-                    row = results.get(code)
-                    dest.append(_lib.FR_DMX_MISSING if row is None else route_of(row))
-                dmx.patch(ex, np.array(dest, dtype=np.int32))
-            first, val, b1, b2 = dmx.route(len(writers), n_pairs)
-            if first >= 0:
-                s, _ = dmx.records(1, [first])
-                code = _line_at(d2, int(s[0])).split(b":")[-1].decode("utf-8")
-                if val == _lib.FR_DMX_MISSING:
-                    raise SystemExit(f"Couldn't find barcode {code} in supplied frender result file!")
-                raise SystemExit("Unrecognized read type found in supplied frender result file!")
-            o1 = dmx.fetch(0, int(b1.sum()))
-            o2 = dmx.fetch(1, int(b2.sum()))
-            c1 = np.concatenate([[0], np.cumsum(b1)]).astype(np.int64)
-            c2 = np.concatenate([[0], np.cumsum(b2)]).astype(np.int64)
-            jobs = []
-            for k, w in enumerate(writers):
-                if b1[k]:
-                    jobs.append(pool.submit(w["R1"].write, memoryview(o1)[c1[k]:c1[k + 1]]))
-                if b2[k]:
-                    jobs.append(pool.submit(w["R2"].write, memoryview(o2)[c2[k]:c2[k + 1]]))
-            for j in jobs:
-                j.result()
+            _demux_pair(dmx, pool, read1_file, read2_file, results, route_of, writers, window)
     finally:
         pool.shutdown(wait=True)
         for w in writers:

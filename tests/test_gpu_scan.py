@@ -332,8 +332,8 @@ def test_demux_golden_on_gpu(name):
     assert not diffs, "\n".join(diffs)
 
 
-@pytest.mark.parametrize("seed", [1, 2])
-def test_demux_random_vs_oracle(seed, tmp_path):
+@pytest.mark.parametrize("seed,window", [(1, None), (2, None), (3, 20000), (4, 4096)])
+def test_demux_random_vs_oracle(seed, window, tmp_path):
     """Random paired inputs with mixed codes, CRLF/CR, long headers and a short R2 against
     the demux oracle (content of every writer)."""
     import argparse
@@ -369,7 +369,8 @@ def test_demux_random_vs_oracle(seed, tmp_path):
 
     def ns(d):
         return argparse.Namespace(r=str(inp / "results.csv"), d=str(d), o=None, no_index_hop=False,
-                                  no_ambiguous=False, no_undeter=False, no_samples=False, files=files)
+                                  no_ambiguous=False, no_undeter=False, no_samples=False, files=files,
+                                  window=window)
 
     want = demux_oracle.demux(ns(tmp_path / "o_ref"))
     frender_demux(ns(tmp_path / "o_gpu"))

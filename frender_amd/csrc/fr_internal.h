@@ -21,7 +21,10 @@ constexpr int TSTEP = TILE - SEG;    // tile stride: tiles overlap by one segmen
 constexpr int HALO = 0;              // bytes staged past the tile (lines past it are read from HBM)
 constexpr int LOG_NS = 10;
 constexpr int NS = 1 << LOG_NS;      // LDS hash slots per workgroup
-constexpr int LPROBE = 32;           // LDS probe bound before going to HBM directly
+#ifndef FR_LPROBE
+#define FR_LPROBE 4
+#endif
+constexpr int LPROBE = FR_LPROBE;          // LDS probe bound before going to HBM directly
 constexpr int GPROBE = 256;          // HBM probe bound before the overflow list
 constexpr int MAXSYM = 21;           // fast key: <= 21 symbols of 3 bits
 constexpr u64 RANGE_MAX = 1ull << 30;  // bytes per tally launch (device feeds)

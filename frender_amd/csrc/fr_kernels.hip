@@ -22,6 +22,14 @@
 
 namespace fr {
 
+// FR_OUTLINE_COLD=1 keeps the rare paths out of line (measured slower: the calls make the
+// hot loop save registers to scratch)
+#if FR_OUTLINE_COLD
+#define FR_COLD __attribute__((noinline))
+#else
+#define FR_COLD __forceinline__
+#endif
+
 // ------------------------------------------------------------------------------------
 // small helpers
 // ------------------------------------------------------------------------------------
@@ -181,6 +189,10 @@ __device__ __forceinline__ u64 make_ord(const ScanArgs& a, u64 off_in_range) {
     return ((u64)a.file_tag << ORD_SHIFT) | (a.file_offset + off_in_range);
 }
 
+__device__ FR_COLD void direct_insert(ScanShared& sh, const ScanArgs& a, u64 key, u32 off) {
+    if (global_insert(*a.tab, a.st, key, 1, make_ord(a, off), a.file_tag)) atomicAdd(&sh.created, 1u);
+}
+
 __device__ __forceinline__ void lds_insert(ScanShared& sh, const ScanArgs& a, u64 key, u32 off) {
     // one 32-bit multiply (keys hold <= 63 bits: fold the top down first)
     u32 h = (((u32)key ^ (u32)(key >> 27)) * 0x9E3779B1u) >> (32 - LOG_NS);
@@ -225,7 +237,7 @@ __device__ __forceinline__ void lds_insert(ScanShared& sh, const ScanArgs& a, u6
         }
         // exact phase and a full cold list: insert directly
     }
-    if (global_insert(*a.tab, a.st, key, 1, make_ord(a, off), a.file_tag)) atomicAdd(&sh.created, 1u);
+    direct_insert(sh, a, key, off);
 }
 
 // Decoupled look-back over the launch's tile descriptors {tag = 2*epoch + inclusive, value}.
@@ -294,7 +306,7 @@ __device__ __forceinline__ u64 lookback(const ScanArgs& a, u32 t, u32 agg, int l
 // validate UTF-8 for the bytes [s0, s0+n) of the tile (only called when a byte >= 0x80
 // is present).  Bytes inside the staged tile come from LDS, others (before the tile or past
 // the staged bytes) from HBM when readable, -1 otherwise.
-__device__ bool utf8_segment_ok(const ScanShared& sh, const ScanArgs& a, u64 tile0, int s0, int n, int nb) {
+__device__ FR_COLD bool utf8_segment_ok(const ScanShared& sh, const ScanArgs& a, u64 tile0, int s0, int n, int nb) {
     auto byte_at = [&](int q) -> int {
         if (q >= 0 && q < nb) return (int)sh.buf[16 + q];
         const i64 g = (i64)tile0 + q;
@@ -757,7 +769,16 @@ __device__ __forceinline__ u32 insert_many(const ScanArgs& a, const u64 (&key)[B
 __device__ __forceinline__ void commit_buffers(ScanShared& sh, const ScanArgs& a, bool table, int tid) {
     __syncthreads();
     u32 made = 0;
-    if (table) {
+    if (a.ablate & 64u) {  // diag: flushed LDS slots and cold entries per commit
+        u32 live = 0;
+        for (int i = tid; i < NS; i += WG) live += sh.ls[i].key != 0;
+        if (live) atomicAdd((unsigned long long*)&a.st->stamp[4], (unsigned long long)live);
+        if (tid == 0) atomicAdd((unsigned long long*)&a.st->stamp[5], (unsigned long long)min(sh.ncold, a.cold_cap));
+        if (tid == 0) atomicAdd((unsigned long long*)&a.st->stamp[6], 1ull);
+    }
+    const bool flush = table && !(a.ablate & 8u);  // ablation 8: no HBM flush of the LDS table / cold list
+    const u32 nc = (a.ablate & 8u) ? 0u : min(sh.ncold, a.cold_cap);
+    if (flush) {
         for (int i0 = tid; i0 < NS; i0 += 2 * WG) {
             u64 key[2], cnt[2], ord[2];
             bool v[2];
@@ -773,7 +794,6 @@ __device__ __forceinline__ void commit_buffers(ScanShared& sh, const ScanArgs& a
             made += insert_many<2>(a, key, cnt, ord, v);
         }
     }
-    const u32 nc = min(sh.ncold, a.cold_cap);
     const u64* cl = a.cold + 2ull * (u64)blockIdx.x * a.cold_cap;
     for (u32 i0 = tid; i0 < nc; i0 += 2 * WG) {
         u64 key[2], cnt[2], ord[2];
@@ -868,7 +888,7 @@ __device__ __forceinline__ bool encode_perm(const u8* lb, u32 start, u32 n, u64&
 }
 
 // the rare header outcomes: word-scan fallback, no ' ' (IndexError), or an exotic code
-__device__ __forceinline__ void slow_header(ScanShared& sh, const ScanArgs& a, u64 tile0, u32 p, u32 nb, int r,
+__device__ FR_COLD void slow_header(ScanShared& sh, const ScanArgs& a, u64 tile0, u32 p, u32 nb, int r,
                                          u32 start, u32 n) {
     if (r == 2) process_header(sh, a, tile0, p, nb);
     else if (r == 1) nospace(a, tile0, p, sh);

@@ -1,0 +1,6 @@
+#!/bin/bash
+# Build an experimental variant of the library: scripts/build_exp.sh NAME "-DFOO=1 -DBAR=2"
+set -eu
+cd "$(dirname "$0")/.."
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared $2 -I include \
+  frender_amd/csrc/fr_kernels.hip frender_amd/csrc/fr_api.hip frender_amd/csrc/fr_demux.hip -o frender_amd/libfrender_hip_exp_$1.so

@@ -43,8 +43,12 @@ struct fr_ctx {
     Table tab{};
     u64 nslots = 0;
 
-    // host feed ring
+    // launch sizes: chunk_bytes bytes per tally launch of device feeds (<= RANGE_MAX); host feeds
+    // go through a pinned ring of ring_bytes slots (<= HOST_CHUNK_MAX)
     u64 chunk_bytes = 0;
+    u64 ring_bytes = 0;
+    u32 chunk_tiles = 64;  // tiles per full chunk of a ramped launch (FR_CHUNK_TILES)
+    bool ramp = true;      // FR_RAMP=0: one uniform chunk per workgroup
     u8* pin[2] = {nullptr, nullptr};
     u8* dbuf[2] = {nullptr, nullptr};
     hipEvent_t copied[2] = {nullptr, nullptr};
@@ -271,11 +275,25 @@ static int launch_range(fr_ctx* ctx, const u8* dptr, u64 len, u64 avail, int own
         ctx->ev_b.push_back(e2);
     }
     CK(hipEventRecord(ctx->ev_a[ctx->ev_used], ctx->stream));
-    a.chunk_tiles = (u32)std::max<u64>(1, (a.num_tiles + ctx->grid - 1) / ctx->grid);
-    a.num_chunks = (a.num_tiles + a.chunk_tiles - 1) / a.chunk_tiles;
+    // chunking (chunk_bounds in fr_kernels.hip): ramped when the range holds both ramps and a full
+    // chunk, else one uniform chunk per workgroup
+    const u64 G = (u64)ctx->grid, C = ctx->chunk_tiles;
+    const u64 rg = G + ((C - 1) * G * (G + 1)) / (2 * G);  // R(G)
+    if (ctx->ramp && (u64)a.num_tiles >= 2 * rg + C) {
+        a.ramp_g = (u32)G;
+        a.chunk_tiles = (u32)C;
+        a.mid_chunks = (u32)(((u64)a.num_tiles - 2 * rg + C - 1) / C);
+        a.num_chunks = (u32)(2 * G) + a.mid_chunks;
+    } else {
+        a.ramp_g = 0;
+        a.mid_chunks = 0;
+        a.chunk_tiles = (u32)std::max<u64>(1, (a.num_tiles + G - 1) / G);
+        a.num_chunks = (a.num_tiles + a.chunk_tiles - 1) / a.chunk_tiles;
+    }
     a.cold_cap = ctx->cold_cap;
     a.cold = ctx->cold;
-    CK(launch_chunk_scan(a, (int)a.num_chunks, ctx->stream));
+    // workgroups take chunks by ticket; never more than the resident grid (cold lists are per block)
+    CK(launch_chunk_scan(a, (int)std::min<u64>(a.num_chunks, G), ctx->stream));
     CK(hipEventRecord(ctx->ev_b[ctx->ev_used], ctx->stream));
     ctx->ev_used++;
     ctx->scan_launches++;
@@ -310,6 +328,9 @@ fr_ctx* fr_create(int device, uint64_t chunk_bytes, uint64_t table_slots) {
 
     ctx->chunk_bytes = chunk_bytes ? ((chunk_bytes + TILE - 1) / TILE) * TILE : (256ull << 20);
     if (ctx->chunk_bytes > RANGE_MAX) ctx->chunk_bytes = RANGE_MAX;
+    ctx->ring_bytes = std::min<u64>(ctx->chunk_bytes, HOST_CHUNK_MAX);
+    if (const char* f = getenv("FR_CHUNK_TILES")) ctx->chunk_tiles = (u32)std::max(2, atoi(f));
+    if (const char* f = getenv("FR_RAMP")) ctx->ramp = atoi(f) != 0;
     ctx->tiles_cap = RANGE_MAX / TSTEP + 2;
     ctx->nslots = pow2_at_least(std::max<u64>(table_slots, 1024));
     if ((e = hipMalloc((void**)&ctx->st, sizeof(DevState))) != hipSuccess) return bad("state", e);
@@ -335,9 +356,9 @@ fr_ctx* fr_create(int device, uint64_t chunk_bytes, uint64_t table_slots) {
     if ((e = dalloc(&ctx->tab.exo_len, ctx->tab.exo_cap)) != hipSuccess) return bad("exotic", e);
     if ((e = dalloc(&ctx->tab.exo_pool, ctx->tab.exo_pool_cap)) != hipSuccess) return bad("exotic", e);
     for (int i = 0; i < 2; ++i) {
-        if ((e = hipHostMalloc((void**)&ctx->pin[i], ctx->chunk_bytes, hipHostMallocDefault)) != hipSuccess)
+        if ((e = hipHostMalloc((void**)&ctx->pin[i], ctx->ring_bytes, hipHostMallocDefault)) != hipSuccess)
             return bad("pinned ring", e);
-        if ((e = dalloc(&ctx->dbuf[i], ctx->chunk_bytes + 64)) != hipSuccess) return bad("device ring", e);
+        if ((e = dalloc(&ctx->dbuf[i], ctx->ring_bytes + 64)) != hipSuccess) return bad("device ring", e);
         if ((e = hipEventCreateWithFlags(&ctx->copied[i], hipEventDisableTiming)) != hipSuccess) return bad("event", e);
         if ((e = hipEventCreateWithFlags(&ctx->consumed[i], hipEventDisableTiming)) != hipSuccess)
             return bad("event", e);
@@ -557,9 +578,9 @@ int fr_feed(fr_ctx* ctx, const uint8_t* data, uint64_t len) {
         if (ctx->used[slot]) CK(hipEventSynchronize(ctx->copied[slot]));  // pinned slot free again
         u8* pin = ctx->pin[slot];
         const u64 nc = ctx->carry.size();
-        if (nc >= ctx->chunk_bytes) return fail(ctx, FR_ERR_CAPACITY, "a line is longer than the chunk size");
+        if (nc >= ctx->ring_bytes) return fail(ctx, FR_ERR_CAPACITY, "a line is longer than the chunk size");
         if (nc) std::memcpy(pin, ctx->carry.data(), nc);
-        const u64 take = std::min<u64>(len - done, ctx->chunk_bytes - nc);
+        const u64 take = std::min<u64>(len - done, ctx->ring_bytes - nc);
         std::memcpy(pin + nc, data + done, take);
         done += take;
         const u64 n = nc + take;
@@ -586,8 +607,11 @@ int fr_feed_device(fr_ctx* ctx, const uint8_t* dev_data, uint64_t len) {
     if (ctx->file_offset != 0 || !ctx->carry.empty())
         return fail(ctx, FR_ERR_INVALID, "fr_feed_device takes a whole file (no prior fr_feed)");
     if (((uintptr_t)dev_data & 15u) != 0) return fail(ctx, FR_ERR_INVALID, "device data must be 16-byte aligned");
-    for (u64 off = 0; off < len; off += ctx->chunk_bytes) {
-        const u64 n = std::min<u64>(ctx->chunk_bytes, len - off);
+    // equal ranges of at most chunk_bytes
+    const u64 nr = (len + ctx->chunk_bytes - 1) / ctx->chunk_bytes;
+    const u64 step = nr ? (len + nr - 1) / nr : 0;
+    for (u64 off = 0; off < len; off += step) {
+        const u64 n = std::min<u64>(step, len - off);
         int rc = launch_range(ctx, dev_data + off, n, len - off, off == 0 ? 1 : 0, 1, off ? 1 : 0);
         if (rc) return rc;
     }

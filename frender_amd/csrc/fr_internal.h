@@ -27,7 +27,9 @@ constexpr int NS = 1 << LOG_NS;      // LDS hash slots per workgroup
 constexpr int LPROBE = FR_LPROBE;          // LDS probe bound before going to HBM directly
 constexpr int GPROBE = 256;          // HBM probe bound before the overflow list
 constexpr int MAXSYM = 21;           // fast key: <= 21 symbols of 3 bits
-constexpr u64 RANGE_MAX = 1ull << 30;  // bytes per tally launch (device feeds)
+constexpr u64 RANGE_MAX = (4ull << 30) - (1ull << 20);  // bytes per tally launch (device feeds): range
+                                     // offsets, LDS first-offsets and per-range line counts stay u32
+constexpr u64 HOST_CHUNK_MAX = 1ull << 30;  // bytes per host-fed launch (pinned ring slot)
 constexpr u32 SPIN_MAX = 1u << 24;   // look-back spin bound (then FR_ERR_DEVICE)
 constexpr int ORD_SHIFT = 44;        // ordinal = file_tag << 44 | file byte offset
 constexpr int EXO_BUF = 32;          // chunk kernel: exotic records buffered while speculating
@@ -103,6 +105,10 @@ struct ScanArgs {
     u32 ablate;          // timing ablation bits (FR_ABLATE; 0 in production): 1 parse, 2 encode, 4 insert
     u32 chunk_tiles;     // chunk kernel: tiles per chunk (a workgroup's contiguous unit)
     u32 num_chunks;
+    u32 ramp_g;          // 0: uniform chunks of chunk_tiles.  Else the first ramp_g chunks grow and the
+                         // last ramp_g shrink linearly (chunk_bounds), so workgroups finish their chunks
+                         // (look-back, HBM commit) at staggered times and all run out of work together
+    u32 mid_chunks;      // full chunks between the two ramps
     u32 cold_cap;        // chunk kernel: entries of each workgroup's cold list
     u64* cold;           // chunk kernel: cold lists, [grid][cold_cap] x {key, ordinal}
     DevState* st;

@@ -765,7 +765,12 @@ __device__ __forceinline__ u32 insert_many(const ScanArgs& a, const u64 (&key)[B
     return made;
 }
 
-// publish the LDS table and/or the cold list / buffered side effects into HBM (all threads)
+// publish the LDS table and/or the cold list / buffered side effects into HBM (all threads).
+// CB entries per thread have their slot loads in flight together.
+#ifndef FR_CB
+#define FR_CB 4
+#endif
+constexpr int CB = FR_CB;
 __device__ __forceinline__ void commit_buffers(ScanShared& sh, const ScanArgs& a, bool table, int tid) {
     __syncthreads();
     u32 made = 0;
@@ -779,11 +784,11 @@ __device__ __forceinline__ void commit_buffers(ScanShared& sh, const ScanArgs& a
     const bool flush = table && !(a.ablate & 8u);  // ablation 8: no HBM flush of the LDS table / cold list
     const u32 nc = (a.ablate & 8u) ? 0u : min(sh.ncold, a.cold_cap);
     if (flush) {
-        for (int i0 = tid; i0 < NS; i0 += 2 * WG) {
-            u64 key[2], cnt[2], ord[2];
-            bool v[2];
+        for (int i0 = tid; i0 < NS; i0 += CB * WG) {
+            u64 key[CB], cnt[CB], ord[CB];
+            bool v[CB];
 #pragma unroll
-            for (int b = 0; b < 2; ++b) {
+            for (int b = 0; b < CB; ++b) {
                 const int i = i0 + b * WG;
                 const LSlot e = i < NS ? sh.ls[i] : LSlot{0, 0, 0};
                 v[b] = e.key != 0;
@@ -791,22 +796,22 @@ __device__ __forceinline__ void commit_buffers(ScanShared& sh, const ScanArgs& a
                 cnt[b] = e.cnt;
                 ord[b] = v[b] ? make_ord(a, e.mino) : 0;
             }
-            made += insert_many<2>(a, key, cnt, ord, v);
+            made += insert_many<CB>(a, key, cnt, ord, v);
         }
     }
     const u64* cl = a.cold + 2ull * (u64)blockIdx.x * a.cold_cap;
-    for (u32 i0 = tid; i0 < nc; i0 += 2 * WG) {
-        u64 key[2], cnt[2], ord[2];
-        bool v[2];
+    for (u32 i0 = tid; i0 < nc; i0 += CB * WG) {
+        u64 key[CB], cnt[CB], ord[CB];
+        bool v[CB];
 #pragma unroll
-        for (int b = 0; b < 2; ++b) {
+        for (int b = 0; b < CB; ++b) {
             const u32 i = i0 + b * WG;
             v[b] = i < nc;
             key[b] = v[b] ? cl[2 * i] : 0;
             ord[b] = v[b] ? cl[2 * i + 1] : 0;
             cnt[b] = 1;
         }
-        made += insert_many<2>(a, key, cnt, ord, v);
+        made += insert_many<CB>(a, key, cnt, ord, v);
     }
     if (made) atomicAdd(&sh.created, made);
     // buffered exotic records and the first "no space" error
@@ -1056,6 +1061,36 @@ __device__ __forceinline__ u64 walk_chunk(ScanShared& sh, const ScanArgs& a, u32
     return lines;
 }
 
+// Tiles [tb, te) of chunk c.  Uniform: chunk_tiles each.  Ramped (ramp_g = G > 0, C = chunk_tiles):
+// R(j) = j + floor((C-1) j (j+1) / 2G) tiles precede ramp-up chunk j, so chunk j holds
+// 1 + ~(C-1)(j+1)/G tiles and the G first chunks, all taken at once, finish in ticket order;
+// mid_chunks full chunks follow; the last G chunks mirror the ramp-up, so every workgroup runs
+// out of work at about the same time.  fr_api only ramps ranges of >= 2 R(G) + C tiles.
+__device__ __forceinline__ u64 ramp_prefix(const ScanArgs& a, u64 j) {
+    return j + ((u64)(a.chunk_tiles - 1u) * j * (j + 1)) / (2ull * a.ramp_g);
+}
+
+__device__ __forceinline__ void chunk_bounds(const ScanArgs& a, u32 c, u32& tb, u32& te) {
+    if (a.ramp_g == 0) {
+        tb = min(c * a.chunk_tiles, a.num_tiles);
+        te = min(tb + a.chunk_tiles, a.num_tiles);
+        return;
+    }
+    const u64 G = a.ramp_g, rg = ramp_prefix(a, G), mid_end = (u64)a.num_tiles - rg;
+    if (c < G) {
+        tb = (u32)ramp_prefix(a, c);
+        te = (u32)ramp_prefix(a, c + 1);
+    } else if (c < G + a.mid_chunks) {
+        const u64 b = rg + (u64)(c - G) * a.chunk_tiles;
+        tb = (u32)b;
+        te = (u32)min(b + a.chunk_tiles, mid_end);
+    } else {
+        const u64 j = c - G - a.mid_chunks;  // 0 .. G-1: shrinking
+        tb = (u32)((u64)a.num_tiles - ramp_prefix(a, G - j));
+        te = (u32)((u64)a.num_tiles - ramp_prefix(a, G - j - 1));
+    }
+}
+
 #ifndef FR_OCC
 #define FR_OCC 4  // workgroups (= waves per SIMD) per CU; fr_api sizes the grid with fr_chunk_occupancy()
 #endif
@@ -1085,17 +1120,18 @@ __global__ __launch_bounds__(WG, FR_OCC) void chunk_kernel(ScanArgs a) {
         __syncthreads();
         const u32 c = sh.chunk;
         if (c >= a.num_chunks) break;
-        const u32 tb = c * a.chunk_tiles;
-        const u32 te = min(tb + a.chunk_tiles, a.num_tiles);
+        u32 tb, te;
+        chunk_bounds(a, c, tb, te);
         // ---- the line phase at the chunk start: exact for chunk 0, else guessed ----------
 #ifdef FR_STAMPS
         u64 stamps[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         u64 last_ = __builtin_amdgcn_s_memtime();
 #endif
+        const bool empty = tb >= te;  // defensive: no tile to stage (publishes 0 lines)
         int P = -1;
         if (c == 0) {
             P = (int)(base_lines & 3ull);
-        } else if (a.max_records <= 0) {
+        } else if (a.max_records <= 0 && !empty) {
             TileRegs r;
             tile_fetch(a, tb, r, tid);
             tile_stage(sh, a, tb, r, tid);
@@ -1117,7 +1153,7 @@ __global__ __launch_bounds__(WG, FR_OCC) void chunk_kernel(ScanArgs a) {
         if (tid == 0) sh.spec = spec ? 1u : 0u;
         __syncthreads();
         for (int pass = 0;; ++pass) {
-            const u64 cnt = walk_chunk(sh, a, tb, te, L0, parse, exact, tid, lane, wid);
+            const u64 cnt = empty ? 0ull : walk_chunk(sh, a, tb, te, L0, parse, exact, tid, lane, wid);
 #ifdef FR_STAMPS
             last_ = __builtin_amdgcn_s_memtime();
 #endif
@@ -1137,7 +1173,7 @@ __global__ __launch_bounds__(WG, FR_OCC) void chunk_kernel(ScanArgs a) {
             __syncthreads();
             STAMP(6);
             const u64 exact_L = base_lines + sh.tile_excl;
-            const bool keep = c == 0 || (spec && (u32)P == (u32)(exact_L & 3ull) && !uniform_flag(sh.spec_bad));
+            const bool keep = c == 0 || empty || (spec && (u32)P == (u32)(exact_L & 3ull) && !uniform_flag(sh.spec_bad));
             if (keep) break;
             discard_buffers(sh, tid);
             L0 = exact_L;

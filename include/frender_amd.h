@@ -64,6 +64,9 @@ typedef struct fr_timing {
 } fr_timing;
 
 /* ---- lifecycle ------------------------------------------------------------------ */
+/* chunk_bytes: bytes per tally launch, at most 4 GiB - 1 MiB (device feeds are cut into equal
+ * ranges of at most this size; host feeds use a pinned ring of min(chunk_bytes, 1 GiB) slots).
+ * table_slots: initial HBM hash-table slots (grown between launches). */
 fr_ctx* fr_create(int device, uint64_t chunk_bytes, uint64_t table_slots);
 void fr_destroy(fr_ctx* ctx);
 const char* fr_last_error(const fr_ctx* ctx);

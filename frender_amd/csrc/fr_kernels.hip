@@ -658,6 +658,174 @@ __device__ __forceinline__ TileCount count_tile(ScanShared& sh, const ScanArgs& 
     return tc;
 }
 
+// ---- v5 staging: lane-contiguous segments classified straight from registers ---------
+// Lane tid loads its own 64-byte segment [tid*64, tid*64+64) of the tile (four 16-B loads) plus
+// the first dword of the next segment (a '\r' ending the segment needs the byte after it), so the
+// byte classification runs on the loaded registers: no LDS read-back, and two barriers per tile
+// (B1: the previous tile's parse is done with the LDS tile; B2: this tile's bytes, bitmaps and
+// wave sums are in LDS).
+#ifndef FR_V5
+#define FR_V5 1
+#endif
+struct SegRegs {
+    uint4 v[SEG / 16];
+    u32 nx;  // first dword of the next segment (zero past the staged bytes)
+};
+
+__device__ __forceinline__ void seg_fetch(const ScanArgs& a, u32 t, SegRegs& r, int tid, bool want = true) {
+    const bool live = want && t < a.num_tiles;
+    const u64 tile0 = live ? (u64)t * TSTEP : 0ull;
+    const u32 nb = live ? (u32)min((u64)(TILE + HALO), a.avail - tile0) : 0u;
+    const u64 base = (u64)(a.buf + tile0);
+    const u32 lo = __builtin_amdgcn_readfirstlane((u32)base), hi = __builtin_amdgcn_readfirstlane((u32)(base >> 32));
+    const u8* ub = (const u8*)(((u64)hi << 32) | lo);
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)ub, (short)0, (int)__builtin_amdgcn_readfirstlane(nb),
+                                                        0x00020000);
+#pragma unroll
+    for (int k = 0; k < SEG / 16; ++k) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, tid * SEG, k * 16, 0);
+        r.v[k] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+    r.nx = __builtin_amdgcn_raw_buffer_load_b32(rsrc, tid * SEG + SEG, 0, 0);
+}
+
+// the data end: bytes at or past nb read as zero (the range check is trusted only for whole
+// vectors; the partial ones are rebuilt from bytes).  Uniform test, rare.
+__device__ __forceinline__ void seg_fix_tail(const ScanArgs& a, u32 t, SegRegs& r, int tid) {
+    const u64 tile0 = (u64)t * TSTEP;
+    const u32 nb = (u32)min((u64)(TILE + HALO), a.avail - tile0);
+    if (nb >= (u32)(TILE + HALO)) return;
+    const u32 s0 = tid * SEG;
+#pragma unroll
+    for (int k = 0; k < SEG / 16; ++k) {
+        const u32 off = s0 + k * 16;
+        if (off + 16u > nb) {
+            u32 w[4] = {0u, 0u, 0u, 0u};
+            for (u32 q = 0; off + q < nb && q < 16; ++q) w[q >> 2] |= (u32)a.buf[tile0 + off + q] << (8 * (q & 3));
+            r.v[k] = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+    }
+    if (s0 + SEG + 4u > nb) r.nx = s0 + SEG < nb ? (u32)a.buf[tile0 + s0 + SEG] : 0u;
+}
+
+struct SegClass {
+    u64 tmask, sp, col, eol;  // terminators (own bytes), and the parse bitmaps (staged bytes)
+    u32 c, x;                 // popcount(tmask), its inclusive wave scan
+    u32 wtot;                 // the wave's terminators
+    bool hi;                  // a byte >= 0x80 among the own bytes (UTF-8 check after B2)
+};
+
+__device__ __forceinline__ SegClass seg_classify(const ScanArgs& a, u32 t, const SegRegs& r, int tid) {
+    const u64 tile0 = (u64)t * TSTEP;
+    const u32 tlen = (u32)min((u64)TSTEP, a.len - tile0);
+    const u32 nb = (u32)min((u64)(TILE + HALO), a.avail - tile0);
+    const u32 bl = min((u32)TILE, nb);
+    const u32 s0 = tid * SEG;
+    SegClass sc;
+    sc.tmask = 0;
+    sc.sp = sc.col = sc.eol = 0;
+    sc.hi = false;
+    if (s0 < bl) {
+        u32 nl16[4], cr16[4], sp16[4], col16[4];
+        u32 hiw = 0;
+#pragma unroll
+        for (int qv = 0; qv < SEG / 16; ++qv) {
+            const uint4 v = r.v[qv];
+            const u32 c0 = classify4(v.x), c1 = classify4(v.y), c2 = classify4(v.z), c3 = classify4(v.w);
+            nl16[qv] = gather16<0>(c0, c1, c2, c3);
+            cr16[qv] = gather16<1>(c0, c1, c2, c3);
+            sp16[qv] = gather16<2>(c0, c1, c2, c3);
+            col16[qv] = gather16<3>(c0, c1, c2, c3);
+            hiw |= v.x | v.y | v.z | v.w;
+        }
+        auto join = [](const u32 (&g)[4]) {
+            return ((u64)(g[2] | (g[3] << 16)) << 32) | (u64)(g[0] | (g[1] << 16));
+        };
+        const u64 nl = join(nl16), cr = join(cr16);
+        u64 sp = join(sp16), col = join(col16);
+        const u64 nxt = (r.nx & 0xFFu) == (u32)'\n' ? 1ull : 0ull;
+        u64 tm = nl | (cr & ~((nl >> 1) | (nxt << 63)));
+        u64 eol = nl | cr;
+        const u32 bvalid = bl - s0;
+        if (bvalid < SEG) {
+            const u64 vm = (1ull << bvalid) - 1ull;
+            sp &= vm;
+            col &= vm;
+            eol &= vm;
+        }
+        sc.sp = sp;
+        sc.col = col;
+        sc.eol = eol;
+        if (s0 < tlen) {
+            const u32 valid = tlen - s0;
+            if (valid < SEG) tm &= (1ull << valid) - 1ull;
+            sc.tmask = tm;
+            sc.hi = (hiw & 0x80808080u) != 0;  // exact own-byte test happens in seg_utf8
+        }
+    }
+    sc.c = __popcll(sc.tmask);
+    u32 x = 0, wtot = 0;
+#pragma unroll
+    for (int b = 0; b < 7; ++b) {
+        const u64 m = __ballot((sc.c >> b) & 1u);
+        x += (__builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u)) + ((sc.c >> b) & 1u)) << b;
+        wtot += (u32)__popcll(m) << b;
+    }
+    sc.x = x;
+    sc.wtot = wtot;
+    return sc;
+}
+
+// after B1: the segment's bytes and bitmaps into LDS, the wave's terminator count
+__device__ __forceinline__ void seg_store(ScanShared& sh, const SegRegs& r, const SegClass& sc, int tid, int lane,
+                                          int wid) {
+#pragma unroll
+    for (int k = 0; k < SEG / 16; ++k) *(uint4*)(sh.buf + 16 + tid * SEG + k * 16) = r.v[k];
+    sh.bsp[tid] = sc.sp;
+    sh.bcol[tid] = sc.col;
+    sh.beol[tid] = sc.eol;
+    if (lane == 0) sh.wsum[wid] = sc.wtot;
+}
+
+// after B2: the tile's line prefix for this lane (TileCount, as parse_own_headers takes it)
+__device__ __forceinline__ TileCount seg_count(const ScanShared& sh, const SegClass& sc, int wid) {
+    TileCount tc;
+    tc.tmask = sc.tmask;
+    tc.c = sc.c;
+    tc.x = sc.x;
+    u32 wexcl = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < WG / 64; ++w) {
+        const u32 v = sh.wsum[w];
+        wexcl += w < wid ? v : 0u;
+        tot += v;
+    }
+    tc.wexcl = wexcl;
+    tc.tot = tot;
+    return tc;
+}
+
+// after B2, only when the segment holds a byte >= 0x80: exact mask, UTF-8 validation
+__device__ __forceinline__ void seg_utf8(ScanShared& sh, const ScanArgs& a, u32 t, int tid) {
+    const u64 tile0 = (u64)t * TSTEP;
+    const u32 tlen = (u32)min((u64)TSTEP, a.len - tile0);
+    const u32 nb = (u32)min((u64)(TILE + HALO), a.avail - tile0);
+    const u32 s0 = tid * SEG;
+    const u32 valid = min(tlen - s0, (u32)SEG);
+    u64 hi = 0;
+#pragma unroll
+    for (int qv = 0; qv < SEG / 16; ++qv) {
+        const uint4 v = *(const uint4*)(sh.buf + 16 + s0 + qv * 16);
+        const u32 w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) hi |= (u64)hi4(w[k]) << (qv * 16 + k * 4);
+    }
+    if (valid < SEG) hi &= (1ull << valid) - 1ull;
+    if (!hi) return;
+    atomicOr(&sh.flags, 1u);
+    if (!utf8_segment_ok(sh, a, tile0, (int)s0, (int)valid, (int)nb)) atomicOr(&sh.flags, 2u);
+}
+
 // per-phase s_memtime stamps (FR_STAMPS diagnostic builds only)
 #ifdef FR_STAMPS
 #define STAMP(i)                                                   \
@@ -1011,7 +1179,26 @@ __device__ __forceinline__ u64 walk_chunk(ScanShared& sh, const ScanArgs& a, u32
     u64 last_ = __builtin_amdgcn_s_memtime();
 #endif
     u64 lines = 0;
-#if FR_PREFETCH
+#if FR_V5
+    SegRegs r;
+    seg_fetch(a, tb, r, tid);
+    for (u32 t = tb; t < te; ++t) {
+        seg_fix_tail(a, t, r, tid);
+        const SegClass sc = seg_classify(a, t, r, tid);
+        __syncthreads();  // B1: the previous tile's parse is done with the LDS tile
+        seg_store(sh, r, sc, tid, lane, wid);
+        seg_fetch(a, t + 1, r, tid, t + 1 < te);  // lands while this tile is parsed
+        __syncthreads();  // B2
+        STAMP(2);
+        const TileCount tc = seg_count(sh, sc, wid);
+        if (sc.hi) seg_utf8(sh, a, t, tid);
+        if (parse && !uniform_flag(sh.spec_bad) && !(a.ablate & 1u))
+            parse_own_headers(sh, a, t, tc, L0 + lines, tid);
+        STAMP(1);
+        lines += tc.tot;
+    }
+    __syncthreads();  // the LDS tile and bitmaps are free for the caller
+#elif FR_PREFETCH
     TileRegs r;
     tile_fetch(a, tb, r, tid);
     tile_stage(sh, a, tb, r, tid);
@@ -1132,6 +1319,15 @@ __global__ __launch_bounds__(WG, FR_OCC) void chunk_kernel(ScanArgs a) {
         if (c == 0) {
             P = (int)(base_lines & 3ull);
         } else if (a.max_records <= 0 && !empty) {
+#if FR_V5
+            SegRegs r;
+            seg_fetch(a, tb, r, tid);
+            seg_fix_tail(a, tb, r, tid);
+            const SegClass sc = seg_classify(a, tb, r, tid);
+            seg_store(sh, r, sc, tid, lane, wid);
+            sh.bsp[tid] = sc.tmask;  // infer_phase reads the terminator bitmap
+            __syncthreads();
+#else
             TileRegs r;
             tile_fetch(a, tb, r, tid);
             tile_stage(sh, a, tb, r, tid);
@@ -1139,6 +1335,7 @@ __global__ __launch_bounds__(WG, FR_OCC) void chunk_kernel(ScanArgs a) {
             const TileCount tc0 = count_tile(sh, a, tb, tid, lane, wid, false);
             sh.bsp[tid] = tc0.tmask;
             __syncthreads();
+#endif
             if (tid == 0) sh.phase = infer_phase(sh, 0);
             __syncthreads();
             P = sh.phase;

@@ -27,6 +27,7 @@ struct fr_ctx {
     u32 ablate = 0;
     u64* cold = nullptr;
     u32 cold_cap = 8192;
+    uint4* rare = nullptr;
 
     DevState* st = nullptr;
     DevState* h_st = nullptr;      // pinned snapshot
@@ -292,6 +293,7 @@ static int launch_range(fr_ctx* ctx, const u8* dptr, u64 len, u64 avail, int own
     }
     a.cold_cap = ctx->cold_cap;
     a.cold = ctx->cold;
+    a.rare = ctx->rare;
     // workgroups take chunks by ticket; never more than the resident grid (cold lists are per block)
     CK(launch_chunk_scan(a, (int)std::min<u64>(a.num_chunks, G), ctx->stream));
     CK(hipEventRecord(ctx->ev_b[ctx->ev_used], ctx->stream));
@@ -325,6 +327,7 @@ fr_ctx* fr_create(int device, uint64_t chunk_bytes, uint64_t table_slots) {
     if (const char* f = getenv("FR_ABLATE")) ctx->ablate = (u32)atoi(f);
     if (const char* f = getenv("FR_COLD_CAP")) ctx->cold_cap = (u32)std::max(1024, atoi(f));
     if ((e = dalloc(&ctx->cold, 2ull * ctx->cold_cap * (u64)ctx->grid)) != hipSuccess) return bad("cold lists", e);
+    if ((e = dalloc(&ctx->rare, (u64)RARE_RING * (u64)ctx->grid)) != hipSuccess) return bad("rare rings", e);
 
     ctx->chunk_bytes = chunk_bytes ? ((chunk_bytes + TILE - 1) / TILE) * TILE : (256ull << 20);
     if (ctx->chunk_bytes > RANGE_MAX) ctx->chunk_bytes = RANGE_MAX;
@@ -380,7 +383,7 @@ void fr_destroy(fr_ctx* ctx) {
                    ctx->d_keys, ctx->d_counts, ctx->d_first, ctx->d_keys_s, ctx->d_counts_s,
                    ctx->d_first_s, ctx->d_pos, ctx->d_perm, ctx->d_rank, ctx->d_counter, ctx->d_temp, ctx->d_pres_u,
                    ctx->d_pres_f, ctx->d_m1, ctx->d_m2, ctx->d_row, ctx->d_rm2, ctx->d_rrow, ctx->d_cls, ctx->d_rcls,
-                   ctx->d_errw, ctx->d_errf, ctx->d_rcf, ctx->d_rcr, ctx->cold};
+                   ctx->d_errw, ctx->d_errf, ctx->d_rcf, ctx->d_rcr, ctx->cold, ctx->rare};
     for (void* p : dev)
         if (p) (void)hipFree(p);
     if (ctx->h_st) (void)hipHostFree(ctx->h_st);

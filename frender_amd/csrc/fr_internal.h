@@ -33,7 +33,9 @@ constexpr u64 HOST_CHUNK_MAX = 1ull << 30;  // bytes per host-fed launch (pinned
 constexpr u32 SPIN_MAX = 1u << 24;   // look-back spin bound (then FR_ERR_DEVICE)
 constexpr int ORD_SHIFT = 44;        // ordinal = file_tag << 44 | file byte offset
 constexpr int EXO_BUF = 32;          // chunk kernel: exotic records buffered while speculating
-constexpr int PHASE_LINES = 24;      // chunk kernel: lines inspected to guess a chunk's line phase
+constexpr int PHASE_LINES = 24;
+constexpr u32 RARE_RING = 8192;      // chunk kernel: rare events queued per workgroup between drains
+                                     // (<= TILE/4 + 1 headers and WG UTF-8 checks per tile)      // chunk kernel: lines inspected to guess a chunk's line phase
 
 // ---- HBM structures ---------------------------------------------------------------
 struct alignas(32) GSlot {           // open-addressing slot, one 32-B sector
@@ -111,6 +113,7 @@ struct ScanArgs {
     u32 mid_chunks;      // full chunks between the two ramps
     u32 cold_cap;        // chunk kernel: entries of each workgroup's cold list
     u64* cold;           // chunk kernel: cold lists, [grid][cold_cap] x {key, ordinal}
+    uint4* rare;         // chunk kernel: rare-event rings, [grid][RARE_RING] (fr_kernels.hip)
     DevState* st;
     u64* tiles;          // look-back descriptors
     const Table* tab;    // device copy: read where used (rare paths), so the tile loop holds no

@@ -160,7 +160,6 @@ struct alignas(16) LSlot {  // one ds_read_b128 reads key, count and first offse
 };
 
 struct ScanShared {
-    u8 buf[16 + TILE + HALO + 32];   // tile at [16, 16+TILE); +32 zero pad for word reads
     LSlot ls[NS];     // LDS hash table of this workgroup's chunk
     u32 wsum[WG / 64];
     u64 tile_excl;
@@ -169,6 +168,7 @@ struct ScanShared {
     u32 nkeys;        // occupied LDS slots
     u32 created;      // HBM slots this workgroup created (added to n_keys once, at exit)
     u32 flags;
+    u32 rq_tail;      // rare-event ring: events pushed by this workgroup (monotonic)
     // ---- chunk kernel state ----
     u32 buffered;     // LDS-table misses go to this workgroup's cold list (committed later)
     u32 spec;         // speculating on the line phase: exotic records / errors are buffered
@@ -193,6 +193,9 @@ __device__ FR_COLD void direct_insert(ScanShared& sh, const ScanArgs& a, u64 key
     if (global_insert(*a.tab, a.st, key, 1, make_ord(a, off), a.file_tag)) atomicAdd(&sh.created, 1u);
 }
 
+__device__ __forceinline__ void rare_push(ScanShared& sh, const ScanArgs& a, u32 p, u32 kind, u32 x, u32 y);
+
+template <bool DRAIN = false>
 __device__ __forceinline__ void lds_insert(ScanShared& sh, const ScanArgs& a, u64 key, u32 off) {
     // one 32-bit multiply (keys hold <= 63 bits: fold the top down first)
     u32 h = (((u32)key ^ (u32)(key >> 27)) * 0x9E3779B1u) >> (32 - LOG_NS);
@@ -235,9 +238,19 @@ __device__ __forceinline__ void lds_insert(ScanShared& sh, const ScanArgs& a, u6
             atomicOr(&sh.spec_bad, 1u);
             return;
         }
-        // exact phase and a full cold list: insert directly
+        // exact phase and a full cold list: insert directly (queued out of the hot loop)
     }
-    direct_insert(sh, a, key, off);
+    if (DRAIN) direct_insert(sh, a, key, off);
+    else rare_push(sh, a, off, 3u, (u32)key, (u32)(key >> 32));
+}
+
+// Rare events (exotic codes, headers without ' ', headers whose code leaves the bitmap window,
+// direct HBM inserts, UTF-8 checks) go to the workgroup's ring in HBM and are handled by
+// drain_rare between tiles, so their code adds no registers to the tile loop.  Entry: {range
+// offset, kind, x, y}.
+__device__ __forceinline__ void rare_push(ScanShared& sh, const ScanArgs& a, u32 p, u32 kind, u32 x, u32 y) {
+    const u32 i = atomicAdd(&sh.rq_tail, 1u);
+    a.rare[(u64)blockIdx.x * RARE_RING + (i & (RARE_RING - 1u))] = make_uint4(p, kind, x, y);
 }
 
 // Decoupled look-back over the launch's tile descriptors {tag = 2*epoch + inclusive, value}.
@@ -304,11 +317,9 @@ __device__ __forceinline__ u64 lookback(const ScanArgs& a, u32 t, u32 agg, int l
 }
 
 // validate UTF-8 for the bytes [s0, s0+n) of the tile (only called when a byte >= 0x80
-// is present).  Bytes inside the staged tile come from LDS, others (before the tile or past
-// the staged bytes) from HBM when readable, -1 otherwise.
-__device__ FR_COLD bool utf8_segment_ok(const ScanShared& sh, const ScanArgs& a, u64 tile0, int s0, int n, int nb) {
+// is present); bytes are read from HBM (the range, and before it when readable), -1 past them.
+__device__ FR_COLD bool utf8_segment_ok(const ScanArgs& a, u64 tile0, int s0, int n) {
     auto byte_at = [&](int q) -> int {
-        if (q >= 0 && q < nb) return (int)sh.buf[16 + q];
         const i64 g = (i64)tile0 + q;
         if (q < 0 && g < 0 && !a.pre_valid) return -1;
         if (g >= (i64)a.avail) return -1;
@@ -349,15 +360,16 @@ __device__ FR_COLD bool utf8_segment_ok(const ScanShared& sh, const ScanArgs& a,
     return true;
 }
 
+template <bool DRAIN = false>
 __device__ __forceinline__ void count_code(ScanShared& sh, const ScanArgs& a, u64 tile0, u32 p, u64 key) {
     if (a.ablate & 4u) {  // ablation: skip the hash insert (keep the key live)
         asm volatile("" ::"v"(key));
         return;
     }
-    lds_insert(sh, a, key, (u32)(tile0 + p));
+    lds_insert<DRAIN>(sh, a, key, (u32)(tile0 + p));
 }
 
-__device__ void exotic_record(const ScanArgs& a, u64 tile0, u32 p, u64 start, u64 n, ScanShared& sh, u32 nb) {
+__device__ void exotic_record(const ScanArgs& a, u64 tile0, u32 p, u64 start, u64 n, ScanShared& sh) {
     if (sh.spec) {  // speculating: remember where it is; the bytes stay resident in HBM
         const u32 k = atomicAdd(&sh.nexo, 1u);
         if (k < (u32)EXO_BUF) {
@@ -377,7 +389,7 @@ __device__ void exotic_record(const ScanArgs& a, u64 tile0, u32 p, u64 start, u6
         a.tab->exo_len[i] = (u32)n;
         for (u64 k = 0; k < n; ++k) {
             const u64 q = start + k;
-            a.tab->exo_pool[po + k] = q < nb ? sh.buf[16 + q] : a.buf[tile0 + q];
+            a.tab->exo_pool[po + k] = a.buf[tile0 + q];
         }
     } else {
         atomicOr(&a.st->cap_flags, 4u);
@@ -389,27 +401,12 @@ __device__ __forceinline__ void nospace(const ScanArgs& a, u64 tile0, u32 p, Sca
     else atomicMin((unsigned long long*)&a.st->err_nospace, (unsigned long long)(a.file_offset + tile0 + p));
 }
 
-// code bytes [start, start+n) -> fast key (false if outside the fast alphabet)
-__device__ __forceinline__ bool encode_lds(const u8* lb, u32 start, u32 n, u64& key) {
-    if (n < 1 || n > (u32)MAXSYM) return false;
-    u64 k = 0;
-    u32 bad = 0;
-#pragma unroll
-    for (int i = 0; i < MAXSYM; ++i) {  // independent LDS reads (buffer padded past the halo)
-        const u32 c = lb[start + i];
-        const u32 sy = sym_of(c);
-        const bool in = (u32)i < n;
-        bad |= in && sy == 0;
-        k |= (u64)(in ? sy : 0u) << (3 * i);
-    }
-    key = k;
-    return !bad;
-}
-
-// slow path: a header that runs past the LDS halo, read through global memory (rare)
-__device__ void process_header_global(ScanShared& sh, const ScanArgs& a, u64 tile0, u32 p, u32 nb) {
+// slow path (rare): a header whose code does not end inside its 128-bit bitmap window, parsed
+// byte by byte from HBM.  R2 (frender.py:169): the token after the first ' ' up to the next ' '
+// or line end, then its suffix after the last ':'.
+__device__ FR_COLD void process_header_global(ScanShared& sh, const ScanArgs& a, u64 tile0, u32 p) {
     const u64 eof = a.avail - tile0;
-    auto rd = [&](u64 q) -> u32 { return q < nb ? (u32)sh.buf[16 + q] : (u32)a.buf[tile0 + q]; };
+    auto rd = [&](u64 q) -> u32 { return (u32)a.buf[tile0 + q]; };
     u64 q = p;
     for (;;) {
         if (q >= eof) return nospace(a, tile0, p, sh);
@@ -436,117 +433,8 @@ __device__ void process_header_global(ScanShared& sh, const ScanArgs& a, u64 til
         fast = sy != 0;
         key |= (u64)sy << (3 * i);
     }
-    if (fast) count_code(sh, a, tile0, p, key);
-    else exotic_record(a, tile0, p, start, n, sh, nb);
-}
-
-// R2 (frender.py:169): the token after the first ' ' up to the next ' ' or line end, then
-// its suffix after the last ':'.  Word-at-a-time SWAR over the LDS tile; bytes past the
-// end of the data read as zero and count as the line end.
-__device__ void process_header(ScanShared& sh, const ScanArgs& a, u64 tile0, u32 p, u32 nb) {
-    const u8* lb = sh.buf + 16;
-    const bool at_eof = (u64)nb >= a.avail - tile0;
-    u32 q = p & ~3u;
-    u32 fm = (0xFu << (p & 3u)) & 0xFu;
-    int sp1 = -1, lastc = -1, end = -1;
-    for (;;) {
-        u32 beyond = 0;
-        if (q + 4 > nb) {
-            if (!at_eof) return process_header_global(sh, a, tile0, p, nb);
-            beyond = q >= nb ? 0xFu : (0xFu << (nb - q)) & 0xFu;
-        }
-        const u32 w = *(const u32*)(lb + q);
-        u32 sp = eq4(w, 0x20202020u) & fm;
-        u32 eol = (eq4(w, 0x0A0A0A0Au) | eq4(w, 0x0D0D0D0Du) | beyond) & fm;
-        u32 col = eq4(w, 0x3A3A3A3Au) & fm;
-        fm = 0xFu;
-        if (sp1 < 0) {
-            const u32 ev = sp | eol;
-            if (!ev) {
-                q += 4;
-                continue;
-            }
-            const u32 b = __builtin_ctz(ev);
-            if ((eol >> b) & 1u) return nospace(a, tile0, p, sh);
-            sp1 = (int)(q + b);
-            const u32 keep = ~((2u << b) - 1u) & 0xFu;
-            sp &= keep;
-            eol &= keep;
-            col &= keep;
-        }
-        const u32 ev = sp | eol;
-        if (ev) {
-            const u32 b = __builtin_ctz(ev);
-            const u32 cm = col & ((1u << b) - 1u);
-            if (cm) lastc = (int)(q + 31u - __builtin_clz(cm));
-            end = (int)(q + b);
-            break;
-        }
-        if (col) lastc = (int)(q + 31u - __builtin_clz(col));
-        q += 4;
-    }
-    const u32 start = (u32)((lastc > sp1 ? lastc : sp1) + 1);
-    const u32 n = (u32)end - start;
-    if (a.ablate & 2u) {  // ablation: skip the code encode
-        asm volatile("" ::"v"(start), "v"(n));
-        return;
-    }
-    u64 key;
-    if (encode_lds(lb, start, n, key)) count_code(sh, a, tile0, p, key);
-    else exotic_record(a, tile0, p, start, n, sh, nb);
-}
-
-// ---- tile staging: 16-B loads into registers (prefetch), then registers -> LDS ----------
-#ifndef FR_PREFETCH
-#define FR_PREFETCH 1
-#endif
-constexpr int STAGE_VECS = (TILE + HALO + WG * 16 - 1) / (WG * 16);  // 4
-
-struct TileRegs {
-    uint4 v[STAGE_VECS];
-};
-
-// Prefetch: unconditional 16-B loads whose results are not touched until tile_stage, so the
-// loads stay in flight through the parse of the current tile (any select or branch on a loaded
-// value makes the compiler wait for it at once).  Addresses are clamped into the readable
-// range; tile_stage zeroes / re-reads the few vectors at the data end.
-// Branch-free: with want == false (or t past the range) the descriptors hold zero records, so
-// the loads return zeros without touching memory; the caller never branches around a fetch
-// (a conditional fetch makes the compiler copy and wait for the loaded registers at once).
-__device__ __forceinline__ void tile_fetch(const ScanArgs& a, u32 t, TileRegs& r, int tid, bool want = true) {
-    const bool live = want && t < a.num_tiles;
-    const u64 tile0 = live ? (u64)t * TSTEP : 0ull;
-    const u32 nb = live ? (u32)min((u64)(TILE + HALO), a.avail - tile0) : 0u;
-    // wave-uniform buffer descriptors over [tile0, tile0 + nb) and the 16 bytes before the tile:
-    // 32-bit lane offsets (one VGPR for all five loads), hardware range check past the end
-    const u64 base = (u64)(a.buf + tile0);
-    const u32 lo = __builtin_amdgcn_readfirstlane((u32)base), hi = __builtin_amdgcn_readfirstlane((u32)(base >> 32));
-    const u8* ub = (const u8*)(((u64)hi << 32) | lo);
-    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)ub, (short)0, (int)__builtin_amdgcn_readfirstlane(nb),
-                                                        0x00020000);
-#pragma unroll
-    for (int k = 0; k < STAGE_VECS; ++k) {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, tid * 16, k * WG * 16, 0);
-        r.v[k] = make_uint4(v[0], v[1], v[2], v[3]);
-    }
-}
-
-__device__ __forceinline__ void tile_stage(ScanShared& sh, const ScanArgs& a, u32 t, const TileRegs& r, int tid) {
-    const u64 tile0 = (u64)t * TSTEP;
-    const u32 nb = (u32)min((u64)(TILE + HALO), a.avail - tile0);
-#pragma unroll
-    for (int k = 0; k < STAGE_VECS; ++k) {
-        const u32 off = tid * 16 + k * WG * 16;
-        if (off < (u32)(TILE + HALO)) {
-            uint4 v = r.v[k];
-            if (off + 16u > nb) {  // the data end: bytes past it read as zero (rare, synchronous)
-                u32 w[4] = {0u, 0u, 0u, 0u};
-                for (u32 q = 0; off + q < nb; ++q) w[q >> 2] |= (u32)a.buf[tile0 + off + q] << (8 * (q & 3));
-                v = make_uint4(w[0], w[1], w[2], w[3]);
-            }
-            *(uint4*)(sh.buf + 16 + off) = v;
-        }
-    }
+    if (fast) count_code<true>(sh, a, tile0, p, key);
+    else exotic_record(a, tile0, p, start, n, sh);
 }
 
 struct TileCount {
@@ -557,116 +445,13 @@ struct TileCount {
     u32 tot;    // terminators in the tile
 };
 
-// line-terminator bitmap of the staged tile t, block scan, and publication of its aggregate
-// (R1: universal newlines: '\n', '\r\n' and a lone '\r' each end one line)
-__device__ __forceinline__ TileCount count_tile(ScanShared& sh, const ScanArgs& a, u32 t, int tid, int lane, int wid,
-                                bool publish = true) {
-    const u64 tile0 = (u64)t * TSTEP;
-    const u32 tlen = (u32)min((u64)TSTEP, a.len - tile0);   // this tile's own bytes
-    const u32 nb = (u32)min((u64)(TILE + HALO), a.avail - tile0);
-    const u32 bl = min((u32)TILE, nb);                        // bytes with bitmaps
-    const u32 s0 = tid * SEG;
-    TileCount tc;
-    tc.tmask = 0;
-    if (s0 >= bl) {
-        sh.bsp[tid] = 0;
-        sh.bcol[tid] = 0;
-        sh.beol[tid] = 0;
-    } else {  // bitmaps for every staged segment; terminators / UTF-8 only for the tile's own bytes
-        u32 nl16[4], cr16[4], sp16[4], col16[4];
-        u32 hiw = 0;
-#pragma unroll
-        for (int qv = 0; qv < SEG / 16; ++qv) {
-            const uint4 v = *(const uint4*)(sh.buf + 16 + s0 + qv * 16);
-            const u32 c0 = classify4(v.x), c1 = classify4(v.y), c2 = classify4(v.z), c3 = classify4(v.w);
-            nl16[qv] = gather16<0>(c0, c1, c2, c3);
-            cr16[qv] = gather16<1>(c0, c1, c2, c3);
-            sp16[qv] = gather16<2>(c0, c1, c2, c3);
-            col16[qv] = gather16<3>(c0, c1, c2, c3);
-            hiw |= v.x | v.y | v.z | v.w;
-        }
-        auto join = [](const u32 (&g)[4]) {
-            return ((u64)(g[2] | (g[3] << 16)) << 32) | (u64)(g[0] | (g[1] << 16));
-        };
-        const u64 nl = join(nl16), cr = join(cr16);
-        u64 sp = join(sp16), col = join(col16);
-        const u64 nxt = (s0 + SEG < nb && sh.buf[16 + s0 + SEG] == '\n') ? 1ull : 0ull;
-        u64 tm = nl | (cr & ~((nl >> 1) | (nxt << 63)));
-        u64 eol = nl | cr;
-        const u32 bvalid = bl - s0;
-        if (bvalid < SEG) {
-            const u64 vm = (1ull << bvalid) - 1ull;
-            sp &= vm;
-            col &= vm;
-            eol &= vm;
-        }
-        sh.bsp[tid] = sp;
-        sh.bcol[tid] = col;
-        sh.beol[tid] = eol;
-        if (s0 < tlen) {
-            const u32 valid = tlen - s0;
-            u64 hi = 0;
-            if (hiw & 0x80808080u) {  // rare: exact per-byte high-bit mask for the UTF-8 check
-#pragma unroll
-                for (int qv = 0; qv < SEG / 16; ++qv) {
-                    const uint4 v = *(const uint4*)(sh.buf + 16 + s0 + qv * 16);
-                    const u32 w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) hi |= (u64)hi4(w[k]) << (qv * 16 + k * 4);
-                }
-            }
-            if (valid < SEG) {
-                const u64 vm = (1ull << valid) - 1ull;
-                tm &= vm;
-                hi &= vm;
-            }
-            tc.tmask = tm;
-            if (hi) {
-                atomicOr(&sh.flags, 1u);
-                if (!utf8_segment_ok(sh, a, tile0, (int)s0, (int)min(valid, (u32)SEG), (int)nb))
-                    atomicOr(&sh.flags, 2u);
-            }
-        }
-    }
-    tc.c = __popcll(tc.tmask);
-    // inclusive wave scan of c (<= 64, 7 bits) without LDS round trips: bit-sliced ballots,
-    // each lane counting the set bits of the lanes at or below it (v_mbcnt)
-    u32 x = 0, wtot = 0;
-#pragma unroll
-    for (int b = 0; b < 7; ++b) {
-        const u64 m = __ballot((tc.c >> b) & 1u);
-        x += (__builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u)) +
-              ((tc.c >> b) & 1u)) << b;
-        wtot += (u32)__popcll(m) << b;
-    }
-    tc.x = x;
-    if (lane == 0) sh.wsum[wid] = wtot;
-    __syncthreads();
-    u32 wexcl = 0, tot = 0;
-#pragma unroll
-    for (int w = 0; w < WG / 64; ++w) {
-        const u32 v = sh.wsum[w];
-        wexcl += w < wid ? v : 0u;
-        tot += v;
-    }
-    tc.wexcl = wexcl;
-    tc.tot = tot;
-    if (publish && tid == 0) {  // publish: tile 0 is inclusive at once, every other tile its aggregate
-        const u64 tag = (u64)(2u * a.epoch + (t == 0 ? 1u : 0u)) << 32;
-        agent_store(&a.tiles[t], tag | tot);
-    }
-    return tc;
-}
-
-// ---- v5 staging: lane-contiguous segments classified straight from registers ---------
+// ---- tile staging: lane-contiguous segments classified straight from registers ---------
 // Lane tid loads its own 64-byte segment [tid*64, tid*64+64) of the tile (four 16-B loads) plus
-// the first dword of the next segment (a '\r' ending the segment needs the byte after it), so the
-// byte classification runs on the loaded registers: no LDS read-back, and two barriers per tile
-// (B1: the previous tile's parse is done with the LDS tile; B2: this tile's bytes, bitmaps and
-// wave sums are in LDS).
-#ifndef FR_V5
-#define FR_V5 1
-#endif
+// the first dword of the next segment (a '\r' ending the segment needs the byte after it) and
+// classifies it in registers.  Only the ' ' / ':' / line-end bitmaps go to LDS; the raw bytes
+// never do (code bytes are re-read from L2 by the parse), which keeps a workgroup's LDS at
+// ~22 KB so that 7 workgroups share a CU.  Two barriers per tile: B1 (the previous tile's
+// parse is done with the bitmaps) and B2 (this tile's bitmaps and wave sums are in LDS).
 struct SegRegs {
     uint4 v[SEG / 16];
     u32 nx;  // first dword of the next segment (zero past the staged bytes)
@@ -689,23 +474,25 @@ __device__ __forceinline__ void seg_fetch(const ScanArgs& a, u32 t, SegRegs& r, 
     r.nx = __builtin_amdgcn_raw_buffer_load_b32(rsrc, tid * SEG + SEG, 0, 0);
 }
 
-// the data end: bytes at or past nb read as zero (the range check is trusted only for whole
-// vectors; the partial ones are rebuilt from bytes).  Uniform test, rare.
-__device__ __forceinline__ void seg_fix_tail(const ScanArgs& a, u32 t, SegRegs& r, int tid) {
+// the data end (a segment, or the dword after it, reaches past avail): bytewise loads, zeros past
+// the staged bytes (the buffer range check is trusted only for whole vectors)
+__device__ __attribute__((noinline)) SegRegs seg_load_tail(const ScanArgs& a, u32 t, int tid) {
     const u64 tile0 = (u64)t * TSTEP;
     const u32 nb = (u32)min((u64)(TILE + HALO), a.avail - tile0);
-    if (nb >= (u32)(TILE + HALO)) return;
     const u32 s0 = tid * SEG;
-#pragma unroll
-    for (int k = 0; k < SEG / 16; ++k) {
-        const u32 off = s0 + k * 16;
-        if (off + 16u > nb) {
-            u32 w[4] = {0u, 0u, 0u, 0u};
-            for (u32 q = 0; off + q < nb && q < 16; ++q) w[q >> 2] |= (u32)a.buf[tile0 + off + q] << (8 * (q & 3));
-            r.v[k] = make_uint4(w[0], w[1], w[2], w[3]);
+    u32 w[SEG / 4 + 1];
+    for (int k = 0; k <= SEG / 4; ++k) {
+        u32 v = 0;
+        for (u32 q = 0; q < 4; ++q) {
+            const u32 o = s0 + 4 * k + q;
+            if (o < nb) v |= (u32)a.buf[tile0 + o] << (8 * q);
         }
+        w[k] = v;
     }
-    if (s0 + SEG + 4u > nb) r.nx = s0 + SEG < nb ? (u32)a.buf[tile0 + s0 + SEG] : 0u;
+    SegRegs r;
+    for (int k = 0; k < SEG / 16; ++k) r.v[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+    r.nx = w[SEG / 4];
+    return r;
 }
 
 struct SegClass {
@@ -760,7 +547,7 @@ __device__ __forceinline__ SegClass seg_classify(const ScanArgs& a, u32 t, const
             const u32 valid = tlen - s0;
             if (valid < SEG) tm &= (1ull << valid) - 1ull;
             sc.tmask = tm;
-            sc.hi = (hiw & 0x80808080u) != 0;  // exact own-byte test happens in seg_utf8
+            sc.hi = (hiw & 0x80808080u) != 0;  // exact own-byte test in drain_rare (kind 4)
         }
     }
     sc.c = __popcll(sc.tmask);
@@ -776,11 +563,8 @@ __device__ __forceinline__ SegClass seg_classify(const ScanArgs& a, u32 t, const
     return sc;
 }
 
-// after B1: the segment's bytes and bitmaps into LDS, the wave's terminator count
-__device__ __forceinline__ void seg_store(ScanShared& sh, const SegRegs& r, const SegClass& sc, int tid, int lane,
-                                          int wid) {
-#pragma unroll
-    for (int k = 0; k < SEG / 16; ++k) *(uint4*)(sh.buf + 16 + tid * SEG + k * 16) = r.v[k];
+// after B1: the segment's bitmaps into LDS, the wave's terminator count
+__device__ __forceinline__ void seg_store(ScanShared& sh, const SegClass& sc, int tid, int lane, int wid) {
     sh.bsp[tid] = sc.sp;
     sh.bcol[tid] = sc.col;
     sh.beol[tid] = sc.eol;
@@ -805,42 +589,44 @@ __device__ __forceinline__ TileCount seg_count(const ScanShared& sh, const SegCl
     return tc;
 }
 
-// after B2, only when the segment holds a byte >= 0x80: exact mask, UTF-8 validation
-__device__ __forceinline__ void seg_utf8(ScanShared& sh, const ScanArgs& a, u32 t, int tid) {
-    const u64 tile0 = (u64)t * TSTEP;
-    const u32 tlen = (u32)min((u64)TSTEP, a.len - tile0);
-    const u32 nb = (u32)min((u64)(TILE + HALO), a.avail - tile0);
-    const u32 s0 = tid * SEG;
-    const u32 valid = min(tlen - s0, (u32)SEG);
-    u64 hi = 0;
-#pragma unroll
-    for (int qv = 0; qv < SEG / 16; ++qv) {
-        const uint4 v = *(const uint4*)(sh.buf + 16 + s0 + qv * 16);
-        const u32 w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) hi |= (u64)hi4(w[k]) << (qv * 16 + k * 4);
+__device__ FR_COLD void slow_header(ScanShared& sh, const ScanArgs& a, u64 tile0, u32 p, int r, u32 start, u32 n);
+
+// handle the ring entries [from, to) (all threads; between B1 and B2 nothing is pushed)
+__device__ __attribute__((noinline)) void drain_rare(ScanShared& sh, const ScanArgs& a, u32 from, u32 to, int tid) {
+    const uint4* q = a.rare + (u64)blockIdx.x * RARE_RING;
+    for (u32 i = from + tid; i - from < to - from; i += WG) {
+        const uint4 e = q[i & (RARE_RING - 1u)];
+        if (e.y == 3u) {
+            direct_insert(sh, a, ((u64)e.w << 32) | e.z, e.x);
+        } else if (e.y == 4u) {  // UTF-8: the segment's own bytes [e.x, e.x + e.z)
+            bool hi = false;
+            for (u32 k = 0; k < e.z; ++k) hi |= a.buf[e.x + k] >= 0x80;
+            if (hi) {
+                atomicOr(&sh.flags, 1u);
+                if (!utf8_segment_ok(a, 0, (int)e.x, (int)e.z)) atomicOr(&sh.flags, 2u);
+            }
+        } else {
+            slow_header(sh, a, 0, e.x, (int)e.y, e.z, e.w);
+        }
     }
-    if (valid < SEG) hi &= (1ull << valid) - 1ull;
-    if (!hi) return;
-    atomicOr(&sh.flags, 1u);
-    if (!utf8_segment_ok(sh, a, tile0, (int)s0, (int)valid, (int)nb)) atomicOr(&sh.flags, 2u);
 }
 
-// per-phase s_memtime stamps (FR_STAMPS diagnostic builds only)
-#ifdef FR_STAMPS
-#define STAMP(i)                                                   \
-    do {                                                           \
-        __builtin_amdgcn_sched_barrier(0);                         \
-        const u64 now_ = __builtin_amdgcn_s_memtime();             \
-        __builtin_amdgcn_sched_barrier(0);                         \
-        if (tid == 0) stamps[i] += now_ - last_;                   \
-        last_ = now_;                                              \
-    } while (0)
-#else
-#define STAMP(i) \
-    do {         \
-    } while (0)
-#endif
+// phase inference bitmaps of a chunk's first tile: '@' and '+' (first bytes of header / separator
+// lines); exact per-byte equality, once per chunk
+__device__ __forceinline__ void seg_marks(const SegRegs& r, u64& at, u64& plus) {
+    at = 0;
+    plus = 0;
+#pragma unroll
+    for (int qv = 0; qv < SEG / 16; ++qv) {
+        const u32 w[4] = {r.v[qv].x, r.v[qv].y, r.v[qv].z, r.v[qv].w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            at |= (u64)eq4(w[k], 0x40404040u) << (qv * 16 + k * 4);
+            plus |= (u64)eq4(w[k], 0x2B2B2B2Bu) << (qv * 16 + k * 4);
+        }
+    }
+}
+
 
 // =====================================================================================
 // chunk kernel (v3): a workgroup owns a contiguous chunk of tiles and walks it in order, so
@@ -855,8 +641,9 @@ __device__ __forceinline__ void seg_utf8(ScanShared& sh, const ScanArgs& a, u32 
 // staged first tile: with lines indexed P+k+1 after the k-th terminator, a FASTQ record has a
 // header ('@') at phase 0, '+' at phase 2 and equal seq/qual lengths at phases 1/3.  Exactly
 // one consistent P -> the guess; otherwise -1 (unsure).  One lane, once per chunk.
-__device__ __forceinline__ int infer_phase(const ScanShared& sh, u32 tlen) {
-    const u8* lb = sh.buf + 16;
+// Bitmaps (staged by the caller): bsp = line terminators, bcol = '@', beol = '+'.  Line lengths
+// include a '\r' of "\r\n" (equal on both lines of a consistently terminated record).
+__device__ __forceinline__ int infer_phase(const ScanShared& sh) {
     bool ok[4] = {true, true, true, true};
     int seqlen[4] = {-1, -1, -1, -1};
     int prev = -1, k = 0;
@@ -865,17 +652,16 @@ __device__ __forceinline__ int infer_phase(const ScanShared& sh, u32 tlen) {
         while (m && k < PHASE_LINES) {
             const int e = w * SEG + (__ffsll((long long)m) - 1);
             m &= m - 1;
-            if (prev >= 0) {  // the line [prev+1, e) (less a '\r' of "\r\n")
+            if (prev >= 0) {  // the line [prev+1, e)
                 const int st = prev + 1;
-                int en = e;
-                if (lb[e] == '\n' && e - 1 >= st && lb[e - 1] == '\r') en = e - 1;
-                const int len = en - st;
-                const u32 c0 = len > 0 ? lb[st] : 0u;
+                const int len = e - st;
+                const bool is_at = len > 0 && ((sh.bcol[st >> 6] >> (st & 63)) & 1ull);
+                const bool is_plus = len > 0 && ((sh.beol[st >> 6] >> (st & 63)) & 1ull);
 #pragma unroll
                 for (int P = 0; P < 4; ++P) {
                     const int ph = (P + k + 1) & 3;
-                    if (ph == 0) ok[P] &= c0 == '@';
-                    else if (ph == 2) ok[P] &= c0 == '+';
+                    if (ph == 0) ok[P] &= is_at;
+                    else if (ph == 2) ok[P] &= is_plus;
                     else if (ph == 1) seqlen[P] = len;
                     else {
                         if (seqlen[P] >= 0) ok[P] &= seqlen[P] == len;
@@ -887,7 +673,6 @@ __device__ __forceinline__ int infer_phase(const ScanShared& sh, u32 tlen) {
             prev = e;
         }
     }
-    (void)tlen;
     if (k < 8) return -1;
     int found = -1, nfound = 0;
 #pragma unroll
@@ -939,7 +724,7 @@ __device__ __forceinline__ u32 insert_many(const ScanArgs& a, const u64 (&key)[B
 #define FR_CB 4
 #endif
 constexpr int CB = FR_CB;
-__device__ __forceinline__ void commit_buffers(ScanShared& sh, const ScanArgs& a, bool table, int tid) {
+__device__ __attribute__((noinline)) void commit_buffers(ScanShared& sh, const ScanArgs& a, bool table, int tid) {
     __syncthreads();
     u32 made = 0;
     if (a.ablate & 64u) {  // diag: flushed LDS slots and cold entries per commit
@@ -1031,27 +816,35 @@ __device__ __forceinline__ void discard_buffers(ScanShared& sh, int tid) {
 
 __device__ __forceinline__ bool uniform_flag(u32 v) { return __builtin_amdgcn_readfirstlane(v) != 0; }
 
-// code bytes [start, start+n) -> fast key with v_perm SWAR, 4 bytes per step (false if outside
-// the fast alphabet).  Byte index i = (c >> 1) & 7 selects the expected byte (A C T G - + - N)
-// and its symbol (A1 C2 G3 T4 N5 +6); a byte is valid iff it equals the expected one.
-__device__ __forceinline__ bool encode_perm(const u8* lb, u32 start, u32 n, u64& key) {
+// code bytes [start, start+n) of the tile -> fast key with v_perm SWAR, 4 bytes per step (false
+// if outside the fast alphabet).  The bytes come from HBM/L2 through a range-checked buffer
+// descriptor over [tile0, avail) (zeros past the data: such codes fail here and take the exotic
+// path, which reads them exactly).  Byte index i = (c >> 1) & 7 selects the expected byte
+// (A C T G - + - N) and its symbol (A1 C2 G3 T4 N5 +6); a byte is valid iff it equals the
+// expected one.
+__device__ __forceinline__ bool encode_glob(const ScanArgs& a, u64 tile0, u32 start, u32 n, u64& key) {
     if (n < 1 || n > (u32)MAXSYM) return false;
+    const u64 base = (u64)(a.buf + tile0);
+    const u32 lo = __builtin_amdgcn_readfirstlane((u32)base), hi = __builtin_amdgcn_readfirstlane((u32)(base >> 32));
+    const u32 nrec = (u32)min(a.avail - tile0, (u64)0xFFFFFFF0u);
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(((u64)hi << 32) | lo), (short)0,
+                                                        (int)__builtin_amdgcn_readfirstlane(nrec), 0x00020000);
     const u32 b4 = start & ~3u;
     const u32 sh8 = (start & 3u) * 8u;
-    u32 w[7];
-#pragma unroll
-    for (int k = 0; k < 7; ++k) w[k] = *(const u32*)(lb + b4 + 4 * k);
+    const auto v0 = __builtin_amdgcn_raw_buffer_load_b128(rsrc, b4, 0, 0);
+    const auto v1 = __builtin_amdgcn_raw_buffer_load_b128(rsrc, b4, 16, 0);
+    const u32 w[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
     u64 kk = 0;
     u32 bad = 0;
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
-        const u32 a = sh8 ? (u32)((((u64)w[k + 1] << 32) | w[k]) >> sh8) : w[k];
-        const u32 idx = (a >> 1) & 0x07070707u;
+        const u32 x = (u32)((((u64)w[k + 1] << 32) | w[k]) >> sh8);
+        const u32 idx = (x >> 1) & 0x07070707u;
         const u32 expect = __builtin_amdgcn_perm(0x4E002B00u, 0x47544341u, idx);
         const u32 sym = __builtin_amdgcn_perm(0x05000600u, 0x03040201u, idx);
         const int left = (int)n - 4 * k;  // bytes of the code in this word
         const u32 vm = left >= 4 ? 0xFFFFFFFFu : left <= 0 ? 0u : (0xFFFFFFFFu >> (32 - 8 * left));
-        bad |= (expect ^ a) & vm;
+        bad |= (expect ^ x) & vm;
         const u32 sv = sym & vm;
         const u32 packed = (sv & 0x7u) | ((sv >> 5) & 0x38u) | ((sv >> 10) & 0x1C0u) | ((sv >> 15) & 0xE00u);
         kk |= (u64)packed << (12 * k);
@@ -1061,11 +854,10 @@ __device__ __forceinline__ bool encode_perm(const u8* lb, u32 start, u32 n, u64&
 }
 
 // the rare header outcomes: word-scan fallback, no ' ' (IndexError), or an exotic code
-__device__ FR_COLD void slow_header(ScanShared& sh, const ScanArgs& a, u64 tile0, u32 p, u32 nb, int r,
-                                         u32 start, u32 n) {
-    if (r == 2) process_header(sh, a, tile0, p, nb);
+__device__ FR_COLD void slow_header(ScanShared& sh, const ScanArgs& a, u64 tile0, u32 p, int r, u32 start, u32 n) {
+    if (r == 2) process_header_global(sh, a, tile0, p);
     else if (r == 1) nospace(a, tile0, p, sh);
-    else exotic_record(a, tile0, p, start, n, sh, nb);
+    else exotic_record(a, tile0, p, start, n, sh);
 }
 
 // bits [0, k) of a 128-bit window (k in [0, 128])
@@ -1112,10 +904,9 @@ __device__ __forceinline__ int locate_code_bm(const ScanShared& sh, u32 p, u32 b
 // R2 via the tile's ' ' / ':' / line-end bitmaps: first ' ', then the next ' ' or line end,
 // then the last ':' between them.  Lines that reach past the tile's bitmaps fall back to the
 // word-scan parser (process_header).
-__device__ __forceinline__ void process_header_bm(ScanShared& sh, const ScanArgs& a, u64 tile0, u32 p, u32 bl,
-                                                  u32 nb) {
+__device__ __forceinline__ void process_header_bm(ScanShared& sh, const ScanArgs& a, u64 tile0, u32 p, u32 bl) {
     u32 start = 0, n = 0;
-    const int r = locate_code_bm(sh, p, bl, start, n);
+    int r = locate_code_bm(sh, p, bl, start, n);
     u64 key = 0;
     bool fast = false;
     if (r == 0) {
@@ -1123,16 +914,16 @@ __device__ __forceinline__ void process_header_bm(ScanShared& sh, const ScanArgs
             asm volatile("" ::"v"(start), "v"(n));
             return;
         }
-        fast = encode_perm(sh.buf + 16, start, n, key);
+        if ((u64)(start & ~3u) + 32u > a.avail - tile0) r = 2;  // the loads would straddle the data end
+        else fast = encode_glob(a, tile0, start, n, key);
     }
-    if (a.ablate & 64u) atomicAdd((unsigned long long*)&a.st->stamp[fast ? 3 : r], 1ull);  // diag: outcome counts
     if (fast) count_code(sh, a, tile0, p, key);
-    else slow_header(sh, a, tile0, p, nb, r, start, n);
+    else rare_push(sh, a, (u32)(tile0 + p), (u32)r, (u32)(tile0 + start), n);
 }
 
 // Every 4th line start whose terminator lies in this lane's 64-B segment is a header owned by
 // this lane (the range's first byte by lane 0 of its first tile): parse it where it lies.  No
-// header list, no block scan: the tile's line prefix (count_tile) gives each lane its index.
+// header list, no block scan: the tile's line prefix (seg_count) gives each lane its index.
 __device__ __forceinline__ void parse_own_headers(ScanShared& sh, const ScanArgs& a, u32 t, const TileCount& tc,
                                                   u64 L0, int tid) {
     const u64 tile0 = (u64)t * TSTEP;
@@ -1163,7 +954,7 @@ __device__ __forceinline__ void parse_own_headers(ScanShared& sh, const ScanArgs
             rec += 1;
             pend = (int)p;
         }
-        process_header_bm(sh, a, tile0, (u32)pend, min((u32)TILE, nb), nb);
+        process_header_bm(sh, a, tile0, (u32)pend, min((u32)TILE, nb));
         pend = -1;
     }
 }
@@ -1174,77 +965,32 @@ __device__ __forceinline__ void parse_own_headers(ScanShared& sh, const ScanArgs
 // Returns the line terminators in [tb, te).
 __device__ __forceinline__ u64 walk_chunk(ScanShared& sh, const ScanArgs& a, u32 tb, u32 te, u64 L0, bool parse, bool exact, int tid,
                           int lane, int wid) {
-#ifdef FR_STAMPS
-    u64 stamps[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    u64 last_ = __builtin_amdgcn_s_memtime();
-#endif
     u64 lines = 0;
-#if FR_V5
-    SegRegs r;
-    seg_fetch(a, tb, r, tid);
+    u32 done = sh.rq_tail;  // the caller synchronised: every thread reads the same value
     for (u32 t = tb; t < te; ++t) {
-        seg_fix_tail(a, t, r, tid);
+        SegRegs r;
+        if ((u64)t * TSTEP + (TILE + HALO + SEG + 4) <= a.avail) seg_fetch(a, t, r, tid);
+        else r = seg_load_tail(a, t, tid);  // the data end: bytewise, zeros past it
         const SegClass sc = seg_classify(a, t, r, tid);
-        __syncthreads();  // B1: the previous tile's parse is done with the LDS tile
-        seg_store(sh, r, sc, tid, lane, wid);
-        seg_fetch(a, t + 1, r, tid, t + 1 < te);  // lands while this tile is parsed
+        if (sc.hi) rare_push(sh, a, (u32)((u64)t * TSTEP) + tid * SEG, 4u,
+                             min((u32)min((u64)TSTEP, a.len - (u64)t * TSTEP) - tid * SEG, (u32)SEG), 0u);
+        __syncthreads();  // B1: the previous tile's parse is done with the bitmaps
+        const u32 tail = sh.rq_tail;
+        if (tail != done) {  // uniform: nothing is pushed between B1 and B2
+            drain_rare(sh, a, done, tail, tid);
+            done = tail;
+        }
+        seg_store(sh, sc, tid, lane, wid);
         __syncthreads();  // B2
-        STAMP(2);
         const TileCount tc = seg_count(sh, sc, wid);
-        if (sc.hi) seg_utf8(sh, a, t, tid);
         if (parse && !uniform_flag(sh.spec_bad) && !(a.ablate & 1u))
             parse_own_headers(sh, a, t, tc, L0 + lines, tid);
-        STAMP(1);
         lines += tc.tot;
     }
-    __syncthreads();  // the LDS tile and bitmaps are free for the caller
-#elif FR_PREFETCH
-    TileRegs r;
-    tile_fetch(a, tb, r, tid);
-    tile_stage(sh, a, tb, r, tid);
+    __syncthreads();  // the bitmaps are free for the caller; the last tile's events are queued
+    const u32 tail = sh.rq_tail;
+    if (tail != done) drain_rare(sh, a, done, tail, tid);
     __syncthreads();
-    TileCount tc = count_tile(sh, a, tb, tid, lane, wid, false);
-    STAMP(4);
-    for (u32 t = tb; t < te; ++t) {
-        const bool more = t + 1 < te;
-        tile_fetch(a, t + 1, r, tid, more);  // lands while this tile is parsed
-        if (parse && !uniform_flag(sh.spec_bad) && !(a.ablate & 1u))
-            parse_own_headers(sh, a, t, tc, L0 + lines, tid);
-        __syncthreads();
-        STAMP(1);
-        lines += tc.tot;
-        if (more) {
-            tile_stage(sh, a, t + 1, r, tid);
-            __syncthreads();
-            STAMP(2);
-            tc = count_tile(sh, a, t + 1, tid, lane, wid, false);
-            STAMP(3);
-        }
-    }
-#else
-    // no register prefetch: the other workgroups on the CU cover this one's load latency
-    for (u32 t = tb; t < te; ++t) {
-        {
-            TileRegs r;
-            tile_fetch(a, t, r, tid);
-            tile_stage(sh, a, t, r, tid);
-        }
-        __syncthreads();
-        STAMP(2);
-        const TileCount tc = count_tile(sh, a, t, tid, lane, wid, false);
-        STAMP(3);
-        if (parse && !uniform_flag(sh.spec_bad) && !(a.ablate & 1u))
-            parse_own_headers(sh, a, t, tc, L0 + lines, tid);
-        __syncthreads();
-        STAMP(1);
-        lines += tc.tot;
-    }
-#endif
-#ifdef FR_STAMPS
-    if (tid == 0)
-        for (int i = 0; i < 8; ++i)
-            if (stamps[i]) atomicAdd((unsigned long long*)&a.st->stamp[i], (unsigned long long)stamps[i]);
-#endif
     return lines;
 }
 
@@ -1255,6 +1001,26 @@ __device__ __forceinline__ u64 walk_chunk(ScanShared& sh, const ScanArgs& a, u32
 // out of work at about the same time.  fr_api only ramps ranges of >= 2 R(G) + C tiles.
 __device__ __forceinline__ u64 ramp_prefix(const ScanArgs& a, u64 j) {
     return j + ((u64)(a.chunk_tiles - 1u) * j * (j + 1)) / (2ull * a.ramp_g);
+}
+
+// the line phase at a chunk's start, guessed from its first tile (infer_phase); -1 unsure
+__device__ __attribute__((noinline)) int guess_phase(ScanShared& sh, const ScanArgs& a, u32 tb, int tid, int lane,
+                                                     int wid) {
+    SegRegs r;
+    if ((u64)tb * TSTEP + (TILE + HALO + SEG + 4) <= a.avail) seg_fetch(a, tb, r, tid);
+    else r = seg_load_tail(a, tb, tid);
+    const SegClass sc = seg_classify(a, tb, r, tid);
+    u64 at, plus;
+    seg_marks(r, at, plus);
+    sh.bsp[tid] = sc.tmask;  // infer_phase: terminators, '@', '+'
+    sh.bcol[tid] = at;
+    sh.beol[tid] = plus;
+    __syncthreads();
+    if (tid == 0) sh.phase = infer_phase(sh);
+    __syncthreads();
+    const int P = sh.phase;
+    __syncthreads();  // the bitmaps are free again
+    return P;
 }
 
 __device__ __forceinline__ void chunk_bounds(const ScanArgs& a, u32 c, u32& tb, u32& te) {
@@ -1279,9 +1045,14 @@ __device__ __forceinline__ void chunk_bounds(const ScanArgs& a, u32 c, u32& tb, 
 }
 
 #ifndef FR_OCC
-#define FR_OCC 4  // workgroups (= waves per SIMD) per CU; fr_api sizes the grid with fr_chunk_occupancy()
+#define FR_OCC 4  // workgroups (= waves per SIMD) per CU (~22.5 KB LDS would allow 7; measured best at 4); fr_api
+                  // sizes the grid with fr_chunk_occupancy()
 #endif
-__global__ __launch_bounds__(WG, FR_OCC) void chunk_kernel(ScanArgs a) {
+__global__ __launch_bounds__(WG, FR_OCC) void chunk_kernel(ScanArgs args) {
+    // every helper reads the arguments where they lie (the kernarg segment): the out-of-line
+    // helpers take them by reference without a scratch copy of the struct
+    (void)args;
+    const ScanArgs& a = *(const ScanArgs*)__builtin_amdgcn_kernarg_segment_ptr();
     __shared__ ScanShared sh;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -1289,7 +1060,6 @@ __global__ __launch_bounds__(WG, FR_OCC) void chunk_kernel(ScanArgs a) {
     for (int i = tid; i < NS; i += WG) {
         sh.ls[i] = LSlot{0, 0, 0xFFFFFFFFu};
     }
-    if (tid < 2) *(uint4*)(sh.buf + 16 + TILE + HALO + 16 * tid) = make_uint4(0u, 0u, 0u, 0u);
     if (tid == 0) {
         sh.nkeys = 0;
         sh.created = 0;
@@ -1300,6 +1070,7 @@ __global__ __launch_bounds__(WG, FR_OCC) void chunk_kernel(ScanArgs a) {
         sh.ncold = 0;
         sh.nexo = 0;
         sh.err_off = 0xFFFFFFFFu;
+        sh.rq_tail = 0;
     }
     const u64 base_lines = a.st->lines[a.par];
     for (;;) {
@@ -1310,37 +1081,13 @@ __global__ __launch_bounds__(WG, FR_OCC) void chunk_kernel(ScanArgs a) {
         u32 tb, te;
         chunk_bounds(a, c, tb, te);
         // ---- the line phase at the chunk start: exact for chunk 0, else guessed ----------
-#ifdef FR_STAMPS
-        u64 stamps[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        u64 last_ = __builtin_amdgcn_s_memtime();
-#endif
         const bool empty = tb >= te;  // defensive: no tile to stage (publishes 0 lines)
         int P = -1;
         if (c == 0) {
             P = (int)(base_lines & 3ull);
         } else if (a.max_records <= 0 && !empty) {
-#if FR_V5
-            SegRegs r;
-            seg_fetch(a, tb, r, tid);
-            seg_fix_tail(a, tb, r, tid);
-            const SegClass sc = seg_classify(a, tb, r, tid);
-            seg_store(sh, r, sc, tid, lane, wid);
-            sh.bsp[tid] = sc.tmask;  // infer_phase reads the terminator bitmap
-            __syncthreads();
-#else
-            TileRegs r;
-            tile_fetch(a, tb, r, tid);
-            tile_stage(sh, a, tb, r, tid);
-            __syncthreads();
-            const TileCount tc0 = count_tile(sh, a, tb, tid, lane, wid, false);
-            sh.bsp[tid] = tc0.tmask;
-            __syncthreads();
-#endif
-            if (tid == 0) sh.phase = infer_phase(sh, 0);
-            __syncthreads();
-            P = sh.phase;
+            P = guess_phase(sh, a, tb, tid, lane, wid);
         }
-        STAMP(5);
         // pass 0: exact (chunk 0) / speculative (guessed phase) / count-only (unsure, -s);
         // pass 1 (only when pass 0 cannot be kept): exact, after the chunk-level look-back
         const bool spec = c != 0 && P >= 0;
@@ -1351,9 +1098,6 @@ __global__ __launch_bounds__(WG, FR_OCC) void chunk_kernel(ScanArgs a) {
         __syncthreads();
         for (int pass = 0;; ++pass) {
             const u64 cnt = empty ? 0ull : walk_chunk(sh, a, tb, te, L0, parse, exact, tid, lane, wid);
-#ifdef FR_STAMPS
-            last_ = __builtin_amdgcn_s_memtime();
-#endif
             if (pass == 1) break;
             // ---- publish the chunk's aggregate, resolve its exact prefix ---------------
             if (tid == 0) {
@@ -1368,7 +1112,6 @@ __global__ __launch_bounds__(WG, FR_OCC) void chunk_kernel(ScanArgs a) {
                 }
             }
             __syncthreads();
-            STAMP(6);
             const u64 exact_L = base_lines + sh.tile_excl;
             const bool keep = c == 0 || empty || (spec && (u32)P == (u32)(exact_L & 3ull) && !uniform_flag(sh.spec_bad));
             if (keep) break;
@@ -1378,11 +1121,6 @@ __global__ __launch_bounds__(WG, FR_OCC) void chunk_kernel(ScanArgs a) {
             exact = true;
         }
         commit_buffers(sh, a, true, tid);
-        STAMP(7);
-#ifdef FR_STAMPS
-        if (tid == 0)
-            for (int i = 5; i < 8; ++i) atomicAdd((unsigned long long*)&a.st->stamp[i], (unsigned long long)stamps[i]);
-#endif
     }
     __syncthreads();
     if (tid == 0) {

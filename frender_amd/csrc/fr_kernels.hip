@@ -22,6 +22,10 @@
 
 namespace fr {
 
+#ifndef FR_TIMING
+#define FR_TIMING 0  // diagnostic builds: per-phase s_memtime cycles of the tile loop into DevState::stamp
+#endif
+
 // FR_OUTLINE_COLD=1 keeps the rare paths out of line (measured slower: the calls make the
 // hot loop save registers to scratch)
 #if FR_OUTLINE_COLD
@@ -195,6 +199,16 @@ __device__ FR_COLD void direct_insert(ScanShared& sh, const ScanArgs& a, u64 key
 
 __device__ __forceinline__ void rare_push(ScanShared& sh, const ScanArgs& a, u32 p, u32 kind, u32 x, u32 y);
 
+// Barrier of the tile loop: orders LDS only.  __syncthreads() would also drain every global store
+// of the wave (cold-list entries) before the barrier; those are read only at the chunk's commit,
+// behind a full __syncthreads().  Global data handed over inside the loop (the rare ring) is
+// released by its writer (rare_push).
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 template <bool DRAIN = false>
 __device__ __forceinline__ void lds_insert(ScanShared& sh, const ScanArgs& a, u64 key, u32 off) {
     // one 32-bit multiply (keys hold <= 63 bits: fold the top down first)
@@ -251,6 +265,7 @@ __device__ __forceinline__ void lds_insert(ScanShared& sh, const ScanArgs& a, u6
 __device__ __forceinline__ void rare_push(ScanShared& sh, const ScanArgs& a, u32 p, u32 kind, u32 x, u32 y) {
     const u32 i = atomicAdd(&sh.rq_tail, 1u);
     a.rare[(u64)blockIdx.x * RARE_RING + (i & (RARE_RING - 1u))] = make_uint4(p, kind, x, y);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // visible to the drain after the next barrier
 }
 
 // Decoupled look-back over the launch's tile descriptors {tag = 2*epoch + inclusive, value}.
@@ -967,26 +982,55 @@ __device__ __forceinline__ u64 walk_chunk(ScanShared& sh, const ScanArgs& a, u32
                           int lane, int wid) {
     u64 lines = 0;
     u32 done = sh.rq_tail;  // the caller synchronised: every thread reads the same value
+#if FR_TIMING
+    u64 tm0 = 0, tm1 = 0, tm2 = 0, tm3 = 0;
+#endif
     for (u32 t = tb; t < te; ++t) {
+#if FR_TIMING
+        const u64 c0 = __builtin_amdgcn_s_memtime();
+#endif
         SegRegs r;
         if ((u64)t * TSTEP + (TILE + HALO + SEG + 4) <= a.avail) seg_fetch(a, t, r, tid);
         else r = seg_load_tail(a, t, tid);  // the data end: bytewise, zeros past it
         const SegClass sc = seg_classify(a, t, r, tid);
+#if FR_TIMING
+        __builtin_amdgcn_s_waitcnt(0);
+        const u64 c1 = __builtin_amdgcn_s_memtime();
+#endif
         if (sc.hi) rare_push(sh, a, (u32)((u64)t * TSTEP) + tid * SEG, 4u,
                              min((u32)min((u64)TSTEP, a.len - (u64)t * TSTEP) - tid * SEG, (u32)SEG), 0u);
-        __syncthreads();  // B1: the previous tile's parse is done with the bitmaps
+        lds_barrier();  // B1: the previous tile's parse is done with the bitmaps
         const u32 tail = sh.rq_tail;
         if (tail != done) {  // uniform: nothing is pushed between B1 and B2
             drain_rare(sh, a, done, tail, tid);
             done = tail;
         }
         seg_store(sh, sc, tid, lane, wid);
-        __syncthreads();  // B2
+        lds_barrier();  // B2
+#if FR_TIMING
+        const u64 c2 = __builtin_amdgcn_s_memtime();
+#endif
         const TileCount tc = seg_count(sh, sc, wid);
         if (parse && !uniform_flag(sh.spec_bad) && !(a.ablate & 1u))
             parse_own_headers(sh, a, t, tc, L0 + lines, tid);
         lines += tc.tot;
+#if FR_TIMING
+        __builtin_amdgcn_s_waitcnt(0);
+        const u64 c3 = __builtin_amdgcn_s_memtime();
+        tm0 += c1 - c0;  // load + classify
+        tm1 += c2 - c1;  // B1 + drain + store + B2
+        tm2 += c3 - c2;  // parse
+        tm3 += 1;
+#endif
     }
+#if FR_TIMING
+    if ((tid & 63) == 0) {  // diagnostic build only: per-phase shader cycles summed over waves
+        atomicAdd((unsigned long long*)&a.st->stamp[0], (unsigned long long)tm0);
+        atomicAdd((unsigned long long*)&a.st->stamp[1], (unsigned long long)tm1);
+        atomicAdd((unsigned long long*)&a.st->stamp[2], (unsigned long long)tm2);
+        atomicAdd((unsigned long long*)&a.st->stamp[3], (unsigned long long)tm3);
+    }
+#endif
     __syncthreads();  // the bitmaps are free for the caller; the last tile's events are queued
     const u32 tail = sh.rq_tail;
     if (tail != done) drain_rare(sh, a, done, tail, tid);

@@ -413,11 +413,12 @@ class Context:
         return t
 
     def diag(self) -> dict:
-        v = np.zeros(16, dtype=np.uint64)
-        self._ck(lib.fr_get_diag(self.h, _ptr(v), 16), "fr_get_diag")
+        v = np.zeros(17, dtype=np.uint64)
+        self._ck(lib.fr_get_diag(self.h, _ptr(v), 17), "fr_get_diag")
         d = dict(zip(("spin_max", "spin_total", "keys", "overflow", "presence", "exotic", "grid", "slots"),
                      v[:8].tolist()))
-        if v[8:].any():  # FR_STAMPS build: cycles per phase summed over workgroups
+        d["spec_replays"] = int(v[16])
+        if v[8:16].any():  # FR_TIMING build / FR_ABLATE=64: per-phase cycles or commit counts
             names = (("lookback", "barrier", "headers", "parse", "stage", "count", "flush", "prologue")
                      if os.environ.get("FR_KERNEL") == "0" else
                      ("collect", "parse", "stage", "count", "first_tile", "infer", "lookback", "commit"))

@@ -37,7 +37,11 @@ struct fr_ctx {
     hipEvent_t st_ev = nullptr;
     bool st_pending = false;
     u64* tiles = nullptr;
+    u64* chunk_info = nullptr;  // per chunk: line count + speculation flags (verify_launch)
     u64 tiles_cap = 0;
+    bool spec_ok = true;        // FR_SPEC_COMMIT=0: every chunk waits for its exact prefix
+    u64 spec_replays = 0;       // feeds replayed after a wrong speculative guess (diagnostics)
+    u32 spec_commit = 0;        // the current feed commits speculative chunks at once
     u32 epoch = 0;
     u32 par = 0;
 
@@ -254,6 +258,8 @@ static int launch_range(fr_ctx* ctx, const u8* dptr, u64 len, u64 avail, int own
     a.max_records = ctx->max_records;
     a.st = ctx->st;
     a.tiles = ctx->tiles;
+    a.chunk_info = ctx->chunk_info;
+    a.spec_commit = ctx->spec_commit;
     if (std::memcmp(&ctx->tab, ctx->h_tab, sizeof(Table)) != 0) {  // the table moved: refresh its device copy
         CK(hipStreamSynchronize(ctx->stream));  // the previous copy from h_tab has landed
         std::memcpy(ctx->h_tab, &ctx->tab, sizeof(Table));
@@ -266,7 +272,7 @@ static int launch_range(fr_ctx* ctx, const u8* dptr, u64 len, u64 avail, int own
         ctx->epoch = 1;
         a.epoch = 1;
     }
-    CK(hipMemsetAsync(&ctx->st->ticket, 0, sizeof(u32), ctx->stream));
+    CK(hipMemsetAsync(&ctx->st->ticket, 0, 2 * sizeof(u32), ctx->stream));  // ticket, chunks_done
     ctx->st_fresh = false;
     if (ctx->ev_used == ctx->ev_a.size()) {
         hipEvent_t e1, e2;
@@ -345,6 +351,8 @@ fr_ctx* fr_create(int device, uint64_t chunk_bytes, uint64_t table_slots) {
         return bad("pinned state", e);
     if ((e = hipEventCreateWithFlags(&ctx->st_ev, hipEventDisableTiming)) != hipSuccess) return bad("event", e);
     if ((e = dalloc(&ctx->tiles, ctx->tiles_cap)) != hipSuccess) return bad("tiles", e);
+    if ((e = dalloc(&ctx->chunk_info, ctx->tiles_cap)) != hipSuccess) return bad("chunk info", e);
+    if (const char* f = getenv("FR_SPEC_COMMIT")) ctx->spec_ok = atoi(f) != 0;
     if ((e = hipMemset(ctx->tiles, 0, ctx->tiles_cap * sizeof(u64))) != hipSuccess) return bad("tiles", e);
     if ((e = dalloc(&ctx->tab.slots, ctx->nslots)) != hipSuccess) return bad("table", e);
     ctx->tab.mask = ctx->nslots - 1;
@@ -383,7 +391,7 @@ void fr_destroy(fr_ctx* ctx) {
                    ctx->d_keys, ctx->d_counts, ctx->d_first, ctx->d_keys_s, ctx->d_counts_s,
                    ctx->d_first_s, ctx->d_pos, ctx->d_perm, ctx->d_rank, ctx->d_counter, ctx->d_temp, ctx->d_pres_u,
                    ctx->d_pres_f, ctx->d_m1, ctx->d_m2, ctx->d_row, ctx->d_rm2, ctx->d_rrow, ctx->d_cls, ctx->d_rcls,
-                   ctx->d_errw, ctx->d_errf, ctx->d_rcf, ctx->d_rcr, ctx->cold, ctx->rare};
+                   ctx->d_errw, ctx->d_errf, ctx->d_rcf, ctx->d_rcr, ctx->cold, ctx->rare, ctx->chunk_info};
     for (void* p : dev)
         if (p) (void)hipFree(p);
     if (ctx->h_st) (void)hipHostFree(ctx->h_st);
@@ -410,7 +418,7 @@ int fr_get_diag(fr_ctx* ctx, uint64_t* out, int n) {
     const DevState& s = *ctx->h_st;
     const uint64_t v[] = {s.spin_max,   s.spin_total, s.n_keys,   s.n_overflow, s.n_presence, s.n_exotic,
                           (uint64_t)ctx->grid, ctx->nslots, s.stamp[0], s.stamp[1], s.stamp[2], s.stamp[3],
-                          s.stamp[4],  s.stamp[5],  s.stamp[6], s.stamp[7]};
+                          s.stamp[4],  s.stamp[5],  s.stamp[6], s.stamp[7], ctx->spec_replays};
     for (int i = 0; i < n && i < (int)(sizeof(v) / sizeof(v[0])); ++i) out[i] = v[i];
     return FR_OK;
 }
@@ -610,14 +618,63 @@ int fr_feed_device(fr_ctx* ctx, const uint8_t* dev_data, uint64_t len) {
     if (ctx->file_offset != 0 || !ctx->carry.empty())
         return fail(ctx, FR_ERR_INVALID, "fr_feed_device takes a whole file (no prior fr_feed)");
     if (((uintptr_t)dev_data & 15u) != 0) return fail(ctx, FR_ERR_INVALID, "device data must be 16-byte aligned");
+    // Speculative chunks commit without waiting for their exact line prefix; the launch's last
+    // workgroup checks every guess (verify_launch).  A wrong guess -- possible only for inputs that
+    // are not 4-line FASTQ -- rolls the table back to this feed's start and replays it with every
+    // chunk waiting for its prefix.  The rollback point: the table slots (a device copy unless the
+    // table is empty) and the device state.
+    int rc = read_state(ctx);
+    if (rc) return rc;
+    const DevState saved = *ctx->h_st;
+    const u32 par0 = ctx->par;
+    const u64 snap_slots = ctx->nslots;
+    const bool empty = saved.n_keys == 0 && saved.n_overflow == 0;
+    const bool spec = ctx->spec_ok && ctx->max_records == 0 && saved.n_overflow == 0;
+    GSlot* snap = nullptr;
+    if (spec && !empty) {
+        CK(dalloc(&snap, snap_slots));
+        CK(hipMemcpyAsync(snap, ctx->tab.slots, snap_slots * sizeof(GSlot), hipMemcpyDeviceToDevice, ctx->stream));
+    }
     // equal ranges of at most chunk_bytes
     const u64 nr = (len + ctx->chunk_bytes - 1) / ctx->chunk_bytes;
     const u64 step = nr ? (len + nr - 1) / nr : 0;
-    for (u64 off = 0; off < len; off += step) {
-        const u64 n = std::min<u64>(step, len - off);
-        int rc = launch_range(ctx, dev_data + off, n, len - off, off == 0 ? 1 : 0, 1, off ? 1 : 0);
-        if (rc) return rc;
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        ctx->spec_commit = spec && attempt == 0 ? 1u : 0u;
+        for (u64 off = 0; off < len; off += step) {
+            const u64 n = std::min<u64>(step, len - off);
+            rc = launch_range(ctx, dev_data + off, n, len - off, off == 0 ? 1 : 0, 1, off ? 1 : 0);
+            if (rc) break;
+        }
+        ctx->spec_commit = 0;
+        if (!rc) rc = read_state(ctx);
+        if (rc || !spec || attempt == 1 || !ctx->h_st->spec_fail) break;
+        // roll back: the table as it was (its size too), the device state, the launch parity
+        if (ctx->nslots != snap_slots) {
+            GSlot* fresh = nullptr;
+            if ((rc = (dalloc(&fresh, snap_slots) == hipSuccess) ? FR_OK : fail(ctx, FR_ERR_DEVICE, "rollback alloc")))
+                break;
+            CK(hipStreamSynchronize(ctx->stream));
+            CK(hipFree(ctx->tab.slots));
+            ctx->tab.slots = fresh;
+            ctx->tab.mask = snap_slots - 1;
+            ctx->nslots = snap_slots;
+        }
+        if (empty) CK(launch_table_init(ctx->tab.slots, ctx->nslots, ctx->stream));
+        else CK(hipMemcpyAsync(ctx->tab.slots, snap, snap_slots * sizeof(GSlot), hipMemcpyDeviceToDevice, ctx->stream));
+        *ctx->h_st = saved;
+        CK(hipMemcpyAsync(ctx->st, ctx->h_st, sizeof(DevState), hipMemcpyHostToDevice, ctx->stream));
+        CK(hipStreamSynchronize(ctx->stream));
+        ctx->st_pending = false;
+        ctx->st_fresh = true;
+        ctx->par = par0;
+        ctx->file_offset = 0;
+        ctx->spec_replays++;
     }
+    if (snap) {
+        CK(hipStreamSynchronize(ctx->stream));
+        CK(hipFree(snap));
+    }
+    if (rc) return rc;
     if (len) {
         u8 b = 0;
         CK(hipMemcpyAsync(&b, dev_data + len - 1, 1, hipMemcpyDeviceToHost, ctx->stream));

@@ -59,8 +59,10 @@ struct alignas(32) Overflow {
 
 struct DevState {
     u64 lines[2];        // terminators before the current range (launch parity)
-    u32 ticket;          // tile ticket, zeroed before every launch
+    u32 ticket;          // chunk ticket, zeroed before every launch
+    u32 chunks_done;     // chunks that published their line count (zeroed with the ticket)
     u32 spin_fail;
+    u32 spec_fail;       // a committed speculative chunk's guessed line phase was wrong (host redoes the feed)
     u64 n_keys;
     u64 n_overflow;
     u64 n_presence;
@@ -114,6 +116,9 @@ struct ScanArgs {
     u32 cold_cap;        // chunk kernel: entries of each workgroup's cold list
     u64* cold;           // chunk kernel: cold lists, [grid][cold_cap] x {key, ordinal}
     uint4* rare;         // chunk kernel: rare-event rings, [grid][RARE_RING] (fr_kernels.hip)
+    u64* chunk_info;     // chunk kernel: per chunk {line count, spec flag + guessed phase << 1 in the high word}
+    u32 spec_commit;     // commit speculative chunks without waiting for their exact prefix (checked at the
+                         // launch end by verify_launch; a wrong guess sets spec_fail)
     DevState* st;
     u64* tiles;          // look-back descriptors
     const Table* tab;    // device copy: read where used (rare paths), so the tile loop holds no

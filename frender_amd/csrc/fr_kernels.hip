@@ -173,6 +173,7 @@ struct ScanShared {
     u32 created;      // HBM slots this workgroup created (added to n_keys once, at exit)
     u32 flags;
     u32 rq_tail;      // rare-event ring: events pushed by this workgroup (monotonic)
+    u32 last;         // this workgroup published the launch's last chunk count (runs verify_launch)
     // ---- chunk kernel state ----
     u32 buffered;     // LDS-table misses go to this workgroup's cold list (committed later)
     u32 spec;         // speculating on the line phase: exotic records / errors are buffered
@@ -984,6 +985,7 @@ __device__ __forceinline__ u64 walk_chunk(ScanShared& sh, const ScanArgs& a, u32
     u32 done = sh.rq_tail;  // the caller synchronised: every thread reads the same value
 #if FR_TIMING
     u64 tm0 = 0, tm1 = 0, tm2 = 0, tm3 = 0;
+    const u64 w0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
 #endif
     for (u32 t = tb; t < te; ++t) {
 #if FR_TIMING
@@ -1029,6 +1031,8 @@ __device__ __forceinline__ u64 walk_chunk(ScanShared& sh, const ScanArgs& a, u32
         atomicAdd((unsigned long long*)&a.st->stamp[1], (unsigned long long)tm1);
         atomicAdd((unsigned long long*)&a.st->stamp[2], (unsigned long long)tm2);
         atomicAdd((unsigned long long*)&a.st->stamp[3], (unsigned long long)tm3);
+        atomicAdd((unsigned long long*)&a.st->stamp[4], (unsigned long long)(__builtin_amdgcn_s_memtime() - w0));
+        atomicAdd((unsigned long long*)&a.st->stamp[5], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - r0));
     }
 #endif
     __syncthreads();  // the bitmaps are free for the caller; the last tile's events are queued
@@ -1045,6 +1049,45 @@ __device__ __forceinline__ u64 walk_chunk(ScanShared& sh, const ScanArgs& a, u32
 // out of work at about the same time.  fr_api only ramps ranges of >= 2 R(G) + C tiles.
 __device__ __forceinline__ u64 ramp_prefix(const ScanArgs& a, u64 j) {
     return j + ((u64)(a.chunk_tiles - 1u) * j * (j + 1)) / (2ull * a.ramp_g);
+}
+
+// Run by the workgroup that finishes the launch's last chunk: the exact line prefix of every chunk
+// (exclusive scan of the published counts), checked against the phase each committed speculative
+// chunk guessed; writes the range's line total for the next launch.
+__device__ __attribute__((noinline)) void verify_launch(ScanShared& sh, const ScanArgs& a, u64 base_lines, int tid) {
+    const u32 n = a.num_chunks;
+    const u32 per = (n + WG - 1) / WG;
+    const u32 lo = min(tid * per, n), hi = min(lo + per, n);
+    u64 sum = 0;
+    for (u32 c = lo; c < hi; ++c) sum += (u32)agent_load(&a.chunk_info[c]);
+    // block exclusive scan of the per-thread sums (bitmap words are free scratch here)
+    u64 x = sum;
+    const int lane = tid & 63, wid = tid >> 6;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const u64 y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) sh.bsp[wid] = x;
+    __syncthreads();
+    u64 before = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < WG / 64; ++w) {
+        const u64 v = sh.bsp[w];
+        before += w < wid ? v : 0ull;
+        total += v;
+    }
+    u64 run = base_lines + before + (x - sum);
+    bool bad = false;
+    for (u32 c = lo; c < hi; ++c) {
+        const u64 info = agent_load(&a.chunk_info[c]);
+        const u32 f = (u32)(info >> 32);
+        if ((f & 1u) && ((f >> 1) & 3u) != (u32)(run & 3ull)) bad = true;
+        run += (u32)info;
+    }
+    if (bad) atomicOr(&a.st->spec_fail, 1u);
+    if (tid == 0) a.st->lines[a.par ^ 1u] = base_lines + total;
+    __syncthreads();
 }
 
 // the line phase at a chunk's start, guessed from its first tile (infer_phase); -1 unsure
@@ -1143,17 +1186,21 @@ __global__ __launch_bounds__(WG, FR_OCC) void chunk_kernel(ScanArgs args) {
         for (int pass = 0;; ++pass) {
             const u64 cnt = empty ? 0ull : walk_chunk(sh, a, tb, te, L0, parse, exact, tid, lane, wid);
             if (pass == 1) break;
-            // ---- publish the chunk's aggregate, resolve its exact prefix ---------------
+            // ---- publish the chunk's line count; a speculative chunk commits at once (checked
+            // by verify_launch), any other resolves its exact prefix first --------------------
+            const bool fast = spec && a.spec_commit && !uniform_flag(sh.spec_bad);
             if (tid == 0) {
                 sh.spec = 0;
                 agent_store(&a.tiles[c], ((u64)(2u * a.epoch + (c == 0 ? 1u : 0u)) << 32) | (u32)cnt);
+                const u32 f = fast ? (1u | ((u32)P << 1)) : 0u;
+                agent_store(&a.chunk_info[c], ((u64)f << 32) | (u32)cnt);
+                const u32 prev = __hip_atomic_fetch_add(&a.st->chunks_done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                sh.last = prev == a.num_chunks - 1u;
             }
+            if (fast) break;
             if (wid == 0) {
                 const u64 ex = lookback(a, c, (u32)cnt, lane);
-                if (lane == 0) {
-                    sh.tile_excl = ex;
-                    if (c == a.num_chunks - 1) a.st->lines[a.par ^ 1u] = base_lines + ex + cnt;
-                }
+                if (lane == 0) sh.tile_excl = ex;
             }
             __syncthreads();
             const u64 exact_L = base_lines + sh.tile_excl;
@@ -1164,7 +1211,11 @@ __global__ __launch_bounds__(WG, FR_OCC) void chunk_kernel(ScanArgs args) {
             parse = true;
             exact = true;
         }
-        commit_buffers(sh, a, true, tid);
+        commit_buffers(sh, a, true, tid);  // starts and ends with a barrier: sh.last is visible
+        if (sh.last) {
+            __atomic_thread_fence(__ATOMIC_ACQUIRE);
+            verify_launch(sh, a, base_lines, tid);
+        }
     }
     __syncthreads();
     if (tid == 0) {

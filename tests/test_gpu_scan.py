@@ -143,6 +143,25 @@ def test_no_trailing_newline_and_truncated(ctx, lib):
         assert_same(gpu_tally(ctx, lib, files, mode=mode), oracle_tally(files))
 
 
+def test_speculative_commit_replay(lib):
+    """A file whose chunks look like 4-line FASTQ one line off the true phase: every chunk after
+    the first guesses the wrong line phase, commits at once, the launch-end check catches it and
+    the feed is replayed with every chunk waiting for its exact prefix (fr_feed_device)."""
+    recs = ["L 1:N:0:AAAA+CCCC\n"] + [f"@r{i} 1:N:0:ACGT+ACGT\nACGT\n+\nA AC\n" for i in range(60000)]
+    data = "".join(recs).encode()
+    exp = oracle_tally([data])
+    assert list(exp[0]) == ["AAAA+CCCC", "AC"]
+    c = lib.Context(device=0, chunk_bytes=1 << 20, table_slots=1 << 16)
+    try:
+        assert_same(gpu_tally(c, lib, [data], mode="device"), exp)
+        assert c.diag()["spec_replays"] == 1
+        good = "".join(f"@r{i} 1:N:0:ACGT+ACG{'ACGT'[i % 4]}\nACGT\n+\nFFFF\n" for i in range(60000)).encode()
+        assert_same(gpu_tally(c, lib, [data, good], mode="device"), oracle_tally([data, good]))
+        assert c.diag()["spec_replays"] == 2  # the second file (non-empty table) commits without a replay
+    finally:
+        c.close()
+
+
 def test_table_growth_and_overflow(lib):
     """Start from a 1024-slot table with ~60k distinct codes: the table must grow
     between launches (overflow list absorbs in-flight inserts) and stay exact."""

@@ -58,18 +58,15 @@ __device__ __forceinline__ u32 sym_of(u32 c) {
     return ok ? ((symtab >> (4 * i)) & 0xFu) : 0u;
 }
 
-// Fused byte classifier, 4 bytes per call: per byte, bit0 '\n', bit1 '\r', bit2 ' ', bit3 ':'
-// (ASCII only).  Two nibble lookup tables through v_perm_b32: class = T_hi[c >> 4] & T_lo[c & 15].
+// Fused byte classifier, 4 bytes per call: per byte, bit0 '\n', bit1 '\r', bit2 ' ', bit3 ':'.
+// Three 8-entry lookups through v_perm_b32, ANDed: on bits [2:0], on bits [5:3], and on bits [7:6]
+// (only 00 can match).  '\n' = 00 001 010, '\r' = 00 001 101, ' ' = 00 100 000, ':' = 00 111 010:
+// each class is the one byte whose two table entries both carry its bit (checked for all 256 bytes).
 __device__ __forceinline__ u32 classify4(u32 w) {
-    const u32 hn = (w >> 4) & 0x07070707u;                                   // bit 3 handled by `kill`
-    const u32 ln = w & 0x0F0F0F0Fu;
-    const u32 l7 = ln & 0x07070707u;
-    const u32 ch = __builtin_amdgcn_perm(0u, 0x08040003u, hn);               // 0:{nl,cr} 2:sp 3:col
-    const u32 c0 = __builtin_amdgcn_perm(0u, 0x00000004u, l7);               // lo 0: sp
-    const u32 c1 = __builtin_amdgcn_perm(0x00000200u, 0x00090000u, l7);      // lo 0xA: nl|col, 0xD: cr
-    const u32 m8 = ((ln >> 3) & 0x01010101u) * 0xFFu;
-    const u32 kill = ((w >> 7) & 0x01010101u) * 0xFFu;
-    return ch & ((c0 & ~m8) | (c1 & m8)) & ~kill;
+    const u32 lo3 = __builtin_amdgcn_perm(0x00000200u, 0x00090004u, w & 0x07070707u);         // 0 sp, 2 nl|col, 5 cr
+    const u32 mid3 = __builtin_amdgcn_perm(0x08000004u, 0x00000300u, (w >> 3) & 0x07070707u); // 1 nl|cr, 4 sp, 7 col
+    const u32 top2 = __builtin_amdgcn_perm(0u, 0x0000000Fu, (w >> 6) & 0x03030303u);          // 00 only
+    return lo3 & mid3 & top2;
 }
 
 // Class K of 16 bytes (four class words, byte i of word j = position 4j + i) -> a 16-bit mask.
@@ -846,7 +843,7 @@ __device__ __forceinline__ bool encode_glob(const ScanArgs& a, u64 tile0, u32 st
     const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(((u64)hi << 32) | lo), (short)0,
                                                         (int)__builtin_amdgcn_readfirstlane(nrec), 0x00020000);
     const u32 b4 = start & ~3u;
-    const u32 sh8 = (start & 3u) * 8u;
+    const u32 sh = start & 3u;
     const auto v0 = __builtin_amdgcn_raw_buffer_load_b128(rsrc, b4, 0, 0);
     const auto v1 = __builtin_amdgcn_raw_buffer_load_b128(rsrc, b4, 16, 0);
     const u32 w[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
@@ -854,7 +851,7 @@ __device__ __forceinline__ bool encode_glob(const ScanArgs& a, u64 tile0, u32 st
     u32 bad = 0;
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
-        const u32 x = (u32)((((u64)w[k + 1] << 32) | w[k]) >> sh8);
+        const u32 x = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);  // code bytes 4k .. 4k+3
         const u32 idx = (x >> 1) & 0x07070707u;
         const u32 expect = __builtin_amdgcn_perm(0x4E002B00u, 0x47544341u, idx);
         const u32 sym = __builtin_amdgcn_perm(0x05000600u, 0x03040201u, idx);
@@ -862,7 +859,8 @@ __device__ __forceinline__ bool encode_glob(const ScanArgs& a, u64 tile0, u32 st
         const u32 vm = left >= 4 ? 0xFFFFFFFFu : left <= 0 ? 0u : (0xFFFFFFFFu >> (32 - 8 * left));
         bad |= (expect ^ x) & vm;
         const u32 sv = sym & vm;
-        const u32 packed = (sv & 0x7u) | ((sv >> 5) & 0x38u) | ((sv >> 10) & 0x1C0u) | ((sv >> 15) & 0xE00u);
+        // four 3-bit symbols -> 12 bits: dot4 packs the first three, the fourth is shifted in
+        const u32 packed = __builtin_amdgcn_udot4(sv, 0x00400801u, (sv >> 15) & 0xE00u, false);
         kk |= (u64)packed << (12 * k);
     }
     key = kk;

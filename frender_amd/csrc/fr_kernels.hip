@@ -58,14 +58,16 @@ __device__ __forceinline__ u32 sym_of(u32 c) {
     return ok ? ((symtab >> (4 * i)) & 0xFu) : 0u;
 }
 
-// Fused byte classifier, 4 bytes per call: per byte, bit0 '\n', bit1 '\r', bit2 ' ', bit3 ':'.
-// Three 8-entry lookups through v_perm_b32, ANDed: on bits [2:0], on bits [5:3], and on bits [7:6]
-// (only 00 can match).  '\n' = 00 001 010, '\r' = 00 001 101, ' ' = 00 100 000, ':' = 00 111 010:
-// each class is the one byte whose two table entries both carry its bit (checked for all 256 bytes).
+// Fused byte classifier, 4 bytes per call: per byte, bit0 line end ('\n' or '\r'), bit1 '\r',
+// bit2 ' ', bit3 ':', bit4 byte >= 0x80.  Three 8-entry lookups through v_perm_b32, ANDed: on bits
+// [2:0], on bits [5:3], and on bits [7:6].  '\n' = 00 001 010, '\r' = 00 001 101, ' ' = 00 100 000,
+// ':' = 00 111 010: each class is the one byte whose two table entries both carry its bit; bit 4 is
+// in every entry of the first two tables and in the third only for bits [7:6] = 1x (checked for
+// all 256 bytes).
 __device__ __forceinline__ u32 classify4(u32 w) {
-    const u32 lo3 = __builtin_amdgcn_perm(0x00000200u, 0x00090004u, w & 0x07070707u);         // 0 sp, 2 nl|col, 5 cr
-    const u32 mid3 = __builtin_amdgcn_perm(0x08000004u, 0x00000300u, (w >> 3) & 0x07070707u); // 1 nl|cr, 4 sp, 7 col
-    const u32 top2 = __builtin_amdgcn_perm(0u, 0x0000000Fu, (w >> 6) & 0x03030303u);          // 00 only
+    const u32 lo3 = __builtin_amdgcn_perm(0x10101310u, 0x10191014u, w & 0x07070707u);
+    const u32 mid3 = __builtin_amdgcn_perm(0x18101014u, 0x10101310u, (w >> 3) & 0x07070707u);
+    const u32 top2 = __builtin_amdgcn_perm(0u, 0x1010000Fu, (w >> 6) & 0x03030303u);
     return lo3 & mid3 & top2;
 }
 
@@ -526,26 +528,35 @@ __device__ __forceinline__ SegClass seg_classify(const ScanArgs& a, u32 t, const
     sc.sp = sc.col = sc.eol = 0;
     sc.hi = false;
     if (s0 < bl) {
-        u32 nl16[4], cr16[4], sp16[4], col16[4];
-        u32 hiw = 0;
+        u32 c[16], eol16[4], sp16[4], col16[4];
+        u32 acc = 0;
 #pragma unroll
         for (int qv = 0; qv < SEG / 16; ++qv) {
             const uint4 v = r.v[qv];
-            const u32 c0 = classify4(v.x), c1 = classify4(v.y), c2 = classify4(v.z), c3 = classify4(v.w);
-            nl16[qv] = gather16<0>(c0, c1, c2, c3);
-            cr16[qv] = gather16<1>(c0, c1, c2, c3);
-            sp16[qv] = gather16<2>(c0, c1, c2, c3);
-            col16[qv] = gather16<3>(c0, c1, c2, c3);
-            hiw |= v.x | v.y | v.z | v.w;
+            c[4 * qv] = classify4(v.x);
+            c[4 * qv + 1] = classify4(v.y);
+            c[4 * qv + 2] = classify4(v.z);
+            c[4 * qv + 3] = classify4(v.w);
+            eol16[qv] = gather16<0>(c[4 * qv], c[4 * qv + 1], c[4 * qv + 2], c[4 * qv + 3]);
+            sp16[qv] = gather16<2>(c[4 * qv], c[4 * qv + 1], c[4 * qv + 2], c[4 * qv + 3]);
+            col16[qv] = gather16<3>(c[4 * qv], c[4 * qv + 1], c[4 * qv + 2], c[4 * qv + 3]);
+            acc |= c[4 * qv] | c[4 * qv + 1] | c[4 * qv + 2] | c[4 * qv + 3];
         }
         auto join = [](const u32 (&g)[4]) {
             return ((u64)(g[2] | (g[3] << 16)) << 32) | (u64)(g[0] | (g[1] << 16));
         };
-        const u64 nl = join(nl16), cr = join(cr16);
-        u64 sp = join(sp16), col = join(col16);
-        const u64 nxt = (r.nx & 0xFFu) == (u32)'\n' ? 1ull : 0ull;
-        u64 tm = nl | (cr & ~((nl >> 1) | (nxt << 63)));
-        u64 eol = nl | cr;
+        u64 eol = join(eol16), sp = join(sp16), col = join(col16);
+        u64 tm = eol;
+        if (__builtin_amdgcn_readfirstlane(__ballot((acc & 0x02020202u) != 0) != 0)) {
+            // '\r' somewhere in the wave (CRLF / CR files): a '\r' right before a '\n' ends no line
+            u32 cr16[4];
+#pragma unroll
+            for (int qv = 0; qv < SEG / 16; ++qv)
+                cr16[qv] = gather16<1>(c[4 * qv], c[4 * qv + 1], c[4 * qv + 2], c[4 * qv + 3]);
+            const u64 cr = join(cr16), nl = eol & ~cr;
+            const u64 nxt = (r.nx & 0xFFu) == (u32)'\n' ? 1ull : 0ull;
+            tm = eol & ~(cr & ((nl >> 1) | (nxt << 63)));
+        }
         const u32 bvalid = bl - s0;
         if (bvalid < SEG) {
             const u64 vm = (1ull << bvalid) - 1ull;
@@ -560,17 +571,19 @@ __device__ __forceinline__ SegClass seg_classify(const ScanArgs& a, u32 t, const
             const u32 valid = tlen - s0;
             if (valid < SEG) tm &= (1ull << valid) - 1ull;
             sc.tmask = tm;
-            sc.hi = (hiw & 0x80808080u) != 0;  // exact own-byte test in drain_rare (kind 4)
+            sc.hi = (acc & 0x10101010u) != 0;  // exact own-byte test in drain_rare (kind 4)
         }
     }
     sc.c = __popcll(sc.tmask);
-    u32 x = 0, wtot = 0;
-#pragma unroll
-    for (int b = 0; b < 7; ++b) {
-        const u64 m = __ballot((sc.c >> b) & 1u);
-        x += (__builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u)) + ((sc.c >> b) & 1u)) << b;
-        wtot += (u32)__popcll(m) << b;
-    }
+    // inclusive wave scan of c: DPP row shifts within 16-lane rows, then row broadcasts
+    u32 x = sc.c;
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x111, 0xF, 0xF, true);  // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x112, 0xF, 0xF, true);  // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x114, 0xF, 0xF, true);  // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x118, 0xF, 0xF, true);  // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+    const u32 wtot = __builtin_amdgcn_readlane(x, 63);
     sc.x = x;
     sc.wtot = wtot;
     return sc;

@@ -25,6 +25,9 @@ namespace fr {
 #ifndef FR_TIMING
 #define FR_TIMING 0  // diagnostic builds: per-phase s_memtime cycles of the tile loop into DevState::stamp
 #endif
+#ifndef FR_PREFETCH
+#define FR_PREFETCH 0  // load tile t+1's segment before tile t's header parse
+#endif
 
 // FR_OUTLINE_COLD=1 keeps the rare paths out of line (measured slower: the calls make the
 // hot loop save registers to scratch)
@@ -216,13 +219,15 @@ __device__ __forceinline__ void lds_insert(ScanShared& sh, const ScanArgs& a, u6
 #pragma unroll 2
     for (int pr = 0; pr < LPROBE; ++pr) {
         typedef u32 u32x4 __attribute__((ext_vector_type(4)));
-        const u32x4 sl = *(const volatile u32x4*)&sh.ls[h];
+        // volatile through an explicit LDS pointer: a volatile access through a generic pointer
+        // keeps its flat form (flat loads wait on vmcnt(0), i.e. on every outstanding HBM op)
+        const u32x4 sl = *(const volatile __attribute__((address_space(3))) u32x4*)&sh.ls[h];
         u64 k = ((u64)sl.y << 32) | sl.x;
         u32 mino = sl.w;
         if (k == 0) {
             // a full LDS table stops claiming slots: the code goes to HBM directly; the
             // codes already resident (the hot ones arrive first) keep aggregating here
-            if (*(volatile u32*)&sh.nkeys >= a.flush_at) break;
+            if (*(const volatile __attribute__((address_space(3))) u32*)&sh.nkeys >= a.flush_at) break;
             const u64 old = atomicCAS((unsigned long long*)&sh.ls[h].key, 0ull, (unsigned long long)key);
             if (old == 0) {
                 atomicAdd(&sh.nkeys, 1u);
@@ -472,7 +477,8 @@ struct SegRegs {
     u32 nx;  // first dword of the next segment (zero past the staged bytes)
 };
 
-__device__ __forceinline__ void seg_fetch(const ScanArgs& a, u32 t, SegRegs& r, int tid, bool want = true) {
+__device__ __forceinline__ void seg_fetch(const ScanArgs& a, u32 t, SegRegs& r, int tid, bool want = true,
+                                          bool with_nx = false) {
     const bool live = want && t < a.num_tiles;
     const u64 tile0 = live ? (u64)t * TSTEP : 0ull;
     const u32 nb = live ? (u32)min((u64)(TILE + HALO), a.avail - tile0) : 0u;
@@ -486,7 +492,7 @@ __device__ __forceinline__ void seg_fetch(const ScanArgs& a, u32 t, SegRegs& r, 
         const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, tid * SEG, k * 16, 0);
         r.v[k] = make_uint4(v[0], v[1], v[2], v[3]);
     }
-    r.nx = __builtin_amdgcn_raw_buffer_load_b32(rsrc, tid * SEG + SEG, 0, 0);
+    r.nx = with_nx ? __builtin_amdgcn_raw_buffer_load_b32(rsrc, tid * SEG + SEG, 0, 0) : 0u;  // '\r' path only
 }
 
 // the data end (a segment, or the dword after it, reaches past avail): bytewise loads, zeros past
@@ -510,6 +516,17 @@ __device__ __attribute__((noinline)) SegRegs seg_load_tail(const ScanArgs& a, u3
     return r;
 }
 
+// every lane's segment loads of tile t lie inside the data (else seg_load_tail)
+__device__ __forceinline__ bool seg_in_range(const ScanArgs& a, u32 t) {
+    return (u64)t * TSTEP + (TILE + HALO + SEG + 4) <= a.avail;
+}
+
+// tile t's segment into r (the data end: bytewise loads, zeros past it)
+__device__ __forceinline__ void seg_prefetch_next(const ScanArgs& a, u32 t, SegRegs& r, int tid) {
+    if (seg_in_range(a, t)) seg_fetch(a, t, r, tid);
+    else r = seg_load_tail(a, t, tid);
+}
+
 struct SegClass {
     u64 tmask, sp, col, eol;  // terminators (own bytes), and the parse bitmaps (staged bytes)
     u32 c, x;                 // popcount(tmask), its inclusive wave scan
@@ -528,19 +545,16 @@ __device__ __forceinline__ SegClass seg_classify(const ScanArgs& a, u32 t, const
     sc.sp = sc.col = sc.eol = 0;
     sc.hi = false;
     if (s0 < bl) {
-        u32 c[16], eol16[4], sp16[4], col16[4];
+        u32 eol16[4], sp16[4], col16[4];
         u32 acc = 0;
 #pragma unroll
-        for (int qv = 0; qv < SEG / 16; ++qv) {
+        for (int qv = 0; qv < SEG / 16; ++qv) {  // class words live one quarter at a time
             const uint4 v = r.v[qv];
-            c[4 * qv] = classify4(v.x);
-            c[4 * qv + 1] = classify4(v.y);
-            c[4 * qv + 2] = classify4(v.z);
-            c[4 * qv + 3] = classify4(v.w);
-            eol16[qv] = gather16<0>(c[4 * qv], c[4 * qv + 1], c[4 * qv + 2], c[4 * qv + 3]);
-            sp16[qv] = gather16<2>(c[4 * qv], c[4 * qv + 1], c[4 * qv + 2], c[4 * qv + 3]);
-            col16[qv] = gather16<3>(c[4 * qv], c[4 * qv + 1], c[4 * qv + 2], c[4 * qv + 3]);
-            acc |= c[4 * qv] | c[4 * qv + 1] | c[4 * qv + 2] | c[4 * qv + 3];
+            const u32 c0 = classify4(v.x), c1 = classify4(v.y), c2 = classify4(v.z), c3 = classify4(v.w);
+            eol16[qv] = gather16<0>(c0, c1, c2, c3);
+            sp16[qv] = gather16<2>(c0, c1, c2, c3);
+            col16[qv] = gather16<3>(c0, c1, c2, c3);
+            acc |= c0 | c1 | c2 | c3;
         }
         auto join = [](const u32 (&g)[4]) {
             return ((u64)(g[2] | (g[3] << 16)) << 32) | (u64)(g[0] | (g[1] << 16));
@@ -548,13 +562,19 @@ __device__ __forceinline__ SegClass seg_classify(const ScanArgs& a, u32 t, const
         u64 eol = join(eol16), sp = join(sp16), col = join(col16);
         u64 tm = eol;
         if (__builtin_amdgcn_readfirstlane(__ballot((acc & 0x02020202u) != 0) != 0)) {
-            // '\r' somewhere in the wave (CRLF / CR files): a '\r' right before a '\n' ends no line
+            // '\r' somewhere in the wave (CRLF / CR files): a '\r' right before a '\n' ends no line.
+            // The segment (and the byte after it) is re-read from L2 here, so no class word has to
+            // stay live through the common path.
+            SegRegs q;
+            if (seg_in_range(a, t)) seg_fetch(a, t, q, tid, true, true);
+            else q = seg_load_tail(a, t, tid);
             u32 cr16[4];
 #pragma unroll
             for (int qv = 0; qv < SEG / 16; ++qv)
-                cr16[qv] = gather16<1>(c[4 * qv], c[4 * qv + 1], c[4 * qv + 2], c[4 * qv + 3]);
+                cr16[qv] = gather16<1>(classify4(q.v[qv].x), classify4(q.v[qv].y), classify4(q.v[qv].z),
+                                       classify4(q.v[qv].w));
             const u64 cr = join(cr16), nl = eol & ~cr;
-            const u64 nxt = (r.nx & 0xFFu) == (u32)'\n' ? 1ull : 0ull;
+            const u64 nxt = (q.nx & 0xFFu) == (u32)'\n' ? 1ull : 0ull;
             tm = eol & ~(cr & ((nl >> 1) | (nxt << 63)));
         }
         const u32 bvalid = bl - s0;
@@ -848,18 +868,22 @@ __device__ __forceinline__ bool uniform_flag(u32 v) { return __builtin_amdgcn_re
 // path, which reads them exactly).  Byte index i = (c >> 1) & 7 selects the expected byte
 // (A C T G - + - N) and its symbol (A1 C2 G3 T4 N5 +6); a byte is valid iff it equals the
 // expected one.
-__device__ __forceinline__ bool encode_glob(const ScanArgs& a, u64 tile0, u32 start, u32 n, u64& key) {
-    if (n < 1 || n > (u32)MAXSYM) return false;
+__device__ __forceinline__ void encode_load(const ScanArgs& a, u64 tile0, u32 start, u32 (&w)[8]) {
     const u64 base = (u64)(a.buf + tile0);
     const u32 lo = __builtin_amdgcn_readfirstlane((u32)base), hi = __builtin_amdgcn_readfirstlane((u32)(base >> 32));
     const u32 nrec = (u32)min(a.avail - tile0, (u64)0xFFFFFFF0u);
     const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(((u64)hi << 32) | lo), (short)0,
                                                         (int)__builtin_amdgcn_readfirstlane(nrec), 0x00020000);
     const u32 b4 = start & ~3u;
-    const u32 sh = start & 3u;
     const auto v0 = __builtin_amdgcn_raw_buffer_load_b128(rsrc, b4, 0, 0);
     const auto v1 = __builtin_amdgcn_raw_buffer_load_b128(rsrc, b4, 16, 0);
-    const u32 w[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+    w[0] = v0[0]; w[1] = v0[1]; w[2] = v0[2]; w[3] = v0[3];
+    w[4] = v1[0]; w[5] = v1[1]; w[6] = v1[2]; w[7] = v1[3];
+}
+
+__device__ __forceinline__ bool encode_pack(const u32 (&w)[8], u32 start, u32 n, u64& key) {
+    if (n < 1 || n > (u32)MAXSYM) return false;
+    const u32 sh = start & 3u;
     u64 kk = 0;
     u32 bad = 0;
 #pragma unroll
@@ -872,12 +896,18 @@ __device__ __forceinline__ bool encode_glob(const ScanArgs& a, u64 tile0, u32 st
         const u32 vm = left >= 4 ? 0xFFFFFFFFu : left <= 0 ? 0u : (0xFFFFFFFFu >> (32 - 8 * left));
         bad |= (expect ^ x) & vm;
         const u32 sv = sym & vm;
-        // four 3-bit symbols -> 12 bits: dot4 packs the first three, the fourth is shifted in
         const u32 packed = __builtin_amdgcn_udot4(sv, 0x00400801u, (sv >> 15) & 0xE00u, false);
         kk |= (u64)packed << (12 * k);
     }
     key = kk;
     return bad == 0;
+}
+
+__device__ __forceinline__ bool encode_glob(const ScanArgs& a, u64 tile0, u32 start, u32 n, u64& key) {
+    if (n < 1 || n > (u32)MAXSYM) return false;
+    u32 w[8];
+    encode_load(a, tile0, start, w);
+    return encode_pack(w, start, n, key);
 }
 
 // the rare header outcomes: word-scan fallback, no ' ' (IndexError), or an exotic code
@@ -952,9 +982,10 @@ __device__ __forceinline__ void process_header_bm(ScanShared& sh, const ScanArgs
 // this lane (the range's first byte by lane 0 of its first tile): parse it where it lies.  No
 // header list, no block scan: the tile's line prefix (seg_count) gives each lane its index.
 __device__ __forceinline__ void parse_own_headers(ScanShared& sh, const ScanArgs& a, u32 t, const TileCount& tc,
-                                                  u64 L0, int tid) {
+                                                  u64 L0, int tid, SegRegs& r, bool pf) {
     const u64 tile0 = (u64)t * TSTEP;
     const u32 nb = (u32)min((u64)(TILE + HALO), a.avail - tile0);
+    const u32 bl = min((u32)TILE, nb);
     const u32 rem = (u32)min(a.len - tile0, (u64)0xFFFFFFFFu);  // line starts p < rem lie in the range
     const u32 s0 = tid * SEG;
     const bool own0 = t == 0 && tid == 0 && a.own_start && (L0 & 3ull) == 0 && a.avail > 0 &&
@@ -967,22 +998,51 @@ __device__ __forceinline__ void parse_own_headers(ScanShared& sh, const ScanArgs
 #pragma unroll
     for (u32 q = 0; q < 3; ++q) m = q < skip ? (m & (m - 1)) : m;
     u64 rec = (lb + skip + 1u) >> 2;  // record index of the next candidate (-s)
-    int pend = own0 ? 0 : -1;
-    for (;;) {
-        if (pend < 0) {
-            if (!m) break;
-            const u32 p = s0 + (u32)__builtin_ctzll(m) + 1u;
-            m &= m - 1;
-            m &= m - 1;
-            m &= m - 1;
-            m &= m - 1;
-            const bool mine = p < rem || (a.own_end && tile0 + p == a.len && tile0 + p < a.avail);
-            if (!mine || (a.max_records > 0 && (i64)rec >= a.max_records)) break;  // so are all later ones
-            rec += 1;
-            pend = (int)p;
+    auto next = [&]() -> int {
+        if (!m) return -1;
+        const u32 p = s0 + (u32)__builtin_ctzll(m) + 1u;
+        m &= m - 1;
+        m &= m - 1;
+        m &= m - 1;
+        m &= m - 1;
+        const bool mine = p < rem || (a.own_end && tile0 + p == a.len && tile0 + p < a.avail);
+        if (!mine || (a.max_records > 0 && (i64)rec >= a.max_records)) {  // so are all later ones
+            m = 0;
+            return -1;
         }
-        process_header_bm(sh, a, tile0, (u32)pend, min((u32)TILE, nb));
-        pend = -1;
+        rec += 1;
+        return (int)p;
+    };
+    // The first header in two stages around the next tile's segment loads: its code-byte loads
+    // are issued before them (vector loads complete in order, so the parse never waits on the
+    // prefetch), and the prefetch's HBM latency overlaps the encode and the LDS insert.
+    const int p1 = own0 ? 0 : next();
+    u32 start = 0, n = 0;
+    int rr = 0;
+    u32 w[8];
+    if (p1 >= 0) {
+        rr = locate_code_bm(sh, (u32)p1, bl, start, n);
+        if (rr == 0 && (u64)(start & ~3u) + 32u > a.avail - tile0) rr = 2;  // loads would straddle the data end
+        if (rr == 0 && !(a.ablate & 2u)) encode_load(a, tile0, start, w);
+    }
+    // always five loads (zeros when there is no next tile or it reaches the data end), so the
+    // compiler's wait counts for the code bytes stay exact on every path
+    if (FR_PREFETCH) seg_fetch(a, t + 1, r, tid, pf);
+    if (p1 >= 0) {
+        if (rr == 0 && (a.ablate & 2u)) {
+            asm volatile("" ::"v"(start), "v"(n));
+        } else {
+            u64 key = 0;
+            const bool fast = rr == 0 && encode_pack(w, start, n, key);
+            if (fast) count_code(sh, a, tile0, (u32)p1, key);
+            else rare_push(sh, a, (u32)(tile0 + (u32)p1), (u32)rr, (u32)(tile0 + start), n);
+        }
+    }
+    if (p1 < 0) return;
+    for (;;) {
+        const int p = next();
+        if (p < 0) break;
+        process_header_bm(sh, a, tile0, (u32)p, bl);
     }
 }
 
@@ -998,13 +1058,22 @@ __device__ __forceinline__ u64 walk_chunk(ScanShared& sh, const ScanArgs& a, u32
     u64 tm0 = 0, tm1 = 0, tm2 = 0, tm3 = 0;
     const u64 w0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
 #endif
+#if FR_PREFETCH
+    // the next tile's segment is loaded during this tile's parse (parse_own_headers), so its HBM
+    // latency overlaps the parse; a tile reaching the data end is loaded bytewise instead
+    SegRegs r;
+    seg_fetch(a, tb, r, tid, tb < te && seg_in_range(a, tb));
+#endif
     for (u32 t = tb; t < te; ++t) {
 #if FR_TIMING
         const u64 c0 = __builtin_amdgcn_s_memtime();
 #endif
+#if FR_PREFETCH
+        if (!seg_in_range(a, t)) r = seg_load_tail(a, t, tid);
+#else
         SegRegs r;
-        if ((u64)t * TSTEP + (TILE + HALO + SEG + 4) <= a.avail) seg_fetch(a, t, r, tid);
-        else r = seg_load_tail(a, t, tid);  // the data end: bytewise, zeros past it
+        seg_prefetch_next(a, t, r, tid);
+#endif
         const SegClass sc = seg_classify(a, t, r, tid);
 #if FR_TIMING
         __builtin_amdgcn_s_waitcnt(0);
@@ -1024,8 +1093,11 @@ __device__ __forceinline__ u64 walk_chunk(ScanShared& sh, const ScanArgs& a, u32
         const u64 c2 = __builtin_amdgcn_s_memtime();
 #endif
         const TileCount tc = seg_count(sh, sc, wid);
+        const bool pf = t + 1 < te && seg_in_range(a, t + 1);
         if (parse && !uniform_flag(sh.spec_bad) && !(a.ablate & 1u))
-            parse_own_headers(sh, a, t, tc, L0 + lines, tid);
+            parse_own_headers(sh, a, t, tc, L0 + lines, tid, r, pf);
+        else if (FR_PREFETCH)
+            seg_fetch(a, t + 1, r, tid, pf);
         lines += tc.tot;
 #if FR_TIMING
         __builtin_amdgcn_s_waitcnt(0);
@@ -1143,7 +1215,8 @@ __device__ __forceinline__ void chunk_bounds(const ScanArgs& a, u32 c, u32& tb, 
 }
 
 #ifndef FR_OCC
-#define FR_OCC 4  // workgroups (= waves per SIMD) per CU (~22.5 KB LDS would allow 7; measured best at 4); fr_api
+#define FR_OCC 5  // workgroups (= waves per SIMD) per CU: 5 caps the kernel at 96 VGPRs (LDS would allow 7;
+                  // measured best at 5, with the '\r' path re-reading its segment so no class word stays live); fr_api
                   // sizes the grid with fr_chunk_occupancy()
 #endif
 __global__ __launch_bounds__(WG, FR_OCC) void chunk_kernel(ScanArgs args) {
@@ -1154,7 +1227,7 @@ __global__ __launch_bounds__(WG, FR_OCC) void chunk_kernel(ScanArgs args) {
     __shared__ ScanShared sh;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    const int wid = tid >> 6;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: LDS addresses by wave stay scalar
     for (int i = tid; i < NS; i += WG) {
         sh.ls[i] = LSlot{0, 0, 0xFFFFFFFFu};
     }

@@ -186,10 +186,11 @@ struct ScanShared {
     u32 chunk;
     int phase;        // guessed line phase (lines before the chunk, mod 4), -1 unsure
     u32 exo_p[EXO_BUF], exo_start[EXO_BUF], exo_len[EXO_BUF];
-    u64 bsp[WG];      // per 64-B segment of the staged tile: ' ' bitmap (phase inference: the
+    u64 bsp[WG + 1];  // per 64-B segment of the staged tile: ' ' bitmap (phase inference: the
                       // line-terminator bitmap of a chunk's first tile)
-    u64 bcol[WG];     //                                      ':' bitmap
-    u64 beol[WG];     //                                      '\r' | '\n' bitmap
+    u64 bcol[WG + 1]; //                                      ':' bitmap
+    u64 beol[WG + 1]; //                                      '\r' | '\n' bitmap
+                      // entry WG of each stays zero: the window's second segment past the tile
 };
 
 __device__ __forceinline__ u64 make_ord(const ScanArgs& a, u64 off_in_range) {
@@ -917,45 +918,44 @@ __device__ FR_COLD void slow_header(ScanShared& sh, const ScanArgs& a, u64 tile0
     else exotic_record(a, tile0, p, start, n, sh);
 }
 
-// bits [0, k) of a 128-bit window (k in [0, 128])
-__device__ __forceinline__ void below128(u32 k, u64& lo, u64& hi) {
-    lo = k >= 64u ? ~0ull : ((1ull << k) - 1ull);
-    hi = k <= 64u ? 0ull : (k >= 128u ? ~0ull : ((1ull << (k - 64u)) - 1ull));
+// lowest set bit of a 128-bit window, >= 128 when empty (v_ffbl gives ~0 for a zero word, and
+// OR-ing the word's base keeps ~0, so a min over the four words needs no select)
+__device__ __forceinline__ u32 ctz128(u64 lo, u64 hi) {
+    const u32 a = (u32)__builtin_ctzg((u32)lo, -1), b = (u32)__builtin_ctzg((u32)(lo >> 32), -1) | 32u;
+    const u32 c = (u32)__builtin_ctzg((u32)hi, -1) | 64u, d = (u32)__builtin_ctzg((u32)(hi >> 32), -1) | 96u;
+    return min(min(a, b), min(c, d));
 }
 
-__device__ __forceinline__ u32 first128(u64 lo, u64 hi) {  // lowest set bit (window non-empty)
-    return lo ? (u32)__builtin_ctzll(lo) : 64u + (u32)__builtin_ctzll(hi);
+// leading zeros of a 128-bit window counted from bit 127, ~0 when empty
+__device__ __forceinline__ u32 clz128(u64 lo, u64 hi) {
+    const u32 a = (u32)__builtin_clzg((u32)(hi >> 32), -1), b = (u32)__builtin_clzg((u32)hi, -1) | 32u;
+    const u32 c = (u32)__builtin_clzg((u32)(lo >> 32), -1) | 64u, d = (u32)__builtin_clzg((u32)lo, -1) | 96u;
+    return min(min(a, b), min(c, d));
 }
 
 // returns 0 parsed (code at [start, start+n)), 1 no ' ' on the line, 2 fall back to the word scan.
-// The line's bitmaps are read as one 128-bit window (two segments, six independent LDS reads,
-// one round trip); lines whose code does not end inside the window take the word scan.
+// The line's bitmaps are read as one 128-bit window (segments w and w+1; past the tile the second
+// is the zero entry), branch-free: the first ' ' / line end f1, the token end f2 (the next one),
+// and the last ':' below f2 (one at or before f1 leaves the code right after f1).  Lines whose
+// code does not end inside the window take the word scan.
 __device__ __forceinline__ int locate_code_bm(const ScanShared& sh, u32 p, u32 bl, u32& start, u32& n) {
     if (p >= bl) return 2;
     const u32 w = p >> 6, b = p & 63u;
-    const bool has1 = (w + 1u) * 64u < bl;
-    const u32 wn = has1 ? w + 1u : w;
+    const u32 wn = (w + 1u) * 64u < bl ? w + 1u : (u32)WG;
     const u64 s0 = sh.bsp[w], s1 = sh.bsp[wn], e0 = sh.beol[w], e1 = sh.beol[wn];
-    u64 c0 = sh.bcol[w], c1 = sh.bcol[wn];
-    // window positions are relative to segment w: [b, 64) of it, then segment w+1
-    u64 v0 = (s0 | e0) & (~0ull << b), v1 = has1 ? (s1 | e1) : 0ull;
-    if (!(v0 | v1)) return 2;
-    const u32 f1 = first128(v0, v1);                       // the first ' ' or line end
-    if ((f1 < 64u ? (e0 >> f1) : (e1 >> (f1 - 64u))) & 1ull) return 1;
-    u64 m0, m1;
-    below128(f1 + 1u, m0, m1);                             // drop bits [0, f1]
-    v0 &= ~m0;
-    v1 &= ~m1;
-    if (!(v0 | v1)) return 2;
-    const u32 f2 = first128(v0, v1);                       // the token's end
-    u64 k0, k1;
-    below128(f2, k0, k1);
-    c0 &= k0 & ~m0;                                        // ':' strictly inside (f1, f2)
-    c1 = has1 ? (c1 & k1 & ~m1) : 0ull;
-    const u32 lastc = c1 ? 127u - (u32)__builtin_clzll(c1) : c0 ? 63u - (u32)__builtin_clzll(c0) : f1;
+    const u64 c0 = sh.bcol[w], c1 = sh.bcol[wn];
+    const u64 v0 = (s0 | e0) & (~0ull << b), v1 = s1 | e1;  // window positions relative to segment w
+    const u32 f1 = ctz128(v0, v1);
+    const u64 v0b = v0 & (v0 - 1ull), v1b = v0 ? v1 : (v1 & (v1 - 1ull));  // drop bit f1
+    const u32 f2 = ctz128(v0b, v1b);
+    const bool at_eol = (((f1 < 64u ? e0 : e1) >> (f1 & 63u)) & 1ull) != 0;
+    const u64 t = (1ull << (f2 & 63u)) - 1ull;              // colons below f2
+    const u64 k0 = f2 >= 64u ? ~0ull : t, k1 = f2 >= 64u ? t : 0ull;
+    const u32 hc = clz128(c0 & k0, c1 & k1) ^ 127u;         // highest such colon (negative if none)
+    const u32 lastc = (u32)max((int)f1, (int)hc);
     start = w * 64u + lastc + 1u;
     n = f2 - lastc - 1u;
-    return 0;
+    return f1 >= 128u ? 2 : at_eol ? 1 : f2 >= 128u ? 2 : 0;
 }
 
 // R2 via the tile's ' ' / ':' / line-end bitmaps: first ' ', then the next ' ' or line end,
@@ -992,21 +992,26 @@ __device__ __forceinline__ void parse_own_headers(ScanShared& sh, const ScanArgs
                       (a.max_records <= 0 || (i64)(L0 >> 2) < a.max_records);
     // the i-th terminator (from 0) of this segment starts line lb + i + 1: a header line when
     // i = 3 - lb (mod 4); skip to the first such terminator, then step four at a time
-    const u64 lb = L0 + tc.wexcl + (tc.x - tc.c);
-    const u32 skip = (3u - (u32)lb) & 3u;
+    const u32 lb32 = (u32)L0 + tc.wexcl + (tc.x - tc.c);  // the phase needs the low bits only
+    const u32 skip = (3u - lb32) & 3u;
     u64 m = tc.tmask;
 #pragma unroll
     for (u32 q = 0; q < 3; ++q) m = q < skip ? (m & (m - 1)) : m;
-    u64 rec = (lb + skip + 1u) >> 2;  // record index of the next candidate (-s)
+    const bool limited = a.max_records > 0;  // -s: uniform
+    u64 rec = limited ? (L0 + tc.wexcl + (tc.x - tc.c) + skip + 1u) >> 2 : 0ull;  // next candidate's record
     auto next = [&]() -> int {
         if (!m) return -1;
         const u32 p = s0 + (u32)__builtin_ctzll(m) + 1u;
-        m &= m - 1;
-        m &= m - 1;
-        m &= m - 1;
-        m &= m - 1;
+        if (__builtin_popcountll(m) > 4) {  // another header in this segment (short records)
+            m &= m - 1;
+            m &= m - 1;
+            m &= m - 1;
+            m &= m - 1;
+        } else {
+            m = 0;
+        }
         const bool mine = p < rem || (a.own_end && tile0 + p == a.len && tile0 + p < a.avail);
-        if (!mine || (a.max_records > 0 && (i64)rec >= a.max_records)) {  // so are all later ones
+        if (!mine || (limited && (i64)rec >= a.max_records)) {  // so are all later ones
             m = 0;
             return -1;
         }
@@ -1232,6 +1237,9 @@ __global__ __launch_bounds__(WG, FR_OCC) void chunk_kernel(ScanArgs args) {
         sh.ls[i] = LSlot{0, 0, 0xFFFFFFFFu};
     }
     if (tid == 0) {
+        sh.bsp[WG] = 0;
+        sh.bcol[WG] = 0;
+        sh.beol[WG] = 0;
         sh.nkeys = 0;
         sh.created = 0;
         sh.flags = 0;

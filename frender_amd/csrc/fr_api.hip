@@ -31,6 +31,7 @@ struct fr_ctx {
 
     DevState* st = nullptr;
     DevState* h_st = nullptr;      // pinned snapshot
+    DevState* h_zero = nullptr;    // pinned reset image (zero counters, no error), never modified
     bool st_fresh = false;         // h_st equals the device state (no device work on it since)
     Table* d_tab = nullptr;        // device copy of tab for the tally kernel
     Table* h_tab = nullptr;        // pinned staging of that copy (last uploaded value)
@@ -67,6 +68,7 @@ struct fr_ctx {
     bool file_open = false;
     u32 file_tag = 0;
     bool merged = false;  // the table holds ordinals merged from other contexts (any file tag)
+    u64 max_file_bytes = 0;  // bytes of the longest file tallied since fr_reset (ordinal offsets are below it)
     u64 file_offset = 0;
     i64 max_records = 0;
     int last_byte = -1;
@@ -85,6 +87,7 @@ struct fr_ctx {
     u8* d_sheet = nullptr;  // one device blob holding every sheet array above
     u8* h_sheet = nullptr;  // its pinned staging copy
     u64 sheet_cap = 0;
+    u64 sheet_bytes = 0;  // the blob last uploaded (h_sheet holds it)
     int cp_stride = 0;
 
     // finalized table
@@ -143,13 +146,11 @@ static u64 pow2_at_least(u64 x) {
 }
 
 static int state_reset_counts(fr_ctx* ctx) {
-    DevState z;
-    std::memset(&z, 0, sizeof(z));
-    z.err_nospace = ~0ull;
-    CK(hipStreamSynchronize(ctx->stream));
-    *ctx->h_st = z;
-    CK(hipMemcpyAsync(ctx->st, ctx->h_st, sizeof(DevState), hipMemcpyHostToDevice, ctx->stream));
-    CK(hipStreamSynchronize(ctx->stream));
+    // the device copy comes from a pinned image that never changes, so nothing waits for it; the
+    // host snapshot is overwritten only once no asynchronous snapshot can still land on it
+    if (ctx->st_pending) CK(hipStreamSynchronize(ctx->stream));
+    *ctx->h_st = *ctx->h_zero;
+    CK(hipMemcpyAsync(ctx->st, ctx->h_zero, sizeof(DevState), hipMemcpyHostToDevice, ctx->stream));
     ctx->st_pending = false;
     ctx->st_fresh = true;
     return FR_OK;
@@ -308,6 +309,7 @@ static int launch_range(fr_ctx* ctx, const u8* dptr, u64 len, u64 avail, int own
     ctx->scan_bytes += len;
     ctx->par ^= 1u;
     ctx->file_offset += len;
+    ctx->max_file_bytes = std::max(ctx->max_file_bytes, ctx->file_offset);  // bounds every ordinal's offset
     return snapshot_async(ctx);
 }
 
@@ -349,6 +351,10 @@ fr_ctx* fr_create(int device, uint64_t chunk_bytes, uint64_t table_slots) {
     std::memset(ctx->h_tab, 0, sizeof(Table));
     if ((e = hipHostMalloc((void**)&ctx->h_st, sizeof(DevState), hipHostMallocDefault)) != hipSuccess)
         return bad("pinned state", e);
+    if ((e = hipHostMalloc((void**)&ctx->h_zero, sizeof(DevState), hipHostMallocDefault)) != hipSuccess)
+        return bad("pinned reset state", e);
+    std::memset(ctx->h_zero, 0, sizeof(DevState));
+    ctx->h_zero->err_nospace = ~0ull;
     if ((e = hipEventCreateWithFlags(&ctx->st_ev, hipEventDisableTiming)) != hipSuccess) return bad("event", e);
     if ((e = dalloc(&ctx->tiles, ctx->tiles_cap)) != hipSuccess) return bad("tiles", e);
     if ((e = dalloc(&ctx->chunk_info, ctx->tiles_cap)) != hipSuccess) return bad("chunk info", e);
@@ -395,6 +401,7 @@ void fr_destroy(fr_ctx* ctx) {
     for (void* p : dev)
         if (p) (void)hipFree(p);
     if (ctx->h_st) (void)hipHostFree(ctx->h_st);
+    if (ctx->h_zero) (void)hipHostFree(ctx->h_zero);
     if (ctx->h_sheet) (void)hipHostFree(ctx->h_sheet);
     if (ctx->h_tab) (void)hipHostFree(ctx->h_tab);
     for (int i = 0; i < 2; ++i) {
@@ -461,18 +468,8 @@ int fr_set_sheet(fr_ctx* ctx, int S, const uint64_t* idx1_packed, const int32_t*
     const u64 o_cp1 = o_name + al(S * 4ull), o_cp2 = o_cp1 + al(ncp * 4), o_cp2rc = o_cp2 + al(ncp * 4);
     const u64 o_l1 = o_cp2rc + al(ncp * 4), o_l2 = o_l1 + (with_cp ? al(S * 4ull) : 0);
     const u64 total = o_l2 + (with_cp ? al(S * 4ull) : 0) + 8;
-    CK(hipStreamSynchronize(ctx->stream));  // the previous sheet may still be in use / in flight
-    if (total > ctx->sheet_cap) {
-        if (ctx->d_sheet) CK(hipFree(ctx->d_sheet));
-        if (ctx->h_sheet) CK(hipHostFree(ctx->h_sheet));
-        ctx->d_sheet = nullptr;
-        ctx->h_sheet = nullptr;
-        const u64 cap = std::max<u64>(total * 2, 4096);
-        CK(hipMalloc(&ctx->d_sheet, cap));
-        CK(hipHostMalloc(&ctx->h_sheet, cap, hipHostMallocDefault));
-        ctx->sheet_cap = cap;
-    }
-    u8* h = ctx->h_sheet;
+    std::vector<u8> blob(total, 0);
+    u8* h = blob.data();
     if (S) {
         std::memcpy(h, idx1_packed, S * 8ull);
         std::memcpy(h + o_i2, idx2_packed, S * 8ull);
@@ -486,7 +483,24 @@ int fr_set_sheet(fr_ctx* ctx, int S, const uint64_t* idx1_packed, const int32_t*
         std::memcpy(h + o_l1, idx1_len, S * 4ull);
         std::memcpy(h + o_l2, idx2_len, S * 4ull);
     }
-    CK(hipMemcpyAsync(ctx->d_sheet, h, total, hipMemcpyHostToDevice, ctx->stream));
+    // the same sheet again (pass B without rc rows, repeated scans): the device copy is current
+    const bool same = ctx->h_sheet && total == ctx->sheet_bytes && std::memcmp(h, ctx->h_sheet, total) == 0;
+    if (!same) {
+        CK(hipStreamSynchronize(ctx->stream));  // the previous sheet may still be in use / in flight
+        if (total > ctx->sheet_cap) {
+            if (ctx->d_sheet) CK(hipFree(ctx->d_sheet));
+            if (ctx->h_sheet) CK(hipHostFree(ctx->h_sheet));
+            ctx->d_sheet = nullptr;
+            ctx->h_sheet = nullptr;
+            const u64 cap = std::max<u64>(total * 2, 4096);
+            CK(hipMalloc(&ctx->d_sheet, cap));
+            CK(hipHostMalloc(&ctx->h_sheet, cap, hipHostMallocDefault));
+            ctx->sheet_cap = cap;
+        }
+        std::memcpy(ctx->h_sheet, h, total);
+        ctx->sheet_bytes = total;
+        CK(hipMemcpyAsync(ctx->d_sheet, ctx->h_sheet, total, hipMemcpyHostToDevice, ctx->stream));
+    }
     u8* d = ctx->d_sheet;
     ctx->d_i1 = (u64*)d;
     ctx->d_i2 = (u64*)(d + o_i2);
@@ -521,6 +535,7 @@ int fr_reset(fr_ctx* ctx) {
     ctx->file_open = false;
     ctx->file_tag = 0;
     ctx->merged = false;
+    ctx->max_file_bytes = 0;
     ctx->par = 0;
     ctx->U = 0;
     ctx->n_pres = 0;
@@ -770,14 +785,24 @@ int fr_finalize(fr_ctx* ctx, uint64_t* n_unique, uint64_t* n_presence, uint64_t*
     CK(hipMemsetAsync(ctx->d_counter, 0, sizeof(u64), ctx->stream));
     CK(launch_compact(ctx->tab.slots, ctx->nslots, ctx->d_keys, ctx->d_counts, ctx->d_first, ctx->d_pos,
                       ctx->d_counter, ctx->stream));
-    // ordinals are < (file_tag + 1) << ORD_SHIFT: sort only the bits that can be set
-    int end_bit = 64;
+    // ordinals are < (file_tag + 1) << ORD_SHIFT: sort only the bits that can be set.  Without
+    // merged rows every ordinal is a record start of this context's files, and records span at
+    // least 4 bytes (four line terminators), so bits [0, 2) never decide the order; with one file
+    // the ordinal is its byte offset (file tag 1 sits above every offset bit).  100M SYN-v1 reads
+    // (7.4 GB): bits [2, 33), 4 radix passes instead of 6.
+    int begin_bit = 0, end_bit = 64;
     if (!ctx->merged) {
+        begin_bit = 2;
         end_bit = ORD_SHIFT;
         while (end_bit < 64 && ((u64)ctx->file_tag >> (end_bit - ORD_SHIFT)) != 0) ++end_bit;
+        if (ctx->file_tag == 1) {
+            end_bit = begin_bit + 1;
+            while (end_bit < ORD_SHIFT && (ctx->max_file_bytes >> end_bit) != 0) ++end_bit;
+        }
     }
     size_t need = 0;
-    CK(launch_order(ctx->d_first, ctx->d_pos, nk, ctx->d_first_s, ctx->d_perm, nullptr, &need, end_bit, ctx->stream));
+    CK(launch_order(ctx->d_first, ctx->d_pos, nk, ctx->d_first_s, ctx->d_perm, nullptr, &need, begin_bit, end_bit,
+                    ctx->stream));
     if (need > ctx->temp_bytes) {
         if (ctx->d_temp) CK(hipFree(ctx->d_temp));
         CK(hipMalloc(&ctx->d_temp, need));
@@ -785,8 +810,8 @@ int fr_finalize(fr_ctx* ctx, uint64_t* n_unique, uint64_t* n_presence, uint64_t*
     }
     size_t tb = ctx->temp_bytes;
     if (nk)
-        CK(launch_order(ctx->d_first, ctx->d_pos, nk, ctx->d_first_s, ctx->d_perm, ctx->d_temp, &tb, end_bit,
-                        ctx->stream));
+        CK(launch_order(ctx->d_first, ctx->d_pos, nk, ctx->d_first_s, ctx->d_perm, ctx->d_temp, &tb, begin_bit,
+                        end_bit, ctx->stream));
     CK(launch_gather(ctx->d_perm, nk, ctx->d_keys, ctx->d_counts, ctx->d_keys_s, ctx->d_counts_s, ctx->d_rank,
                      ctx->stream));
     CK(launch_set_uidx(ctx->tab.slots, ctx->tab.mask, ctx->d_keys_s, nk, ctx->d_rank, ctx->stream));

@@ -172,7 +172,7 @@ hipError_t launch_compact(const GSlot* slots, u64 nslots, u64* keys, u64* counts
 hipError_t launch_set_uidx(GSlot* slots, u64 mask, const u64* keys, u64 n, const u32* rank_of_pos,
                            hipStream_t s);
 hipError_t launch_order(const u64* first_in, const u32* pos_in, u64 n, u64* first_out, u32* perm_out,
-                        void* temp, size_t* temp_bytes, int end_bit, hipStream_t s);
+                        void* temp, size_t* temp_bytes, int begin_bit, int end_bit, hipStream_t s);
 hipError_t launch_gather(const u32* perm, u64 n, const u64* keys, const u64* counts, u64* keys_o,
                          u64* counts_o, u32* rank, hipStream_t s);
 hipError_t launch_presence_map(const GSlot* slots, u64 mask, const Presence* pres, u64 n, u32* uidx,

@@ -1463,9 +1463,9 @@ hipError_t launch_compact(const GSlot* slots, u64 nslots, u64* keys, u64* counts
 }
 
 hipError_t launch_order(const u64* first_in, const u32* pos_in, u64 n, u64* first_out, u32* perm_out, void* temp,
-                        size_t* temp_bytes, int end_bit, hipStream_t s) {
-    return rocprim::radix_sort_pairs(temp, *temp_bytes, first_in, first_out, pos_in, perm_out, (size_t)n, 0,
-                                     (unsigned)end_bit, s);
+                        size_t* temp_bytes, int begin_bit, int end_bit, hipStream_t s) {
+    return rocprim::radix_sort_pairs(temp, *temp_bytes, first_in, first_out, pos_in, perm_out, (size_t)n,
+                                     (unsigned)begin_bit, (unsigned)end_bit, s);
 }
 
 __global__ void gather_kernel(const u32* perm, u64 n, const u64* keys, const u64* counts, u64* keys_o,

@@ -33,9 +33,12 @@ constexpr u64 HOST_CHUNK_MAX = 1ull << 30;  // bytes per host-fed launch (pinned
 constexpr u32 SPIN_MAX = 1u << 24;   // look-back spin bound (then FR_ERR_DEVICE)
 constexpr int ORD_SHIFT = 44;        // ordinal = file_tag << 44 | file byte offset
 constexpr int EXO_BUF = 32;          // chunk kernel: exotic records buffered while speculating
-constexpr int PHASE_LINES = 24;
+#ifndef FR_PHASE_LINES
+#define FR_PHASE_LINES 24
+#endif
+constexpr int PHASE_LINES = FR_PHASE_LINES;  // lines the chunk phase guess looks at (>= 8)
 constexpr u32 RARE_RING = 8192;      // chunk kernel: rare events queued per workgroup between drains
-                                     // (<= TILE/4 + 1 headers and WG UTF-8 checks per tile)      // chunk kernel: lines inspected to guess a chunk's line phase
+                                     // (<= TILE/4 + 1 headers and WG UTF-8 checks per tile)
 
 // ---- HBM structures ---------------------------------------------------------------
 struct alignas(32) GSlot {           // open-addressing slot, one 32-B sector

@@ -1,5 +1,6 @@
 """`python -m frender_amd scan|demux ...` — the reference's CLI (frender.py:817-930) on MI355X."""
 import argparse
+import os
 import sys
 from datetime import datetime, timezone
 
@@ -21,6 +22,8 @@ def main(argv=None):
                    help="When matching sample ids to filenames, remove this prefix from the sample id")
     p.add_argument("-b", metavar="barcode_table",
                    help=".csv barcode association table; required unless a directory holding one is given")
+    p.add_argument("--gpus", type=int, default=1,
+                   help="GPUs (one process each; files are sharded over them, rank 0 writes the outputs)")
     p.add_argument("files", nargs="+", help="Fastq file(s) or a directory of fastq files")
     p.set_defaults(cmd="scan")
     d = sub.add_parser("demux", help="Demultiplex paired fastq files using a frender scan result file")
@@ -43,6 +46,10 @@ def main(argv=None):
     d.set_defaults(cmd="demux")
     args = parser.parse_args(argv)
     if getattr(args, "cmd", None) == "scan":
+        if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+            return launch_ranks(args.gpus, sys.argv[1:] if argv is None else list(argv))
+        if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+            return run_rank(args)
         from .scan import frender_scan
         frender_scan(args)
         return 0
@@ -52,6 +59,61 @@ def main(argv=None):
         return 0
     parser.print_help()
     return 2
+
+
+def launch_ranks(n: int, argv: list) -> int:
+    """`scan --gpus N`: one child process per GPU (this process never touches a GPU), joined by
+    torch.distributed over 127.0.0.1; rank 0's stdout is the command's.  A rank that fails ends the
+    others; the exit status is rank 0's, or the first failure's."""
+    import socket
+    import subprocess
+    import time
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-m", "frender_amd", *argv], env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    codes = [None] * n
+    while any(c is None for c in codes):
+        for r, p in enumerate(procs):
+            if codes[r] is None:
+                codes[r] = p.poll()
+        if any(c not in (None, 0) for c in codes):  # a failed rank: the others cannot finish
+            time.sleep(2)
+            for r, p in enumerate(procs):
+                if p.poll() is None:
+                    p.terminate()
+            for r, p in enumerate(procs):
+                codes[r] = p.wait()
+            break
+        time.sleep(0.05)
+    return codes[0] if codes[0] else next((c for c in codes if c), 0)
+
+
+def run_rank(args) -> int:
+    """One rank of a multi-GPU scan (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* from the launcher or
+    torchrun): RCCL between GPUs (FRENDER_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs)."""
+    import torch
+    import torch.distributed as dist
+
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("FRENDER_DIST_BACKEND", "nccl")
+    if backend == "nccl":
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        dist.init_process_group(backend)
+    try:
+        from .scan import frender_scan
+        frender_scan(args)
+    finally:
+        dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":

@@ -35,7 +35,7 @@ class FrenderError(RuntimeError):
 
 class FileStats(C.Structure):
     _fields_ = [("records", C.c_uint64), ("lines", C.c_uint64), ("new_keys", C.c_uint64),
-                ("exotic", C.c_uint64), ("error", C.c_int32), ("pad", C.c_int32),
+                ("exotic", C.c_uint64), ("error", C.c_int32), ("utf8_bad", C.c_int32),
                 ("error_offset", C.c_uint64)]
 
 
@@ -60,13 +60,15 @@ _SIGS = {
     "fr_set_sheet": (C.c_int, [P, C.c_int, P, P, P, P, P, P, C.c_int, P, P, P, C.c_int]),
     "fr_reset": (C.c_int, [P]),
     "fr_begin_file": (C.c_int, [P, C.c_int64]),
+    "fr_begin_file_at": (C.c_int, [P, C.c_int64, C.c_uint64, C.c_int64]),
     "fr_feed": (C.c_int, [P, P, C.c_uint64]),
     "fr_feed_device": (C.c_int, [P, P, C.c_uint64]),
     "fr_end_file": (C.c_int, [P, C.POINTER(FileStats)]),
     "fr_finalize": (C.c_int, [P, u64p, u64p, u64p]),
     "fr_get_unique": (C.c_int, [P, P, P, P]),
     "fr_get_presence": (C.c_int, [P, P, P]),
-    "fr_get_exotic": (C.c_int, [P, C.c_uint64, C.c_uint64, P, P, P, P, C.c_uint64, u64p]),
+    "fr_exotic_sizes": (C.c_int, [P, u64p, u64p, u64p]),
+    "fr_get_exotic_table": (C.c_int, [P, P, P, P, P, P, P]),
     "fr_classify": (C.c_int, [P, C.c_int, C.c_int, P, P, P, P, P, P, P, P, P]),
     "fr_rc_counts": (C.c_int, [P, P, P]),
     "fr_classify_cp": (C.c_int, [P, C.c_int, P, P, P, P, C.c_int, C.c_int, C.c_int, P, P, P, P, P, P, P, P]),
@@ -105,15 +107,62 @@ def _ptr(a: np.ndarray | None):
 
 M21 = np.arange(21, dtype=np.uint64) * np.uint64(3)
 SYM_LUT = np.frombuffer(b"\0ACGTN+\0", dtype=np.uint8)
+WIDE_BIT = np.uint64(1 << 63)
+WIDE_MAXN, WIDE_NOPLUS = 24, 31
+WIDE_OFF = np.array([(5 ** n - 1) // 4 for n in range(WIDE_MAXN + 2)], dtype=np.uint64)  # length offsets
+
+
+def _decode_wide(keys: np.ndarray) -> list:
+    """Wide keys (include/frender_amd.h) -> code strings, vectorised over the keys."""
+    V = keys & np.uint64((1 << 57) - 1)
+    plus = ((keys >> np.uint64(57)) & np.uint64(31)).astype(np.int64)
+    lower = ((keys >> np.uint64(62)) & np.uint64(1)).astype(bool)
+    n = np.searchsorted(WIDE_OFF, V, side="right") - 1  # letters: the largest n with off[n] <= V
+    D = V - WIDE_OFF[n]
+    digits = np.empty((keys.size, WIDE_MAXN), dtype=np.uint8)
+    for i in range(WIDE_MAXN):
+        digits[:, i] = (D % np.uint64(5)).astype(np.uint8)
+        D //= np.uint64(5)
+    up = np.frombuffer(b"ACGTN", dtype=np.uint8)[digits]
+    out = []
+    for r, k, p, lo in zip(up.view(f"S{WIDE_MAXN}").ravel().tolist(), n.tolist(), plus.tolist(), lower.tolist()):
+        s = r[:k].decode("ascii")
+        if p != WIDE_NOPLUS:
+            s = s[:p] + "+" + s[p:]
+        out.append(s.lower() if lo else s)
+    return out
 
 
 def decode_keys(keys: np.ndarray) -> list:
-    """3-bit packed fast keys -> code strings (char i at bits [3i, 3i+3))."""
+    """Packed keys -> code strings: fast keys 3 bits per char (char i at bits [3i, 3i+3)), wide
+    keys (bit 63) base 5 per letter (include/frender_amd.h)."""
     if keys.size == 0:
         return []
+    wide = (keys & WIDE_BIT) != 0
     syms = ((keys[:, None] >> M21[None, :]) & np.uint64(7)).astype(np.uint8)
     raw = np.ascontiguousarray(SYM_LUT[syms]).view("S21").ravel()
-    return [b.decode("ascii") for b in raw.tolist()]
+    out = [b.decode("ascii") for b in raw.tolist()]
+    if wide.any():
+        w = np.nonzero(wide)[0]
+        for i, c in zip(w.tolist(), _decode_wide(keys[w])):
+            out[i] = c
+    return out
+
+
+def encode_wide(code: str):
+    """The wide key of a code (None outside the wide form): the host statement of wide_encode in
+    fr_kernels.hip, for tests and the demux results table."""
+    if not 1 <= len(code) <= WIDE_MAXN + 1 or code.count("+") > 1:
+        return None
+    letters = code.replace("+", "")
+    if not letters or not (set(letters) <= set("ACGTN") or set(letters) <= set("acgtn")):
+        return None
+    p = code.find("+")
+    n1, n2 = (len(letters), 0) if p < 0 else (p, len(letters) - p)
+    if len(letters) > WIDE_MAXN or n1 > 21 or n2 > 21:
+        return None
+    v = sum("acgtn".index(ch) * 5 ** i for i, ch in enumerate(letters.lower())) + (5 ** len(letters) - 1) // 4
+    return (1 << 63) | (int(letters.islower()) << 62) | ((WIDE_NOPLUS if p < 0 else p) << 57) | v
 
 
 def pack_lower(s: str) -> int:
@@ -285,8 +334,14 @@ class Context:
     def reset(self):
         self._ck(lib.fr_reset(self.h), "fr_reset")
 
-    def begin_file(self, max_records: int | None):
-        self._ck(lib.fr_begin_file(self.h, int(max_records or 0)), "fr_begin_file")
+    def begin_file(self, max_records: int | None, file_index: int | None = None, byte_base: int = 0):
+        """Open the next file (or, for sharded scans, file `file_index` of the whole scan from byte
+        `byte_base` on: fr_begin_file_at)."""
+        if file_index is None and not byte_base:
+            self._ck(lib.fr_begin_file(self.h, int(max_records or 0)), "fr_begin_file")
+        else:
+            self._ck(lib.fr_begin_file_at(self.h, int(file_index or 0), int(byte_base), int(max_records or 0)),
+                     "fr_begin_file_at")
 
     def feed(self, data) -> bool:
         """Feed decoded bytes; returns True once the -s sample limit is reached."""
@@ -326,22 +381,23 @@ class Context:
         self._ck(lib.fr_get_presence(self.h, _ptr(u), _ptr(f)), "fr_get_presence")
         return u, f
 
-    def exotic(self, first: int, count: int):
-        """Exotic records [first, first+count): (ordinals, lengths, pool offsets, pool)."""
-        ords = np.empty(count, dtype=np.uint64)
-        lens = np.empty(count, dtype=np.uint32)
-        offs = np.empty(count, dtype=np.uint64)
-        got = C.c_uint64()
-        self._ck(lib.fr_get_exotic(self.h, first, count, _ptr(ords), _ptr(lens), _ptr(offs), None, 0,
-                                   C.byref(got)), "fr_get_exotic")
-        k = got.value
-        ords, lens, offs = ords[:k], lens[:k], offs[:k]
-        pool_bytes = int((offs + lens).max()) if k else 0
-        pool = np.empty(max(pool_bytes, 1), dtype=np.uint8)
-        if pool_bytes:
-            self._ck(lib.fr_get_exotic(self.h, first, 0, None, None, None, _ptr(pool), pool_bytes, None),
-                     "fr_get_exotic")
-        return ords, lens, offs, pool
+    def exotic_table(self):
+        """The scan's exotic codes aggregated by the library: (codes as bytes, counts, first
+        ordinals, presence code indices, presence file indices)."""
+        n, nb, npres = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        self._ck(lib.fr_exotic_sizes(self.h, C.byref(n), C.byref(nb), C.byref(npres)), "fr_exotic_sizes")
+        counts = np.empty(n.value, np.uint64)
+        first = np.empty(n.value, np.uint64)
+        offs = np.empty(n.value + 1, np.uint64)
+        data = np.empty(max(nb.value, 1), np.uint8)
+        pc = np.empty(npres.value, np.uint32)
+        pf = np.empty(npres.value, np.uint32)
+        self._ck(lib.fr_get_exotic_table(self.h, _ptr(counts), _ptr(first), _ptr(offs), _ptr(data), _ptr(pc),
+                                         _ptr(pf)), "fr_get_exotic_table")
+        raw = data.tobytes()
+        o = offs.tolist()
+        codes = [raw[o[i]:o[i + 1]] for i in range(n.value)]
+        return codes, counts, first, pc, pf
 
     # ---- classify -------------------------------------------------------------------
     def classify(self, num_subs: int, rc: bool, to_host: bool = True):
@@ -413,11 +469,12 @@ class Context:
         return t
 
     def diag(self) -> dict:
-        v = np.zeros(17, dtype=np.uint64)
-        self._ck(lib.fr_get_diag(self.h, _ptr(v), 17), "fr_get_diag")
+        v = np.zeros(18, dtype=np.uint64)
+        self._ck(lib.fr_get_diag(self.h, _ptr(v), 18), "fr_get_diag")
         d = dict(zip(("spin_max", "spin_total", "keys", "overflow", "presence", "exotic", "grid", "slots"),
                      v[:8].tolist()))
         d["spec_replays"] = int(v[16])
+        d["exo_replays"] = int(v[17])
         if v[8:16].any():  # FR_TIMING build / FR_ABLATE=64: per-phase cycles or commit counts
             names = (("lookback", "barrier", "headers", "parse", "stage", "count", "flush", "prologue")
                      if os.environ.get("FR_KERNEL") == "0" else

@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/frender_amd.h"
@@ -66,14 +67,33 @@ struct fr_ctx {
     // current file
     bool scanning = false;
     bool file_open = false;
-    u32 file_tag = 0;
+    u32 file_tag = 0;         // current (last) file's tag = file index + 1; increases within a scan
+    u32 first_tag = 0;        // the first file's tag since fr_reset (0: none yet)
+    u64 file_base = 0;        // file offset of the current file's first fed byte (fr_begin_file_at)
     bool merged = false;  // the table holds ordinals merged from other contexts (any file tag)
     u64 max_file_bytes = 0;  // bytes of the longest file tallied since fr_reset (ordinal offsets are below it)
     u64 file_offset = 0;
     i64 max_records = 0;
     int last_byte = -1;
     u64 pres_before = 0;
-    u64 exo_before = 0;
+    // exotic codes (outside the fast and wide key forms): the device captures each record's bytes
+    // into a list sized per launch; the host drains it after every launch that produced records
+    // and aggregates by exact byte string here (count, first ordinal, per-file presence)
+    struct ExoCode {
+        u64 count, first;
+        u32 last_tag;
+    };
+    std::unordered_map<std::string, u32> exo_index;
+    std::vector<std::string> exo_str;     // first-appearance order of the drains
+    std::vector<ExoCode> exo_codes;
+    std::vector<u32> exo_pres_code, exo_pres_file;
+    u64 exo_new_file = 0;                 // distinct exotic codes of the current file
+    u64 exo_records_file = 0;             // exotic records of the current file
+    bool host_feed = false;               // launches come from fr_feed (each checked before the next)
+    ScanArgs last_args{};                 // the previous launch (exotic-only replay after an overflow)
+    int last_grid = 0;
+    bool last_valid = false;
+    u64 exo_replays = 0;
     bool sample_done = false;
 
     // sheet
@@ -102,7 +122,7 @@ struct fr_ctx {
     u64 n_pres = 0;
     u64 pmap_cap = 0;
     u32 *d_pres_u = nullptr, *d_pres_f = nullptr;
-    u64 n_exo = 0;
+    u64 n_exo = 0;  // exotic codes of the finalized scan
 
     // classify scratch
     u64 ccap = 0;
@@ -222,9 +242,12 @@ static int ensure_presence_cap(fr_ctx* ctx) {
 
 // called before each tally launch: act on the latest asynchronous snapshot, if ready
 static int maybe_grow(fr_ctx* ctx) {
-    if (!ctx->st_pending) return FR_OK;
-    if (hipEventQuery(ctx->st_ev) != hipSuccess) return FR_OK;
-    ctx->st_pending = false;
+    if (ctx->st_pending) {
+        if (hipEventQuery(ctx->st_ev) != hipSuccess) return FR_OK;
+        ctx->st_pending = false;
+    } else if (!ctx->st_fresh) {
+        return FR_OK;  // nothing new since the last decision
+    }
     const DevState& s = *ctx->h_st;
     if (s.n_overflow || s.n_keys * 2 > ctx->nslots) return grow_table(ctx, false);
     return FR_OK;
@@ -237,9 +260,151 @@ static int snapshot_async(fr_ctx* ctx) {
     return FR_OK;
 }
 
-static int launch_range(fr_ctx* ctx, const u8* dptr, u64 len, u64 avail, int own_start, int own_end, int pre_valid) {
+static int upload_table(fr_ctx* ctx) {
+    if (std::memcmp(&ctx->tab, ctx->h_tab, sizeof(Table)) != 0) {  // the table moved: refresh its device copy
+        CK(hipStreamSynchronize(ctx->stream));  // the previous copy from h_tab has landed
+        std::memcpy(ctx->h_tab, &ctx->tab, sizeof(Table));
+        CK(hipMemcpyAsync(ctx->d_tab, ctx->h_tab, sizeof(Table), hipMemcpyHostToDevice, ctx->stream));
+    }
+    return FR_OK;
+}
+
+// exotic list capacity for `need` records and `need_bytes` code bytes (contents are dropped: the
+// list is empty whenever it grows)
+static int grow_exotic(fr_ctx* ctx, u64 need, u64 need_bytes) {
+    if (need > ctx->tab.exo_cap) {
+        CK(hipStreamSynchronize(ctx->stream));
+        const u64 cap = std::max<u64>(need + need / 4, 2 * ctx->tab.exo_cap);
+        CK(hipFree(ctx->tab.exo_ord));
+        CK(hipFree(ctx->tab.exo_off));
+        CK(hipFree(ctx->tab.exo_len));
+        ctx->tab.exo_ord = nullptr;
+        ctx->tab.exo_off = nullptr;
+        ctx->tab.exo_len = nullptr;
+        CK(dalloc(&ctx->tab.exo_ord, cap));
+        CK(dalloc(&ctx->tab.exo_off, cap));
+        CK(dalloc(&ctx->tab.exo_len, cap));
+        ctx->tab.exo_cap = cap;
+    }
+    if (need_bytes > ctx->tab.exo_pool_cap) {
+        CK(hipStreamSynchronize(ctx->stream));
+        const u64 cap = std::max<u64>(need_bytes + need_bytes / 4, 2 * ctx->tab.exo_pool_cap);
+        CK(hipFree(ctx->tab.exo_pool));
+        ctx->tab.exo_pool = nullptr;
+        CK(dalloc(&ctx->tab.exo_pool, cap));
+        ctx->tab.exo_pool_cap = cap;
+    }
+    return upload_table(ctx);
+}
+
+// Move the device's exotic records into the host aggregate and empty the list (the state must be
+// exact and hold no overflow).  Stream-ordered: later launches append to the emptied list.
+static int drain_exotic(fr_ctx* ctx) {
+    DevState& s = *ctx->h_st;
+    const u64 n = s.n_exotic, used = s.exo_pool_used;
+    if (!n) return FR_OK;
+    if (n > ctx->tab.exo_cap || used > ctx->tab.exo_pool_cap)
+        return fail(ctx, FR_ERR_DEVICE, "exotic list drained while overflowed");
+    std::vector<u64> ord(n), off(n);
+    std::vector<u32> len(n);
+    std::vector<u8> pool(used);
+    CK(hipMemcpyAsync(ord.data(), ctx->tab.exo_ord, n * 8, hipMemcpyDeviceToHost, ctx->stream));
+    CK(hipMemcpyAsync(off.data(), ctx->tab.exo_off, n * 8, hipMemcpyDeviceToHost, ctx->stream));
+    CK(hipMemcpyAsync(len.data(), ctx->tab.exo_len, n * 4, hipMemcpyDeviceToHost, ctx->stream));
+    if (used) CK(hipMemcpyAsync(pool.data(), ctx->tab.exo_pool, used, hipMemcpyDeviceToHost, ctx->stream));
+    CK(hipMemsetAsync(&ctx->st->n_exotic, 0, 2 * sizeof(u64), ctx->stream));  // n_exotic, exo_pool_used
+    CK(hipStreamSynchronize(ctx->stream));
+    s.n_exotic = 0;
+    s.exo_pool_used = 0;
+    // records arrive in no particular order: the first ordinal is a min, presence a per-file flag
+    for (u64 i = 0; i < n; ++i) {
+        std::string code((const char*)pool.data() + off[i], len[i]);
+        auto it = ctx->exo_index.find(code);
+        u32 k;
+        if (it == ctx->exo_index.end()) {
+            k = (u32)ctx->exo_codes.size();
+            ctx->exo_index.emplace(code, k);
+            ctx->exo_str.push_back(std::move(code));
+            ctx->exo_codes.push_back({0, ~0ull, 0});
+        } else {
+            k = it->second;
+        }
+        auto& e = ctx->exo_codes[k];
+        e.count += 1;
+        e.first = std::min(e.first, ord[i]);
+        const u32 tag = (u32)(ord[i] >> ORD_SHIFT);
+        if (e.last_tag != tag) {  // a file's records all carry its tag; files are scanned in order
+            e.last_tag = tag;
+            ctx->exo_pres_code.push_back(k);
+            ctx->exo_pres_file.push_back(tag - 1u);
+            ctx->exo_new_file++;
+        }
+    }
+    ctx->exo_records_file += n;
+    return FR_OK;
+}
+
+static int launch_args(fr_ctx* ctx, const ScanArgs& a, int grid);
+
+// After a launch whose exotic records overflowed the list: grow it to the counted totals and run
+// the same launch again capturing exotic records only (no table updates; exact line phases).  The
+// launch's input is still resident (host feeds check every launch before the next one's data
+// overwrites its ring slot).
+static int replay_exotic(fr_ctx* ctx) {
+    if (!ctx->last_valid) return fail(ctx, FR_ERR_DEVICE, "exotic overflow without a launch to replay");
+    DevState& s = *ctx->h_st;
+    int rc = grow_exotic(ctx, s.n_exotic, s.exo_pool_used);
+    if (rc) return rc;
+    s.n_exotic = 0;
+    s.exo_pool_used = 0;
+    s.cap_flags &= ~4u;
+    CK(hipMemsetAsync(&ctx->st->n_exotic, 0, 2 * sizeof(u64), ctx->stream));
+    CK(hipMemcpyAsync(&ctx->st->cap_flags, &s.cap_flags, sizeof(u32), hipMemcpyHostToDevice, ctx->stream));
+    ScanArgs a = ctx->last_args;
+    a.exo_only = 1;
+    a.spec_commit = 0;
+    a.epoch = ++ctx->epoch;
+    a.tab = ctx->d_tab;
+    CK(hipMemsetAsync(&ctx->st->ticket, 0, 2 * sizeof(u32), ctx->stream));  // ticket, chunks_done
+    rc = launch_args(ctx, a, ctx->last_grid);
+    if (rc) return rc;
+    ctx->exo_replays++;
+    ctx->st_fresh = false;
+    rc = read_state(ctx);
+    if (rc) return rc;
+    if (ctx->h_st->cap_flags & 4u) return fail(ctx, FR_ERR_DEVICE, "exotic replay overflowed");
+    return FR_OK;
+}
+
+// the previous launch's exotic records: replay it on overflow, then drain (exact state needed)
+static int settle_exotic(fr_ctx* ctx) {
+    int rc = read_state(ctx);
+    if (rc) return rc;
+    if (ctx->h_st->cap_flags & 4u) {
+        rc = replay_exotic(ctx);
+        if (rc) return rc;
+    }
+    return drain_exotic(ctx);
+}
+
+static int launch_args(fr_ctx* ctx, const ScanArgs& a, int grid) {  // the caller zeroed the ticket
+    if (a.num_tiles > ctx->tiles_cap) return fail(ctx, FR_ERR_INVALID, "range larger than the look-back array");
+    ctx->st_fresh = false;
+    CK(launch_chunk_scan(a, grid, ctx->stream));
+    return FR_OK;
+}
+
+static int launch_range(fr_ctx* ctx, const u8* dptr, u64 len, u64 avail, int own_start, int own_end, int pre_valid,
+                        int exo_only = 0) {
     if (len == 0) return FR_OK;
-    int rc = maybe_grow(ctx);
+    int rc = FR_OK;
+    if (ctx->host_feed && ctx->last_valid) {
+        // host feeds: the previous launch's exotic records are settled before this one is queued (its
+        // ring slot is still intact for a replay); the H2D copy of this launch is already in flight
+        rc = settle_exotic(ctx);
+        if (rc) return rc;
+    }
+    rc = maybe_grow(ctx);
     if (rc) return rc;
     ScanArgs a;
     std::memset(&a, 0, sizeof(a));
@@ -260,14 +425,11 @@ static int launch_range(fr_ctx* ctx, const u8* dptr, u64 len, u64 avail, int own
     a.st = ctx->st;
     a.tiles = ctx->tiles;
     a.chunk_info = ctx->chunk_info;
-    a.spec_commit = ctx->spec_commit;
-    if (std::memcmp(&ctx->tab, ctx->h_tab, sizeof(Table)) != 0) {  // the table moved: refresh its device copy
-        CK(hipStreamSynchronize(ctx->stream));  // the previous copy from h_tab has landed
-        std::memcpy(ctx->h_tab, &ctx->tab, sizeof(Table));
-        CK(hipMemcpyAsync(ctx->d_tab, ctx->h_tab, sizeof(Table), hipMemcpyHostToDevice, ctx->stream));
-    }
+    a.spec_commit = exo_only ? 0u : ctx->spec_commit;
+    a.exo_only = (u32)exo_only;
+    rc = upload_table(ctx);
+    if (rc) return rc;
     a.tab = ctx->d_tab;
-    if (a.num_tiles > ctx->tiles_cap) return fail(ctx, FR_ERR_INVALID, "range larger than the look-back array");
     if (ctx->epoch >= 0x7FFFFFFFu) {  // tag wrap: restart epochs on a cleared descriptor array
         CK(hipMemsetAsync(ctx->tiles, 0, ctx->tiles_cap * sizeof(u64), ctx->stream));
         ctx->epoch = 1;
@@ -302,7 +464,12 @@ static int launch_range(fr_ctx* ctx, const u8* dptr, u64 len, u64 avail, int own
     a.cold = ctx->cold;
     a.rare = ctx->rare;
     // workgroups take chunks by ticket; never more than the resident grid (cold lists are per block)
-    CK(launch_chunk_scan(a, (int)std::min<u64>(a.num_chunks, G), ctx->stream));
+    const int grid = (int)std::min<u64>(a.num_chunks, G);
+    rc = launch_args(ctx, a, grid);
+    if (rc) return rc;
+    ctx->last_args = a;
+    ctx->last_grid = grid;
+    ctx->last_valid = true;
     CK(hipEventRecord(ctx->ev_b[ctx->ev_used], ctx->stream));
     ctx->ev_used++;
     ctx->scan_launches++;
@@ -425,7 +592,7 @@ int fr_get_diag(fr_ctx* ctx, uint64_t* out, int n) {
     const DevState& s = *ctx->h_st;
     const uint64_t v[] = {s.spin_max,   s.spin_total, s.n_keys,   s.n_overflow, s.n_presence, s.n_exotic,
                           (uint64_t)ctx->grid, ctx->nslots, s.stamp[0], s.stamp[1], s.stamp[2], s.stamp[3],
-                          s.stamp[4],  s.stamp[5],  s.stamp[6], s.stamp[7], ctx->spec_replays};
+                          s.stamp[4],  s.stamp[5],  s.stamp[6], s.stamp[7], ctx->spec_replays, ctx->exo_replays};
     for (int i = 0; i < n && i < (int)(sizeof(v) / sizeof(v[0])); ++i) out[i] = v[i];
     return FR_OK;
 }
@@ -534,12 +701,19 @@ int fr_reset(fr_ctx* ctx) {
     ctx->scanning = true;
     ctx->file_open = false;
     ctx->file_tag = 0;
+    ctx->first_tag = 0;
     ctx->merged = false;
     ctx->max_file_bytes = 0;
     ctx->par = 0;
     ctx->U = 0;
     ctx->n_pres = 0;
     ctx->n_exo = 0;
+    ctx->exo_index.clear();
+    ctx->exo_str.clear();
+    ctx->exo_codes.clear();
+    ctx->exo_pres_code.clear();
+    ctx->exo_pres_file.clear();
+    ctx->last_valid = false;
     ctx->ev_used = 0;
     ctx->scan_launches = ctx->scan_bytes = 0;
     ctx->classify_ms = ctx->finalize_ms = 0;
@@ -548,12 +722,21 @@ int fr_reset(fr_ctx* ctx) {
 }
 
 int fr_begin_file(fr_ctx* ctx, int64_t max_records) {
+    return fr_begin_file_at(ctx, (int64_t)ctx->file_tag, 0, max_records);
+}
+
+int fr_begin_file_at(fr_ctx* ctx, int64_t file_index, uint64_t byte_base, int64_t max_records) {
     if (ctx->file_open) return fail(ctx, FR_ERR_INVALID, "fr_begin_file: a file is already open");
-    if (ctx->file_tag + 1 >= (1u << 19)) return fail(ctx, FR_ERR_INVALID, "too many files in one scan");
+    if (file_index < 0 || file_index + 1 >= (1 << 19)) return fail(ctx, FR_ERR_INVALID, "too many files in one scan");
+    if ((u32)file_index + 1u <= ctx->file_tag)
+        return fail(ctx, FR_ERR_INVALID, "fr_begin_file_at: file indices must increase within a scan");
+    if (byte_base >= (1ull << ORD_SHIFT)) return fail(ctx, FR_ERR_INVALID, "fr_begin_file_at: byte base too large");
     int rc = read_state(ctx);
     if (rc) return rc;
     ctx->pres_before = ctx->h_st->n_presence;
-    ctx->exo_before = ctx->h_st->n_exotic;
+    ctx->exo_new_file = 0;
+    ctx->exo_records_file = 0;
+    ctx->last_valid = false;
     // per-file device flags + line carry
     CK(hipMemsetAsync(&ctx->st->lines[0], 0, 2 * sizeof(u64), ctx->stream));
     CK(hipMemsetAsync(&ctx->st->err_nospace, 0xFF, sizeof(u64), ctx->stream));
@@ -561,8 +744,10 @@ int fr_begin_file(fr_ctx* ctx, int64_t max_records) {
     ctx->h_st->lines[0] = ctx->h_st->lines[1] = 0;  // the snapshot stays exact
     ctx->h_st->err_nospace = ~0ull;
     ctx->h_st->nonascii = ctx->h_st->utf8_bad = 0;
-    ctx->file_tag++;
-    ctx->file_offset = 0;
+    ctx->file_tag = (u32)file_index + 1u;
+    if (!ctx->first_tag) ctx->first_tag = ctx->file_tag;
+    ctx->file_offset = byte_base;
+    ctx->file_base = byte_base;
     ctx->max_records = max_records > 0 ? max_records : 0;
     ctx->last_byte = -1;
     ctx->carry.clear();
@@ -596,6 +781,7 @@ static int ship_slot(fr_ctx* ctx, int slot, u64 n) {
 
 int fr_feed(fr_ctx* ctx, const uint8_t* data, uint64_t len) {
     if (!ctx->file_open) return fail(ctx, FR_ERR_INVALID, "fr_feed: no open file");
+    ctx->host_feed = true;
     if (ctx->sample_done) return FR_SAMPLE_DONE;
     if (len) ctx->last_byte = data[len - 1];
     u64 done = 0;
@@ -610,9 +796,12 @@ int fr_feed(fr_ctx* ctx, const uint8_t* data, uint64_t len) {
         std::memcpy(pin + nc, data + done, take);
         done += take;
         const u64 n = nc + take;
-        // cut after the last '\n' so no header crosses a launch (R1 line phase is carried on device)
+        // cut after the last line terminator so no line crosses a launch (R1 universal newlines: the
+        // line phase is carried on the device).  A '\r' ends a line only when the byte after it is
+        // known and is not '\n', so a '\r' at the buffer's end waits in the carry (CR-only files
+        // cut at their lone '\r's; a CRLF is never split)
         u64 cut = n;
-        while (cut > 0 && pin[cut - 1] != '\n') --cut;
+        while (cut > 0 && !(pin[cut - 1] == '\n' || (pin[cut - 1] == '\r' && cut < n && pin[cut] != '\n'))) --cut;
         if (cut == 0) {
             ctx->carry.assign(pin, pin + n);
             continue;
@@ -630,7 +819,7 @@ int fr_feed(fr_ctx* ctx, const uint8_t* data, uint64_t len) {
 
 int fr_feed_device(fr_ctx* ctx, const uint8_t* dev_data, uint64_t len) {
     if (!ctx->file_open) return fail(ctx, FR_ERR_INVALID, "fr_feed_device: no open file");
-    if (ctx->file_offset != 0 || !ctx->carry.empty())
+    if (ctx->file_offset != ctx->file_base || !ctx->carry.empty())
         return fail(ctx, FR_ERR_INVALID, "fr_feed_device takes a whole file (no prior fr_feed)");
     if (((uintptr_t)dev_data & 15u) != 0) return fail(ctx, FR_ERR_INVALID, "device data must be 16-byte aligned");
     // Speculative chunks commit without waiting for their exact line prefix; the launch's last
@@ -638,7 +827,8 @@ int fr_feed_device(fr_ctx* ctx, const uint8_t* dev_data, uint64_t len) {
     // are not 4-line FASTQ -- rolls the table back to this feed's start and replays it with every
     // chunk waiting for its prefix.  The rollback point: the table slots (a device copy unless the
     // table is empty) and the device state.
-    int rc = read_state(ctx);
+    ctx->host_feed = false;
+    int rc = settle_exotic(ctx);  // an empty exotic list at the feed's start
     if (rc) return rc;
     const DevState saved = *ctx->h_st;
     const u32 par0 = ctx->par;
@@ -682,13 +872,41 @@ int fr_feed_device(fr_ctx* ctx, const uint8_t* dev_data, uint64_t len) {
         ctx->st_pending = false;
         ctx->st_fresh = true;
         ctx->par = par0;
-        ctx->file_offset = 0;
+        ctx->file_offset = ctx->file_base;
         ctx->spec_replays++;
     }
     if (snap) {
         CK(hipStreamSynchronize(ctx->stream));
         CK(hipFree(snap));
     }
+    if (rc) return rc;
+    // exotic records overflowed the list: grow it to the counted totals and run the feed's launches
+    // again capturing exotic records only (the table is already complete), then drain
+    rc = read_state(ctx);
+    if (rc) return rc;
+    if (ctx->h_st->cap_flags & 4u) {
+        DevState& s = *ctx->h_st;
+        rc = grow_exotic(ctx, s.n_exotic, s.exo_pool_used);
+        if (rc) return rc;
+        s.n_exotic = 0;
+        s.exo_pool_used = 0;
+        s.cap_flags &= ~4u;
+        s.lines[par0] = saved.lines[par0];
+        CK(hipMemcpyAsync(ctx->st, ctx->h_st, sizeof(DevState), hipMemcpyHostToDevice, ctx->stream));
+        ctx->par = par0;
+        ctx->file_offset = ctx->file_base;
+        ctx->exo_replays++;
+        for (u64 off = 0; off < len && !rc; off += step) {
+            const u64 n = std::min<u64>(step, len - off);
+            rc = launch_range(ctx, dev_data + off, n, len - off, off == 0 ? 1 : 0, 1, off ? 1 : 0, 1);
+        }
+        if (rc) return rc;
+        ctx->st_fresh = false;
+        rc = read_state(ctx);
+        if (rc) return rc;
+        if (ctx->h_st->cap_flags & 4u) return fail(ctx, FR_ERR_DEVICE, "exotic replay overflowed");
+    }
+    rc = drain_exotic(ctx);
     if (rc) return rc;
     if (len) {
         u8 b = 0;
@@ -718,7 +936,10 @@ int fr_end_file(fr_ctx* ctx, fr_file_stats* out) {
     }
     ctx->carry.clear();
     CK(hipStreamSynchronize(ctx->copy));
-    int rc = grow_table(ctx, false);  // re-inserts any overflow; exact state afterwards
+    int rc = ctx->host_feed ? settle_exotic(ctx) : FR_OK;  // device feeds settled at their end
+    if (rc) return rc;
+    ctx->last_valid = false;
+    rc = grow_table(ctx, false);  // re-inserts any overflow; exact state afterwards
     if (rc) return rc;
     rc = ensure_presence_cap(ctx);
     if (rc) return rc;
@@ -738,11 +959,13 @@ int fr_end_file(fr_ctx* ctx, fr_file_stats* out) {
     std::memset(out, 0, sizeof(*out));
     out->records = records;
     out->lines = lines;
-    out->new_keys = s.n_presence - ctx->pres_before;
-    out->exotic = s.n_exotic - ctx->exo_before;
+    out->new_keys = s.n_presence - ctx->pres_before + ctx->exo_new_file;
+    out->exotic = ctx->exo_records_file;
     out->error = FR_SCAN_OK;
-    ctx->n_exo = std::min<u64>(s.n_exotic, ctx->tab.exo_cap);
-    if (s.utf8_bad) out->error = FR_SCAN_UTF8;
+    if (s.utf8_bad) {
+        out->error = FR_SCAN_UTF8;
+        out->utf8_bad = 1;
+    }
     if (s.err_nospace != ~0ull) {
         out->error = FR_SCAN_NO_SPACE;
         out->error_offset = s.err_nospace;
@@ -795,7 +1018,7 @@ int fr_finalize(fr_ctx* ctx, uint64_t* n_unique, uint64_t* n_presence, uint64_t*
         begin_bit = 2;
         end_bit = ORD_SHIFT;
         while (end_bit < 64 && ((u64)ctx->file_tag >> (end_bit - ORD_SHIFT)) != 0) ++end_bit;
-        if (ctx->file_tag == 1) {
+        if (ctx->file_tag == ctx->first_tag) {  // one file: its tag is a constant above every offset bit
             end_bit = begin_bit + 1;
             while (end_bit < ORD_SHIFT && (ctx->max_file_bytes >> end_bit) != 0) ++end_bit;
         }
@@ -837,7 +1060,7 @@ int fr_finalize(fr_ctx* ctx, uint64_t* n_unique, uint64_t* n_presence, uint64_t*
     if (got != nk) return fail(ctx, FR_ERR_DEVICE, "compaction count mismatch");
     ctx->U = nk;
     ctx->n_pres = np;
-    ctx->n_exo = std::min<u64>(ctx->h_st->n_exotic, ctx->tab.exo_cap);
+    ctx->n_exo = ctx->exo_codes.size();
     if (n_unique) *n_unique = ctx->U;
     if (n_presence) *n_presence = ctx->n_pres;
     if (n_exotic) *n_exotic = ctx->n_exo;
@@ -861,20 +1084,30 @@ int fr_get_presence(fr_ctx* ctx, uint32_t* unique_idx, uint32_t* file_idx) {
     return FR_OK;
 }
 
-int fr_get_exotic(fr_ctx* ctx, uint64_t first, uint64_t count, uint64_t* ordinal, uint32_t* length,
-                  uint64_t* pool_offset, uint8_t* pool, uint64_t pool_bytes, uint64_t* written) {
-    const u64 have = ctx->n_exo;
-    const u64 n = first < have ? std::min<u64>(count, have - first) : 0;
-    if (written) *written = n;
-    if (n) {
-        if (ordinal) CK(hipMemcpy(ordinal, ctx->tab.exo_ord + first, n * 8, hipMemcpyDeviceToHost));
-        if (length) CK(hipMemcpy(length, ctx->tab.exo_len + first, n * 4, hipMemcpyDeviceToHost));
-        if (pool_offset) CK(hipMemcpy(pool_offset, ctx->tab.exo_off + first, n * 8, hipMemcpyDeviceToHost));
+int fr_exotic_sizes(fr_ctx* ctx, uint64_t* n_codes, uint64_t* code_bytes, uint64_t* n_presence) {
+    u64 b = 0;
+    for (const auto& c : ctx->exo_str) b += c.size();
+    if (n_codes) *n_codes = ctx->exo_str.size();
+    if (code_bytes) *code_bytes = b;
+    if (n_presence) *n_presence = ctx->exo_pres_code.size();
+    return FR_OK;
+}
+
+int fr_get_exotic_table(fr_ctx* ctx, uint64_t* counts, uint64_t* first, uint64_t* offsets, uint8_t* bytes,
+                        uint32_t* pres_code, uint32_t* pres_file) {
+    const u64 n = ctx->exo_str.size();
+    u64 b = 0;
+    for (u64 i = 0; i < n; ++i) {
+        if (counts) counts[i] = ctx->exo_codes[i].count;
+        if (first) first[i] = ctx->exo_codes[i].first;
+        if (offsets) offsets[i] = b;
+        if (bytes) std::memcpy(bytes + b, ctx->exo_str[i].data(), ctx->exo_str[i].size());
+        b += ctx->exo_str[i].size();
     }
-    if (pool && pool_bytes) {
-        const u64 used = std::min<u64>(ctx->h_st->exo_pool_used, ctx->tab.exo_pool_cap);
-        CK(hipMemcpy(pool, ctx->tab.exo_pool, std::min(used, pool_bytes), hipMemcpyDeviceToHost));
-    }
+    if (offsets) offsets[n] = b;
+    const u64 np = ctx->exo_pres_code.size();
+    if (pres_code && np) std::memcpy(pres_code, ctx->exo_pres_code.data(), np * 4);
+    if (pres_file && np) std::memcpy(pres_file, ctx->exo_pres_file.data(), np * 4);
     return FR_OK;
 }
 

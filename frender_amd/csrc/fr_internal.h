@@ -27,6 +27,15 @@ constexpr int NS = 1 << LOG_NS;      // LDS hash slots per workgroup
 constexpr int LPROBE = FR_LPROBE;          // LDS probe bound before going to HBM directly
 constexpr int GPROBE = 256;          // HBM probe bound before the overflow list
 constexpr int MAXSYM = 21;           // fast key: <= 21 symbols of 3 bits
+// Wide keys: codes that are not fast keys but whose letters are all ACGTN or all
+// acgtn, with at most one '+', each part <= 21 letters and <= 24 letters in total (12+12 dual
+// indexes, lowercase files).  key = bit 63 | lowercase << 62 | plus position << 57 | V, with
+// V = sum d_i 5^i + (5^n - 1) / 4 over the n letters (A0 C1 G2 T3 N4, case-folded): the length
+// offset makes V unique across lengths, V < (5^25 - 1) / 4 < 2^57.  Plus position = letters before
+// the '+', WIDE_NOPLUS without one.  Fast keys never set bit 63 (21 symbols x 3 bits).
+constexpr u64 WIDE_BIT = 1ull << 63;
+constexpr int WIDE_MAXN = 24;
+constexpr int WIDE_NOPLUS = 31;
 constexpr u64 RANGE_MAX = (4ull << 30) - (1ull << 20);  // bytes per tally launch (device feeds): range
                                      // offsets, LDS first-offsets and per-range line counts stay u32
 constexpr u64 HOST_CHUNK_MAX = 1ull << 30;  // bytes per host-fed launch (pinned ring slot)
@@ -120,6 +129,8 @@ struct ScanArgs {
     u64* cold;           // chunk kernel: cold lists, [grid][cold_cap] x {key, ordinal}
     uint4* rare;         // chunk kernel: rare-event rings, [grid][RARE_RING] (fr_kernels.hip)
     u64* chunk_info;     // chunk kernel: per chunk {line count, spec flag + guessed phase << 1 in the high word}
+    u32 exo_only;        // replay of a launch whose exotic list overflowed: capture exotic records only (no
+                         // table updates), every chunk with its exact line phase
     u32 spec_commit;     // commit speculative chunks without waiting for their exact prefix (checked at the
                          // launch end by verify_launch; a wrong guess sets spec_fail)
     DevState* st;

@@ -383,14 +383,59 @@ __device__ FR_COLD bool utf8_segment_ok(const ScanArgs& a, u64 tile0, int s0, in
 
 template <bool DRAIN = false>
 __device__ __forceinline__ void count_code(ScanShared& sh, const ScanArgs& a, u64 tile0, u32 p, u64 key) {
-    if (a.ablate & 4u) {  // ablation: skip the hash insert (keep the key live)
+    if ((a.ablate & 4u) || a.exo_only) {  // ablation / exotic-only replay: skip the hash insert
         asm volatile("" ::"v"(key));
         return;
     }
     lds_insert<DRAIN>(sh, a, key, (u32)(tile0 + p));
 }
 
+// code bytes [q, q+n) of the range (exact byte reads) -> wide key (fr_internal.h), false when the
+// code is outside the wide form.  Only called for codes that are not fast keys.
+__device__ bool wide_encode(const ScanArgs& a, u64 q, u64 n, u64& key) {
+    if (n < 1 || n > (u64)WIDE_MAXN + 1) return false;
+    int lower = -1, plus = WIDE_NOPLUS, nl = 0;
+    u64 v = 0, pw = 1;
+    for (u64 k = 0; k < n; ++k) {
+        const u32 c = a.buf[q + k];
+        if (c == '+') {
+            if (plus != WIDE_NOPLUS) return false;
+            plus = nl;
+            continue;
+        }
+        const u32 lc = c | 0x20u;
+        const int d = lc == 'a' ? 0 : lc == 'c' ? 1 : lc == 'g' ? 2 : lc == 't' ? 3 : lc == 'n' ? 4 : -1;
+        if (d < 0 || nl >= WIDE_MAXN) return false;
+        const int isl = (c & 0x20u) ? 1 : 0;
+        if (lower < 0) lower = isl;
+        else if (lower != isl) return false;
+        v += (u64)d * pw;
+        pw *= 5;
+        ++nl;
+    }
+    if (lower < 0) return false;  // no letter
+    const int n1 = plus == WIDE_NOPLUS ? nl : plus, n2 = plus == WIDE_NOPLUS ? 0 : nl - plus;
+    if (n1 > MAXSYM || n2 > MAXSYM) return false;
+    key = WIDE_BIT | ((u64)lower << 62) | ((u64)plus << 57) | (v + (pw - 1) / 4);
+    return true;
+}
+
+// a code the fast encoder did not take: exact fast form (defensive), wide key, or an exotic record
+// captured verbatim (speculating: its position is buffered and the bytes stay resident in HBM)
 __device__ void exotic_record(const ScanArgs& a, u64 tile0, u32 p, u64 start, u64 n, ScanShared& sh) {
+    {
+        bool fast = n >= 1 && n <= (u64)MAXSYM;
+        u64 key = 0;
+        for (u64 i = 0; fast && i < n; ++i) {
+            const u32 sy = sym_of(a.buf[tile0 + start + i]);
+            fast = sy != 0;
+            key |= (u64)sy << (3 * i);
+        }
+        if (fast || wide_encode(a, tile0 + start, n, key)) {
+            count_code<true>(sh, a, tile0, p, key);
+            return;
+        }
+    }
     if (sh.spec) {  // speculating: remember where it is; the bytes stay resident in HBM
         const u32 k = atomicAdd(&sh.nexo, 1u);
         if (k < (u32)EXO_BUF) {
@@ -1264,7 +1309,7 @@ __global__ __launch_bounds__(WG, FR_OCC) void chunk_kernel(ScanArgs args) {
         int P = -1;
         if (c == 0) {
             P = (int)(base_lines & 3ull);
-        } else if (a.max_records <= 0 && !empty) {
+        } else if (a.max_records <= 0 && !empty && !a.exo_only) {
             P = guess_phase(sh, a, tb, tid, lane, wid);
         }
         // pass 0: exact (chunk 0) / speculative (guessed phase) / count-only (unsure, -s);
@@ -1676,32 +1721,61 @@ __global__ __launch_bounds__(CLS_WG) void classify_kernel(const u64* keys, const
     const u64 u = blockIdx.x * (u64)CLS_WG + threadIdx.x;
     if (u < n) {
         const u64 key = keys[u];
-        // split the code at '+' (symbol 6): idx1, idx2 = code.split("+")[0:2]  (frender.py:306)
-        int p1 = -1, p2 = MAXSYM, len = 0;
-        for (int i = 0; i < MAXSYM; ++i) {
-            const u32 sy = (u32)(key >> (3 * i)) & 7u;
-            if (!sy) break;
-            len = i + 1;
-            if (sy == 6u) {
-                if (p1 < 0) p1 = i;
-                else if (p2 == MAXSYM) p2 = i;
+        // split the code at '+': idx1, idx2 = code.split("+")[0:2]  (frender.py:306), both case-folded
+        // and packed 3 bits per letter (a1 c2 g3 t4 n5) like the sheet
+        int n1 = 0, n2 = 0;
+        bool plus = false;
+        u64 q1 = 0, q2 = 0;
+        if (key & WIDE_BIT) {  // wide key (fr_internal.h): base-5 letters, '+' position in bits 57-61
+            const u64 V = key & ((1ull << 57) - 1ull);
+            const int pp = (int)((key >> 57) & 31u);
+            int nl = 0;
+            u64 off = 0, pw = 1;
+            while (nl < WIDE_MAXN && off + pw <= V) {  // off = (5^nl - 1) / 4
+                off += pw;
+                pw *= 5;
+                ++nl;
+            }
+            u64 D = V - off;
+            plus = pp != WIDE_NOPLUS;
+            n1 = plus ? pp : nl;
+            n2 = plus ? nl - pp : 0;
+            for (int i = 0; i < nl; ++i) {
+                const u64 sy = D % 5u + 1u;
+                D /= 5u;
+                if (i < n1) q1 |= sy << (3 * i);
+                else q2 |= sy << (3 * (i - n1));
+            }
+        } else {  // fast key: symbols A1 C2 G3 T4 N5 '+'6, folded they equal the sheet's a1..n5
+            int p1 = -1, p2 = MAXSYM, len = 0;
+            for (int i = 0; i < MAXSYM; ++i) {
+                const u32 sy = (u32)(key >> (3 * i)) & 7u;
+                if (!sy) break;
+                len = i + 1;
+                if (sy == 6u) {
+                    if (p1 < 0) p1 = i;
+                    else if (p2 == MAXSYM) p2 = i;
+                }
+            }
+            plus = p1 >= 0;
+            if (plus) {
+                n1 = p1;
+                const int e2 = p2 < len ? p2 : len;
+                n2 = e2 - p1 - 1;
+                q1 = n1 ? (key & ((1ull << (3 * n1)) - 1ull)) : 0ull;
+                q2 = n2 ? ((key >> (3 * (p1 + 1))) & ((1ull << (3 * n2)) - 1ull)) : 0ull;
             }
         }
         int err = 0;
         int m1 = -1, m2 = -1, cls = CLS_UNDET, row = -1;
         int rm2 = -1, rcls = CLS_UNDET, rrow = -1;
-        if (p1 < 0) {
+        if (!plus) {
             err = 3;
         } else {
-            const int n1 = p1;
-            const int e2 = p2 < len ? p2 : len;
-            const int n2 = e2 - p1 - 1;
             // the length asserts (frender.py:227-229), idx1 list first
             if (sh.S > 0 && (sh.L1u == -2 || sh.L1u != n1)) err = 1;
             else if (sh.S > 0 && (sh.L2u == -2 || sh.L2u != n2)) err = 2;
             else {
-                const u64 q1 = n1 ? (key & ((1ull << (3 * n1)) - 1ull)) : 0ull;
-                const u64 q2 = n2 ? ((key >> (3 * (p1 + 1))) & ((1ull << (3 * n2)) - 1ull)) : 0ull;
                 class_pair<W>((W)q1, (W)q2, S1, S2, S2rc, sh.S, nsubs, rc != 0, m1, m2, cls, row, rm2, rcls, rrow);
                 // both calls demuxable to different sample NAMES -> ambiguous (frender.py:336-349)
                 if (rc && cls == CLS_DEMUX && rcls == CLS_DEMUX && sh.name[row] != sh.name[rrow]) {

@@ -23,15 +23,28 @@ from . import _lib
 from .host import parse_files
 
 RESULTS_HEADER = ["idx1", "idx2", "reads", "matched_idx1", "matched_idx2", "read_type", "sample_name"]
+# the column order `scan` itself writes (frender.py:482-501, report_analysis)
+SCAN_HEADER = ["idx1", "idx2", "matched_idx1", "matched_idx2", "read_type", "sample_name", "reads"]
 
 
 def parse_results_file(result_file) -> dict:
-    """frender.py:645-664 (asserts the README column order): code -> (read_type, sample_id)."""
+    """frender.py:645-664: code -> (read_type, sample_id).
+
+    The reference asserts the README's column order, which its own `scan` does not write, so its
+    demux rejects its own scan CSV.  Deliberate deviation: a
+    header in `scan`'s order is accepted too, its columns taken by name; any other header fails
+    with the reference's AssertionError, and README-order files behave exactly as in the
+    reference."""
     with open(result_file, newline="") as f:
         rd = csv.reader(f)
         header = next(rd)
-        assert header[0:7] == RESULTS_HEADER, f"${result_file} does not appear to be a valid frender result file!"
-        return {line[0] + "+" + line[1]: (line[5], line[6]) for line in rd}
+        top = header[0:7]
+        if top == SCAN_HEADER:
+            ti, si = top.index("read_type"), top.index("sample_name")
+        else:
+            assert top == RESULTS_HEADER, f"${result_file} does not appear to be a valid frender result file!"
+            ti, si = 5, 6
+        return {line[0] + "+" + line[1]: (line[ti], line[si]) for line in rd}
 
 
 def open_files(name, out_dir, infix, level):
@@ -42,13 +55,18 @@ def open_files(name, out_dir, infix, level):
                             compresslevel=level) for read in ("R1", "R2")}
 
 
+_MATE_TAG = re.compile("_R([12])_")
+
+
 def is_read_mate(str1, str2) -> bool:
-    """frender.py:685-693."""
-    if len([0 for a, b in zip(str1, str2) if a != b]) != 1:
+    """frender.py:685-693: the two paths differ at exactly one position (compared over the shorter
+    one's length) and their first `_R1_`/`_R2_` tags are one of each.  A path without such a tag
+    fails the way the reference does (TypeError on the missing match)."""
+    diff = sum(map(str.__ne__, str1, str2))
+    if diff != 1:
         return False
-    r1 = int(re.search("_R[12]_", str1)[0].replace("_", "").replace("R", ""))
-    r2 = int(re.search("_R[12]_", str2)[0].replace("_", "").replace("R", ""))
-    return {r1, r2} == {1, 2}
+    mates = {_MATE_TAG.search(s)[1] for s in (str1, str2)}
+    return mates == {"1", "2"}
 
 
 def get_paired_files(files_list) -> list:

@@ -1,4 +1,13 @@
-"""Multi-GPU table merge: one process per GPU, torch.distributed over RCCL.
+"""Multi-GPU scan: one process per GPU, torch.distributed over RCCL.
+
+Product path (`python -m frender_amd scan --gpus K`, or any torchrun launch): sharded_tally
+deals the input files to the GPUs (the reference's unit of parallelism, its Pool over files,
+frender.py:189-193), every GPU tallies its files at their global file indices
+(fr_begin_file_at), and rank 0 gathers the per-GPU tables, merges them on its GPU (count = sum,
+first = min) and continues with classification and the CSVs: byte-identical to one GPU.
+
+Bench path (below): device-resident record shards merged by a tree or a hash-partitioned
+all-to-all.
 
 The record stream shards with no data-path collective: each rank tallies its own
 records into its own device table.  The only exchange is the merge of the
@@ -152,3 +161,125 @@ def partition_merge_device(dist, device, ctx):
     n, _, _ = ctx.finalize()
     ctx.sync()
     return int(n)
+
+
+# ---- product path: files sharded over GPUs, merged on rank 0 ---------------------------------
+
+def world_group():
+    """torch.distributed when this process is one rank of N > 1, else None."""
+    try:
+        import torch.distributed as dist
+    except Exception:  # pragma: no cover
+        return None
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        return dist
+    return None
+
+
+def assign_files(files, world: int) -> list:
+    """Deal file indices to ranks: longest (compressed size) first onto the least loaded rank,
+    ties to the lower rank and index; each rank's list in increasing index order."""
+    import os
+
+    size = [os.path.getsize(f) if os.path.exists(f) else 0 for f in files]
+    load = [0] * world
+    out = [[] for _ in range(world)]
+    for i in sorted(range(len(files)), key=lambda i: (-size[i], i)):
+        r = min(range(world), key=lambda r: (load[r], r))
+        out[r].append(i)
+        load[r] += size[i] + 1
+    return [sorted(x) for x in out]
+
+
+def merge_tables(ctx, parts):
+    """Rank 0: merge the gathered per-rank tallies on this GPU (fr_merge_unique_device: count =
+    sum, first = min; the file indices in the ordinals are global) and order the result
+    (fr_finalize).  Presence pairs travel as (key, file) and map onto the merged order; exotic
+    codes merge by string.  Returns the table dict scan.build_table takes."""
+    import numpy as np
+
+    ctx.reset()
+    for t in parts:
+        n = int(t["keys"].size)
+        if not n:
+            continue
+        bufs = [ctx.device_alloc(8 * n) for _ in range(3)]
+        try:
+            for b, a in zip(bufs, (t["keys"], t["counts"], t["first"])):
+                ctx.copy_to_device(b, np.ascontiguousarray(a, dtype=np.uint64).tobytes())
+            ctx.merge_unique_device(bufs[0], bufs[1], bufs[2], n)
+            ctx.sync()
+        finally:
+            for b in bufs:
+                ctx.device_free(b)
+    ctx.finalize()
+    keys, counts, first = ctx.unique()
+    order = np.argsort(keys, kind="stable")
+    sk = keys[order]
+    pk = np.concatenate([t["keys"][t["pu"].astype(np.int64)] for t in parts] + [np.zeros(0, np.uint64)])
+    pf = np.concatenate([t["pf"].astype(np.int64) for t in parts] + [np.zeros(0, np.int64)])
+    pu = order[np.searchsorted(sk, pk)] if pk.size else np.zeros(0, np.int64)
+    srt = np.lexsort((pf, pu))  # (unique, file) order, as one context would emit them
+    pu, pf = pu[srt], pf[srt]
+    exo: dict = {}
+    for t in parts:
+        for k, c in enumerate(t["ecodes"]):
+            e = exo.setdefault(c, [0, (1 << 64) - 1, set()])
+            e[0] += int(t["ecounts"][k])
+            e[1] = min(e[1], int(t["efirst"][k]))
+        for k, f in zip(t["epc"].tolist(), t["epf"].tolist()):
+            exo[t["ecodes"][k]][2].add(int(f))
+    ecodes = list(exo)
+    epc = [i for i, c in enumerate(ecodes) for _ in exo[c][2]]
+    epf = [f for c in ecodes for f in sorted(exo[c][2])]
+    return {"keys": keys, "counts": counts, "first": first, "pu": pu, "pf": pf, "ecodes": ecodes,
+            "ecounts": np.array([exo[c][0] for c in ecodes], dtype=np.uint64),
+            "efirst": np.array([exo[c][1] for c in ecodes], dtype=np.uint64),
+            "epc": np.array(epc, dtype=np.int64), "epf": np.array(epf, dtype=np.int64)}
+
+
+def sharded_tally(dist, ctx, files, sample, cores):
+    """tally_barcodes (frender.py:183-207) over N GPUs.  Every rank tallies its share of the files
+    (assign_files) into its own context; the tables, per-file lines and any data error go to rank
+    0, which prints the per-file lines in file order, raises the first file's error as one GPU
+    would, and returns the merged UniqueTable.  Other ranks return None."""
+    import os
+
+    from . import scan
+
+    rank, world = dist.get_rank(), dist.get_world_size()
+    mine = assign_files(files, world)[rank]
+    ctx.reset()
+    err = None
+    per = {}
+    try:
+        scan.scan_files(ctx, files, mine, sample, cores,
+                        after_file=lambda fi, records, new: per.__setitem__(fi, (records, new)))
+    except BaseException as e:  # noqa: BLE001 - rank 0 re-raises it in file order
+        err = (next(i for i in mine if i not in per), e)
+    try:
+        table = scan.local_table(ctx) if err is None else None
+    except BaseException as e:  # noqa: BLE001
+        err, table = (min(mine) if mine else 0, e), None
+    payload = {"rank": rank, "per": per, "err": err, "table": table}
+    got = [None] * world if rank == 0 else None
+    dist.gather_object(payload, got, dst=0)
+    if rank != 0:
+        return None
+    per_all, errs = {}, []
+    for p in got:
+        per_all.update(p["per"])
+        if p["err"] is not None:
+            errs.append(p["err"])
+    first_bad = min((e[0] for e in errs), default=None)
+    for fi, path in enumerate(files):
+        name = str(os.path.basename(path))
+        print(f"Tallying barcodes from {name}...", end="")
+        if first_bad is not None and fi >= first_bad:
+            raise next(e for i, e in errs if i == first_bad)
+        records, new = per_all[fi]
+        print(scan.found_line(new, records))
+    print(type([]), len(files))
+    merged = merge_tables(ctx, [p["table"] for p in got])
+    names = [str(os.path.basename(p)) for p in files]
+    return scan.build_table(merged, names, [per_all[i][0] for i in range(len(files))])

@@ -10,10 +10,12 @@ on the GPU through frender_amd._lib; nothing here falls back to a CPU path.
 Data model: the merged tally (`barcode_counter["total"]`, frender.py:199-203) is a
 UniqueTable of codes in first-occurrence order with counts and per-file presence;
 classification results are arrays aligned with it.  Codes over {A,C,G,T,N,+} up
-to 21 chars are "fast" keys counted entirely on the GPU; anything else
-(lowercase, other bytes, longer codes) is an "exotic" record the GPU captures
-verbatim into a device pool, merged here by string and classified on the GPU by
-the code-point classifier.
+to 21 chars ("fast" keys) and codes whose letters are all ACGTN or all acgtn with
+at most one '+' and <= 24 letters ("wide" keys: 12+12 dual indexes, lowercase
+files) are counted and classified entirely on the GPU.  Anything else ("exotic":
+mixed case, other bytes, longer codes) is captured verbatim by the GPU, merged by
+string inside the library (C++), and classified on the GPU by the code-point
+classifier.
 """
 from __future__ import annotations
 
@@ -23,6 +25,7 @@ import os
 import queue
 import re
 import threading
+from itertools import islice
 from datetime import datetime, timezone
 from pathlib import Path
 
@@ -40,10 +43,13 @@ _CTX = None
 
 
 def default_context() -> _lib.Context:
+    """This process's GPU context: LOCAL_RANK's device (one process per GPU; ranks share a GPU
+    only in single-GPU rehearsals of a multi-rank run)."""
     global _CTX
     if _CTX is None:
         dev = int(os.environ.get("LOCAL_RANK", "0"))
-        _CTX = _lib.Context(device=dev)
+        n = _lib.torch.cuda.device_count() if _lib.torch is not None else 0
+        _CTX = _lib.Context(device=dev % n if n else dev)
     return _CTX
 
 
@@ -110,54 +116,54 @@ class _GzReader:
                 self.t.join(0.01)
 
 
-def _file_done(ctx, st, fi, exo, exo_seen):
+def _replay_decode_error(path, sample):
+    """Error path only, after the GPU flagged invalid UTF-8 in a file.  The reference's exception
+    text (byte, position, reason) is relative to the chunk its text-mode reader handed the decoder
+    (frender.py:159: gzip.open(..., "rt"), whose chunk boundaries depend on the compressed
+    stream), and with -s it raises only if the bad bytes lie in a chunk read before the sample
+    ends (islice over the lines, :160-166).  So re-open the file the same way and read the same
+    lines: this raises exactly what the reference raises (UnicodeDecodeError, or the IndexError
+    of an earlier header without ' ', :169), or returns when the reference would not fail.
+    Nothing it reads feeds the tally."""
+    with gzip.open(path, "rt") as f:
+        for i, line in enumerate(islice(f, 0, None, 4)):
+            if sample and i >= sample:
+                return
+            if " " not in line:
+                raise IndexError("list index out of range")
+
+
+def _file_done(st, path=None, sample=None):
     """Per-file epilogue of scan_file (frender.py:160-181): the reference's exceptions for bad
-    input, and the exotic codes of this file merged by string.  Returns (exo_seen, new_here)."""
+    input.  Exotic codes are merged inside the library (fr_get_exotic_table) and counted in
+    st.new_keys."""
+    if st.utf8_bad:  # gzip.open(..., "rt") decode (frender.py:159)
+        if path is None:
+            raise UnicodeDecodeError("utf-8", b"", 0, 1, "invalid start byte")
+        _replay_decode_error(path, sample)
     if st.error == _lib.FR_SCAN_NO_SPACE:  # frender.py:169 split(" ")[1]
         raise IndexError("list index out of range")
-    if st.error == _lib.FR_SCAN_UTF8:  # gzip.open(..., "rt") decode (frender.py:159)
-        raise UnicodeDecodeError("utf-8", b"", 0, 1, "invalid start byte")
-    new_here = int(st.new_keys)
-    if st.exotic:
-        ords, lens, offs, pool = ctx.exotic(exo_seen, int(st.exotic))
-        for k in range(len(ords)):
-            code = bytes(pool[int(offs[k]):int(offs[k]) + int(lens[k])]).decode("utf-8")
-            e = exo.get(code)
-            if e is None:
-                exo[code] = [1, int(ords[k]), {fi}]
-                new_here += 1
-            else:
-                e[0] += 1
-                e[1] = min(e[1], int(ords[k]))
-                if fi not in e[2]:
-                    e[2].add(fi)
-                    new_here += 1
-        exo_seen += len(ords)
-    return exo_seen, new_here
 
 
-def tally_barcodes(cores, files, sample=None, ctx=None) -> UniqueTable:
-    """frender.py:183-207 (+ scan_file :154-181) on the GPU: files in order, one context."""
-    print(f"Scanning {len(files)} files with {cores} core{'' if cores == 1 else 's'}...")
-    if sample:
-        assert sample >= 1, "Number of reads to sample must be ≥ 1!"
-        print(f"Sampling {sample} reads from the head of each file...")
-    ctx = ctx or default_context()
-    ctx.reset()
-    names, records = [], []
-    exo: dict = {}
-    exo_seen = 0
+def scan_files(ctx, files, indices, sample, cores, on_file=None, after_file=None):
+    """scan_file (frender.py:154-181) for files[i], i in `indices` (increasing), into ctx's table:
+    up to `cores` files inflate ahead in helper threads while the GPU tallies them in order (the
+    reference's Pool over files, :189-193).  Every file is opened at its global index, so any
+    subset of a scan's files, on any GPU, yields the single-GPU ordinals.  on_file(i, name)
+    runs before a file is read (the reference's "Tallying barcodes from ..." line), after_file(i,
+    records, new barcodes) once it is tallied.  Returns {i: (records, new barcodes)}."""
+    out = {}
     ahead = max(1, int(cores))
     readers: dict = {}
     try:
-        for fi, path in enumerate(files):
-            for j in range(fi, min(len(files), fi + ahead)):
+        for k, fi in enumerate(indices):
+            for j in indices[k:k + ahead]:
                 if j not in readers:
                     readers[j] = _GzReader(files[j])
-            name = str(os.path.basename(path))
-            names.append(name)
-            print(f"Tallying barcodes from {name}...", end="")
-            ctx.begin_file(sample)
+            path = files[fi]
+            if on_file:
+                on_file(fi, str(os.path.basename(path)))
+            ctx.begin_file(sample, file_index=fi)
             rd = readers.pop(fi)
             try:
                 for chunk in rd:
@@ -166,20 +172,40 @@ def tally_barcodes(cores, files, sample=None, ctx=None) -> UniqueTable:
             finally:
                 rd.close()
             st = ctx.end_file()
-            exo_seen, new_here = _file_done(ctx, st, fi, exo, exo_seen)
-            records.append(int(st.records))
-            print(f"found {new_here} new barcode{'' if new_here == 1 else 's'} in {st.records} reads.")
+            _file_done(st, path, sample)
+            out[fi] = (int(st.records), int(st.new_keys))
+            if after_file:
+                after_file(fi, *out[fi])
     finally:
         for rd in readers.values():
             rd.close()
-    print(type([]), len(files))
+    return out
+
+
+def found_line(new_here, records) -> str:
+    return f"found {new_here} new barcode{'' if new_here == 1 else 's'} in {records} reads."
+
+
+def local_table(ctx) -> dict:
+    """This context's finalized tally as host arrays: fast/wide keys in first-occurrence order with
+    counts and first ordinals, their (unique index, file index) presence pairs, and the exotic codes
+    the library aggregated (bytes, counts, firsts, (code, file) presence)."""
     ctx.finalize()
     keys, counts, first = ctx.unique()
     pu, pf = ctx.presence()
+    ecodes, ecounts, efirst, epc, epf = ctx.exotic_table()
+    return {"keys": keys, "counts": counts, "first": first, "pu": pu, "pf": pf,
+            "ecodes": ecodes, "ecounts": ecounts, "efirst": efirst, "epc": epc, "epf": epf}
+
+
+def build_table(t: dict, names, records) -> UniqueTable:
+    """barcode_counter["total"] (frender.py:199-203) from a finalized tally: keyed and exotic codes
+    interleaved in (file, first occurrence) order."""
+    keys, counts, first = t["keys"], t["counts"], t["first"]
     fast_codes = _lib.decode_keys(keys)
-    exo_codes = list(exo.keys())
-    exo_counts = np.array([exo[c][0] for c in exo_codes], dtype=np.uint64)
-    exo_first = np.array([exo[c][1] for c in exo_codes], dtype=np.uint64)
+    exo_codes = [c.decode("utf-8") for c in t["ecodes"]]
+    exo_counts = np.asarray(t["ecounts"], dtype=np.uint64)
+    exo_first = np.asarray(t["efirst"], dtype=np.uint64)
     all_first = np.concatenate([first, exo_first])
     order = np.argsort(all_first, kind="stable")
     nf = len(fast_codes)
@@ -189,13 +215,38 @@ def tally_barcodes(cores, files, sample=None, ctx=None) -> UniqueTable:
     pos[order] = np.arange(order.size)
     fast_idx = np.where(order < nf, order, -1)
     exo_idx = np.where(order >= nf, order - nf, -1)
-    ep_u = [pos[nf + i] for i, c in enumerate(exo_codes) for _ in exo[c][2]]
-    ep_f = [f for c in exo_codes for f in sorted(exo[c][2])]
-    pres_u = np.concatenate([pos[pu.astype(np.int64)] if pu.size else np.zeros(0, np.int64),
-                             np.array(ep_u, dtype=np.int64)])
-    pres_f = np.concatenate([pf.astype(np.int64), np.array(ep_f, dtype=np.int64)])
+    pu, pf = np.asarray(t["pu"], dtype=np.int64), np.asarray(t["pf"], dtype=np.int64)
+    epc, epf = np.asarray(t["epc"], dtype=np.int64), np.asarray(t["epf"], dtype=np.int64)
+    pres_u = np.concatenate([pos[pu], pos[nf + epc]])
+    pres_f = np.concatenate([pf, epf])
     return UniqueTable(codes, np.concatenate([counts, exo_counts])[order], all_first[order], fast_idx, exo_idx,
-                       pres_u, pres_f, names, records)
+                       pres_u, pres_f, list(names), list(records))
+
+
+def tally_barcodes(cores, files, sample=None, ctx=None) -> UniqueTable:
+    """frender.py:183-207 (+ scan_file :154-181) on the GPU: files in order, one context.  With a
+    torch.distributed group of N > 1 ranks (one per GPU) the files are sharded over the GPUs
+    (frender_amd/dist.py: sharded_tally); rank 0 returns the merged table, other ranks None."""
+    from .dist import sharded_tally, world_group
+    group = world_group()
+    lead = group is None or group.get_rank() == 0  # the lines rank 0 prints for the whole job
+    if lead:
+        print(f"Scanning {len(files)} files with {cores} core{'' if cores == 1 else 's'}...")
+    if sample:
+        assert sample >= 1, "Number of reads to sample must be ≥ 1!"
+        if lead:
+            print(f"Sampling {sample} reads from the head of each file...")
+    ctx = ctx or default_context()
+    if group is not None:
+        return sharded_tally(group, ctx, files, sample, cores)
+    ctx.reset()
+    names = [str(os.path.basename(p)) for p in files]
+
+    per = scan_files(ctx, files, list(range(len(files))), sample, cores,
+                     on_file=lambda fi, name: print(f"Tallying barcodes from {name}...", end=""),
+                     after_file=lambda fi, records, new: print(found_line(new, records)))
+    print(type([]), len(files))
+    return build_table(local_table(ctx), names, [per[i][0] for i in range(len(files))])
 
 
 class Results:
@@ -434,6 +485,8 @@ def frender_scan(args, ctx=None) -> dict:
     files = parse_files(spec, just_r1=True)
     ctx = ctx or default_context()
     table = tally_barcodes(cores, files, sample, ctx=ctx)
+    if table is None:  # a rank > 0 of a multi-GPU scan: rank 0 classifies and writes the outputs
+        return None
     print("Scanning complete! Analyzing barcodes...")
     results = process(cores, table, indexes, num_subs, rc_mode, ctx=ctx)
     if rc_mode:

@@ -47,10 +47,11 @@ typedef struct fr_ctx fr_ctx;
 typedef struct fr_file_stats {
     uint64_t records;        /* header lines counted (after -s), = `actual_reads` (frender.py:160-166) */
     uint64_t lines;          /* lines in the file (universal newlines) */
-    uint64_t new_keys;       /* distinct fast-path codes in this file (`new_barcodes`, :175) */
-    uint64_t exotic;         /* records whose code left the fast alphabet (see fr_get_exotic) */
-    int32_t error;           /* FR_SCAN_* */
-    int32_t pad;
+    uint64_t new_keys;       /* distinct codes in this file, exotic ones included (`new_barcodes`, :175) */
+    uint64_t exotic;         /* records whose code is outside both key forms (see fr_get_exotic_table) */
+    int32_t error;           /* FR_SCAN_* (FR_SCAN_NO_SPACE wins when both were seen) */
+    int32_t utf8_bad;        /* 1: an invalid UTF-8 sequence lies in the bytes scanned (with -s possibly past the
+                              * sample: the host decides whether the reference's reader would decode it) */
     uint64_t error_offset;   /* file byte offset of the first offending header (FR_SCAN_NO_SPACE) */
 } fr_file_stats;
 
@@ -72,7 +73,8 @@ void fr_destroy(fr_ctx* ctx);
 const char* fr_last_error(const fr_ctx* ctx);
 int fr_get_timing(fr_ctx* ctx, fr_timing* out);
 int fr_sync(fr_ctx* ctx);
-/* diagnostics: {look-back max polls, total polls, keys, overflow, presence, exotic, grid, slots} */
+/* diagnostics: {look-back max polls, total polls, keys, overflow, presence, exotic, grid, slots,
+ * 8 phase stamps, speculation replays, exotic-only replays} */
 int fr_get_diag(fr_ctx* ctx, uint64_t* out, int n);
 
 /* ---- sample sheet (the idx1/idx2/id lists of get_indexes, frender.py:90-116) -------
@@ -95,6 +97,14 @@ int fr_set_sheet(fr_ctx* ctx, int S,
  * Files are fed in parse_files order (:604); fr_reset starts a new scan. */
 int fr_reset(fr_ctx* ctx);
 int fr_begin_file(fr_ctx* ctx, int64_t max_records /* -s, <=0: no limit */);
+/* fr_begin_file at a global position, for scans sharded over contexts / GPUs (SURVEY §8(e);
+ * replaces the per-file work unit of the reference's Pool, frender.py:189-193): file_index is the
+ * file's index in the whole scan's parse_files order and byte_base the file offset of the first
+ * byte this context will be fed (a record-aligned shard of the file; 0 for a whole file).  The
+ * ordinals ((file_index+1) << 44 | byte_base + offset), the presence pairs' file index and
+ * therefore the merged first-occurrence order are the single-context ones.  file_index must
+ * increase within a scan (fr_begin_file takes the next index). */
+int fr_begin_file_at(fr_ctx* ctx, int64_t file_index, uint64_t byte_base, int64_t max_records);
 /* Decoded (gunzipped) bytes of the current file, any split; the library cuts at
  * line ends, carries the remainder, copies through a pinned ring to HBM and
  * launches.  Returns FR_OK, or 5 (FR_SAMPLE_DONE) once -s records were seen. */
@@ -106,18 +116,26 @@ int fr_end_file(fr_ctx* ctx, fr_file_stats* out);
 
 /* ---- the merged unique table (barcode_counter["total"], :199-203) -----------------
  * fr_finalize compacts the device hash table and orders it by first occurrence
- * (file order, then byte offset) on the GPU; keys are 3-bit packed codes over
- * {A=1,C=2,G=3,T=4,N=5,'+'=6}, char i at bits [3i,3i+3). */
+ * (file order, then byte offset) on the GPU.  Keys: fast keys are 3-bit packed codes over
+ * {A=1,C=2,G=3,T=4,N=5,'+'=6}, char i at bits [3i,3i+3), at most 21 chars; wide keys (bit 63
+ * set) hold codes whose letters are all ACGTN or all acgtn, at most one '+', each part <= 21 and
+ * <= 24 letters in total: bit 62 lowercase, bits 57-61 the '+' position (letters before it; 31
+ * none), bits 0-56 V = sum d_i 5^i + (5^n - 1)/4 over the n letters, d: A0 C1 G2 T3 N4. */
 int fr_finalize(fr_ctx* ctx, uint64_t* n_unique, uint64_t* n_presence, uint64_t* n_exotic);
 int fr_get_unique(fr_ctx* ctx, uint64_t* keys, uint64_t* counts, uint64_t* first_ordinal);
 /* (unique index, file index) for every file a fast-path key occurs in (R10 demux_ok) */
 int fr_get_presence(fr_ctx* ctx, uint32_t* unique_idx, uint32_t* file_idx);
-/* exotic records [first, first+count) (count is clamped to those captured so far):
- * ordinal = (file index+1) << 44 | file byte offset of the header, code length, offset of
- * the code's bytes in the pool; pool receives the first pool_bytes bytes of the pool.
- * Returns the number of records written through *written. */
-int fr_get_exotic(fr_ctx* ctx, uint64_t first, uint64_t count, uint64_t* ordinal, uint32_t* length,
-                  uint64_t* pool_offset, uint8_t* pool, uint64_t pool_bytes, uint64_t* written);
+/* Codes outside both key forms ("exotic": mixed case, other bytes, more than 24 letters, a part
+ * longer than 21, two or more '+'), aggregated over the scan by exact byte string inside the
+ * library: the device captures each such record's code bytes, the library drains them after the
+ * launch that produced them (a launch that overflows the list is replayed capturing exotic codes
+ * only, after the list grows) and merges them natively.  Order: first drained, not first
+ * occurrence (use `first`).  fr_exotic_sizes gives the array sizes for fr_get_exotic_table:
+ * counts/first per code, offsets[n+1] into the concatenated code bytes, and (code, file index)
+ * presence pairs (R10). */
+int fr_exotic_sizes(fr_ctx* ctx, uint64_t* n_codes, uint64_t* code_bytes, uint64_t* n_presence);
+int fr_get_exotic_table(fr_ctx* ctx, uint64_t* counts, uint64_t* first, uint64_t* offsets, uint8_t* bytes,
+                        uint32_t* pres_code, uint32_t* pres_file);
 
 /* ---- classify: replaces process (:391-426) -> analyze_barcodes_with_rc (:294-351)
  *      -> analyze_barcode (:237-291) -> get_indexes_of_approx_matches (:214-234) ----

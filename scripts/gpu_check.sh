@@ -46,7 +46,11 @@ import json
 a = [json.loads(l) for l in open("gpurun_out/dist2.log") if l.startswith("{")][0]
 b = [json.loads(l) for l in open("gpurun_out/dist1.log") if l.startswith("{")][0]
 print("merged uniques", a["config"]["unique_codes"], "single", b["config"]["unique_codes"])
+print("merged checksum", a["config"]["table_checksum"], "single", b["config"]["table_checksum"])
+print("N=2 roofline", a["roofline"])
 assert a["config"]["unique_codes"] == b["config"]["unique_codes"]
+assert a["config"]["table_checksum"] == b["config"]["table_checksum"]  # every (key, count, first) row
+assert a["roofline"]["achieved"] > 0 and a["roofline"]["launches_per_step"] > 0
 PY
   exit $?
 fi

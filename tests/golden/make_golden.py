@@ -250,6 +250,21 @@ def all_cases():
                   sheet_rows=[("L1", "A" * 20, "C" * 20), ("L2", "C" * 20, "A" * 20)]),
         hand_case("unicode_header", {"a_R1.fq.gz": rec(hdr("AAAACCCC+GGGGTTTT")) + rec("@M1:ü:1 1:N:0:AAAACCCC+GGGGTTTT")}, {}),
         hand_case("bad_utf8", {"a_R1.fq.gz": (rec(hdr("AAAACCCC+GGGGTTTT")).encode() + b"@M1:\xff 1:N:0:AAAACCCC+GGGGTTTT\nAC\n+\nFF\n")}, {}),
+        # UTF-8 errors far into a file: the message's position is relative to the reader's decode chunk;
+        # with -s the reference fails only if the bad bytes are decoded before the sample ends
+        hand_case("bad_utf8_deep", {"a_R1.fq.gz": lines.encode() + b"@M1:x 1:N:0:AAAA\xc3\x28CCCC+GGGGTTTT\nAC\n+\nFF\n" +
+                                    lines.encode()}, {}),
+        hand_case("bad_utf8_past_sample", {"a_R1.fq.gz": lines.encode() + b"@M1:x 1:N:0:AAAACCCC+GGGGTTTT\xff\nAC\n+\nFF\n",
+                                           "b_R1.fq.gz": lines.encode()},
+                  {"s": 5, "files": ["a_R1.fq.gz", "b_R1.fq.gz"]}),
+        hand_case("bad_utf8_in_sample_chunk", {"a_R1.fq.gz": "".join(rec(hdr(c, i)) for i, c in enumerate(mix[:40])).encode() +
+                                               b"@M1:x 1:N:0:AAAACCCC+GGGGTTTT\xe2\x82\nAC\n+\nFF\n" + lines.encode()},
+                  {"s": 30}),
+        hand_case("wide_codes_12", {"a_R1.fq.gz": "".join(rec(hdr(c, i)) for i, c in enumerate(
+            ["AAAACCCCGGGG+TTTTAAAACCCC", "AAAACCCCGGGG+TTTTAAAACCCN", "aaaaccccgggg+ttttaaaacccc", "AAAACCCCGGGG+TTTTAAAACCCC",
+             "CCCCGGGGTTTT+AAAACCCCGGGG", "ACGTACGTACGT+ACGTACGTACGT", "AAAACCCCGGGa+TTTTAAAACCCC", "NNNNNNNNNNNN+NNNNNNNNNNNN",
+             "CCCCGGGGTTTT+AAAACCCCGGGG+ACGT", "AAAACCCCGGGG+TTTTAAAACCCG"] * 3))}, {"n": 1},
+            sheet_rows=[("W1", "AAAACCCCGGGG", "TTTTAAAACCCC"), ("W2", "CCCCGGGGTTTT", "AAAACCCCGGGG")]),
     ]
     return cases
 

@@ -68,11 +68,30 @@ def results_rows(r1_texts, sheet_idx1, sheet_idx2, ids, n):
     return rows
 
 
+SCAN_COLS = ["idx1", "idx2", "matched_idx1", "matched_idx2", "read_type", "sample_name", "reads", "demux_ok"]
+
+
 def write_results(path, rows, header=README_COLS):
+    """rows are README-ordered; a header naming the same columns in another order (scan's own CSV)
+    gets each row's fields in that order."""
+    perm = [README_COLS.index(h) for h in header] if sorted(header) == sorted(README_COLS) else None
     with open(path, "w", newline="") as f:
         f.write(",".join(header) + "\r\n")
         for r in rows:
-            f.write(",".join(r) + "\r\n")
+            f.write(",".join([r[i] for i in perm] if perm else r) + "\r\n")
+
+
+def readme_order_copy(src, dst):
+    """The build accepts scan's column order; the reference does not
+    (frender.py:649-657), so its expected outputs for such a case come from the same rows in
+    README order."""
+    import csv
+    with open(src, newline="") as f:
+        rows = list(csv.reader(f))
+    idx = [rows[0].index(c) for c in README_COLS]
+    with open(dst, "w", newline="") as f:
+        for r in rows:
+            f.write(",".join(r[i] for i in idx) + "\r\n")
 
 
 def syn_pair_case(name, S, n_reads, n_pairs, n=1, flags=None, nl="\n", r2_trim_lines=0, drop_codes=0,
@@ -133,9 +152,14 @@ def all_cases():
         syn_pair_case("syn_missing_code", 12, 1000, 1, drop_codes=1),
         syn_pair_case("syn_no_undet", 12, 1000, 1, flags={"no_undeter": True}),
         syn_pair_case("syn_no_samples", 12, 1000, 1, flags={"no_samples": True}),
-        syn_pair_case("syn_scan_order_csv", 12, 1000, 1,
-                      results_header=["idx1", "idx2", "matched_idx1", "matched_idx2", "read_type", "sample_name",
-                                      "reads", "demux_ok"]),
+        syn_pair_case("syn_scan_order_csv", 12, 1000, 1, results_header=SCAN_COLS,
+                      flags={"reference_reads_readme_order": True}),
+        # BASELINE config 5 shape: 96 samples, scan's own CSV fed to demux (paired, 2 lanes)
+        syn_pair_case("syn96_scan_csv", 96, 20000, 2, results_header=SCAN_COLS,
+                      flags={"reference_reads_readme_order": True}),
+        syn_pair_case("syn_bad_header", 12, 500, 1,
+                      results_header=["idx1", "idx2", "reads", "matched_idx1", "read_type", "matched_idx2",
+                                      "sample_name", "demux_ok"]),
         syn_pair_case("syn_bad_type", 12, 1000, 1, tamper=hop_to_weird),
         hand_case("hand_mixed", r1, r2, rows4),
         hand_case("hand_extra_colons", r1, r2.replace(" 2:N:0:", " 2:N:0:x:y:"), rows4),
@@ -146,7 +170,11 @@ def all_cases():
 
 
 def run_reference(ref, d, flags):
-    args = argparse.Namespace(r=os.path.join(d, "inputs", "results.csv"), d=os.path.join(d, "out"),
+    results = os.path.join(d, "inputs", "results.csv")
+    if flags.get("reference_reads_readme_order"):
+        results = os.path.join(d, "results_readme_order.csv")
+        readme_order_copy(os.path.join(d, "inputs", "results.csv"), results)
+    args = argparse.Namespace(r=results, d=os.path.join(d, "out"),
                               o=flags.get("o"), no_index_hop=flags.get("no_index_hop", False),
                               no_ambiguous=flags.get("no_ambiguous", False),
                               no_undeter=flags.get("no_undeter", False), no_samples=flags.get("no_samples", False),

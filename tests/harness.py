@@ -106,7 +106,7 @@ def compare(name: str, outs: dict, err, stdout: str, check_stdout: bool = True) 
     diffs = []
     if (err or {}).get("type") != (exp_err or {}).get("type"):
         diffs.append(f"error: got {err} expected {exp_err}")
-    elif err and err["type"] not in ("UnicodeDecodeError",) and err["msg"] != exp_err["msg"]:
+    elif err and err["msg"] != exp_err["msg"]:
         diffs.append(f"error message: got {err['msg']!r} expected {exp_err['msg']!r}")
     got = {_norm_name(k): v for k, v in outs.items()}
     exp = {_norm_name(k): v for k, v in exp_outs.items()}

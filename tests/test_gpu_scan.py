@@ -397,3 +397,229 @@ def test_demux_random_vs_oracle(seed, window, tmp_path):
         q = p.replace("o_ref", "o_gpu")
         with gzip.open(q, "rb") as g:
             assert g.read() == data, q
+
+
+def test_scan_then_demux_96_samples(tmp_path, monkeypatch):
+    """BASELINE config 5 shape end to end on the product path: `scan` (GPU) writes its CSV, `demux`
+    (GPU) routes a 96-sample paired set with that CSV (scan's own column order), and
+    every writer's decoded content equals the demux oracle's fed the same CSV."""
+    import argparse
+    import gzip
+    from frender_amd import synth
+    from frender_amd.demux import frender_demux
+    from frender_amd.scan import frender_scan
+    from oracle import demux_oracle
+
+    sheet = synth.make_sheet(96, 8, 8)
+    inp = tmp_path / "in"
+    inp.mkdir()
+    sheet.write_csv(str(tmp_path / "sheet.csv"))
+    r1_files = []
+    for lane in range(2):
+        t1 = synth.generate_bytes(sheet, lane * 150_000, 150_000, R=8, seed=3).decode()
+        lines = t1.split("\n")
+        t2 = "\n".join(ln.replace(" 1:N:", " 2:N:", 1) if i % 4 == 0 else (ln[::-1] if i % 4 in (1, 3) else ln)
+                       for i, ln in enumerate(lines))
+        for mate, text in (("R1", t1), ("R2", t2)):
+            p = inp / f"syn_L{lane + 1:03d}_{mate}_001.fastq.gz"
+            synth.write_fastq_gz(str(p), text.encode(), level=1)
+        r1_files.append(str(inp / f"syn_L{lane + 1:03d}_R1_001.fastq.gz"))
+    monkeypatch.chdir(tmp_path)
+    frender_scan(argparse.Namespace(n=1, rc=False, c=2.0, s=None, o="cfg5", p=None, b=str(tmp_path / "sheet.csv"),
+                                    files=r1_files))
+    csvs = [f for f in tmp_path.iterdir() if f.name.startswith("frender-scan-results_")]
+    assert len(csvs) == 1
+    files = sorted(str(p) for p in inp.iterdir())
+
+    def ns(d):
+        return argparse.Namespace(r=str(csvs[0]), d=str(tmp_path / d), o=None, no_index_hop=False,
+                                  no_ambiguous=False, no_undeter=False, no_samples=False, files=files)
+
+    want = demux_oracle.demux(ns("o_ref"))
+    frender_demux(ns("o_gpu"))
+    assert len(want) >= 2 * 99
+    for p, data in want.items():
+        with gzip.open(p.replace("o_ref", "o_gpu"), "rb") as g:
+            assert g.read() == data, p
+
+
+# ---------------------------------------------------------------------------------------
+# multi-GPU product path: `scan --gpus 2` rehearsed on this box's GPU (2 ranks, gloo)
+# ---------------------------------------------------------------------------------------
+@pytest.mark.parametrize("name", ["s96_n1_4files", "s96_n1_rc", "two_files_order", "sample_limit",
+                                  "demux_ok_samples", "same_file_twice", "wide_codes_12", "no_space_header"])
+def test_cli_two_ranks_match_golden(name, tmp_path):
+    """`python -m frender_amd scan --gpus 2` (files sharded over two ranks, tables merged on rank 0)
+    writes the reference's CSV bytes and per-file lines (frender.py:189-205 merge), and raises the
+    first file's error as one GPU would."""
+    import os
+    import re
+    import subprocess
+    import sys
+    from harness import build_inputs, compare
+
+    d = str(tmp_path)
+    spec = build_inputs(name, d)
+    a = spec["args"]
+    cmd = [sys.executable, "-m", "frender_amd", "scan", "-n", str(a["n"]), "-c", str(a["c"]), "--gpus", "2"]
+    if a["rc"]:
+        cmd.append("-rc")
+    for flag in ("s", "o", "p", "b"):
+        if a.get(flag) is not None:
+            cmd += [f"-{flag}", str(a[flag])]
+    cmd += a["files"]
+    env = dict(os.environ, FRENDER_DIST_BACKEND="gloo",
+               PYTHONPATH=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    before = set(os.listdir(d))
+    r = subprocess.run(cmd, cwd=d, env=env, capture_output=True, text=True, timeout=240)
+    outs = {}
+    for fn in sorted(set(os.listdir(d)) - before):
+        with open(os.path.join(d, fn), "rb") as f:
+            outs[fn] = f.read()
+    err = None
+    if r.returncode:
+        lines = [re.sub(r"^\[rank\d+\]: ", "", ln) for ln in r.stderr.strip().splitlines()]
+        last = [ln for ln in lines if ln and not ln.startswith(" ")][-1]
+        typ, _, msg = last.partition(": ")
+        err = {"type": typ, "msg": msg}
+    diffs = compare(name, outs, err, r.stdout)
+    assert not diffs, "\n".join(diffs) + "\n" + r.stderr[-2000:]
+
+
+# ---------------------------------------------------------------------------------------
+# wide keys, exotic volume, universal newlines on the host feed, byte shards
+# ---------------------------------------------------------------------------------------
+def full_tally(c, files, mode="host", sample=None, piece=1 << 22):
+    """Every code (fast, wide, exotic) through the library, in first-occurrence order."""
+    from frender_amd import scan
+    c.reset()
+    recs = []
+    for fi, data in enumerate(files):
+        c.begin_file(sample, file_index=fi)
+        if mode == "device":
+            p = c.device_alloc(len(data) + 16)
+            try:
+                if data:
+                    c.copy_to_device(p, data)
+                c.feed_device(p, len(data))
+                st = c.end_file()
+            finally:
+                c.device_free(p)
+        else:
+            for pos in range(0, len(data), piece):
+                if c.feed(data[pos:pos + piece]):
+                    break
+            st = c.end_file()
+        assert st.error == 0
+        recs.append(int(st.records))
+    t = scan.build_table(scan.local_table(c), [f"f{i}" for i in range(len(files))], recs)
+    return dict(zip(t.codes, t.counts.tolist())), recs, t
+
+
+def _records(codes, nl="\n"):
+    return "".join(f"@r{i} 1:N:0:{cd}{nl}ACGT{nl}+{nl}FFFF{nl}" for i, cd in enumerate(codes)).encode()
+
+
+@pytest.mark.parametrize("mode", ["host", "device"])
+def test_wide_codes_12_12_and_lowercase(lib, mode):
+    """12+12 dual indexes and all-lowercase codes are wide keys counted on the GPU: bit-exact vs the
+    oracle, with no exotic (host) records."""
+    rng = np.random.default_rng(5)
+    n = 1_500_000
+    idx = ["".join("ACGT"[x] for x in rng.integers(0, 4, 12)) for _ in range(300)]
+    a = rng.integers(0, 300, n)
+    b = rng.integers(0, 300, n)
+    codes = [idx[i] + "+" + idx[j] for i, j in zip(a.tolist(), b.tolist())]
+    for k in rng.integers(0, n, 5000).tolist():
+        codes[k] = codes[k][:5] + "N" + codes[k][6:]
+    lower = [c.lower() for c in codes[: n // 2]]
+    files = [_records(codes), _records(lower)]
+    c = lib.Context(device=0, chunk_bytes=64 << 20, table_slots=1 << 16)
+    try:
+        got, recs, t = full_tally(c, files, mode)
+        assert (t.exo_idx < 0).all()  # nothing left the GPU's key forms
+        assert_same((got, recs), oracle_tally(files))
+    finally:
+        c.close()
+
+
+@pytest.mark.parametrize("mode", ["host", "device"])
+def test_exotic_volume_grows_and_replays(lib, mode):
+    """More exotic records (mixed case, other bytes) than the initial list holds, in single
+    launches: the library replays the launch capturing exotic codes only, grows the list and
+    merges natively; bit-exact vs the oracle."""
+    rng = np.random.default_rng(9)
+    n = 1_300_000
+    base = ["AcGtAcGt+TTGGCCAA", "xyz+ACGT", "ACGT+acgt", "A.C+GT", "ÄC+GT"]
+    codes = [base[k] + str(v) for k, v in zip(rng.integers(0, 5, n).tolist(), rng.integers(0, 50000, n).tolist())]
+    codes[::7] = ["ACGTACGT+ACGTACGT"] * len(codes[::7])
+    files = [_records(codes), _records(codes[:1000])]
+    c = lib.Context(device=0, chunk_bytes=256 << 20, table_slots=1 << 16)
+    try:
+        got, recs, _ = full_tally(c, files, mode, piece=64 << 20)
+        assert_same((got, recs), oracle_tally(files))
+        assert c.diag()["exo_replays"] >= 1
+    finally:
+        c.close()
+
+
+def test_cr_only_large_host_feed(lib):
+    """Universal newlines on the host feed: a >= 8 MiB file with lone '\\r' line ends through a 1 MiB
+    ring cuts at its '\\r's (a CRLF is never split)."""
+    rng = random.Random(4)
+    data = random_fastq(rng, 120_000, styles=("\r",))
+    assert len(data) >= 8 << 20
+    mixed = random_fastq(rng, 60_000, styles=("\r", "\r\n", "\n"))
+    c = lib.Context(device=0, chunk_bytes=1 << 20, table_slots=1 << 16)
+    try:
+        for piece in (1 << 20, 999_983, 4096):
+            got = full_tally(c, [data, mixed], "host", piece=piece)
+            assert_same(got[:2], oracle_tally([data, mixed]))
+    finally:
+        c.close()
+
+
+def test_byte_shards_merge_to_whole_file(lib):
+    """fr_begin_file_at: one file tallied as record-aligned byte shards on separate contexts and
+    merged (count = sum, first = min) equals the whole file on one context, row for row (the
+    bench's N-GPU record shards and their ordinals)."""
+    from frender_amd import synth
+    sheet = synth.make_sheet(96, 8, 8)
+    reclen = synth.record_length(8, 8, 8)
+    n = 600_000
+    data = synth.generate_bytes(sheet, 0, n, R=8, seed=2)
+    whole = lib.Context(device=0, chunk_bytes=8 << 20, table_slots=1 << 16)
+    merged = lib.Context(device=0, chunk_bytes=8 << 20, table_slots=1 << 16)
+    shards = [lib.Context(device=0, chunk_bytes=8 << 20, table_slots=1 << 16) for _ in range(3)]
+    try:
+        whole.reset()
+        whole.begin_file(None, file_index=2)
+        whole.feed(data)
+        whole.end_file()
+        whole.finalize()
+        want = whole.unique()
+        cuts = [0, 123_457, 400_001, n]
+        merged.reset()
+        for k, c in enumerate(shards):
+            part = data[cuts[k] * reclen:cuts[k + 1] * reclen]
+            c.reset()
+            c.begin_file(None, file_index=2, byte_base=cuts[k] * reclen)
+            p = c.device_alloc(len(part) + 16)
+            c.copy_to_device(p, part)
+            c.feed_device(p, len(part))
+            assert c.end_file().records == cuts[k + 1] - cuts[k]
+            c.device_free(p)
+            U, _, _ = c.finalize()
+            bufs = [c.device_alloc(8 * U) for _ in range(3)]
+            c.export_unique_device(*bufs, U)
+            merged.merge_unique_device(*bufs, U)
+            merged.sync()
+            for b in bufs:
+                c.device_free(b)
+        merged.finalize()
+        got = merged.unique()
+        for x, y in zip(got, want):
+            assert np.array_equal(x, y)
+    finally:
+        for c in [whole, merged] + shards:
+            c.close()

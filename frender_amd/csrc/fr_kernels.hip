@@ -28,6 +28,13 @@ namespace fr {
 #ifndef FR_PREFETCH
 #define FR_PREFETCH 0  // load tile t+1's segment before tile t's header parse
 #endif
+#ifndef FR_LDS_RAW
+#define FR_LDS_RAW 1  // keep each tile's raw bytes in LDS for the parse (code bytes read from LDS, not L2);
+                      // the next tile's segment loads are issued right after this tile's bytes are stored
+#endif
+#ifndef FR_SEG_AUX
+#define FR_SEG_AUX 0  // cache policy bits of the segment stream loads (2 = nt)
+#endif
 
 // FR_OUTLINE_COLD=1 keeps the rare paths out of line (measured slower: the calls make the
 // hot loop save registers to scratch)
@@ -166,6 +173,9 @@ struct alignas(16) LSlot {  // one ds_read_b128 reads key, count and first offse
 };
 
 struct ScanShared {
+#if FR_LDS_RAW
+    u32 raw[TILE / 4];  // the current tile's bytes (stored after B1, read by the parse after B2)
+#endif
     LSlot ls[NS];     // LDS hash table of this workgroup's chunk
     u32 wsum[WG / 64];
     u64 tile_excl;
@@ -535,7 +545,7 @@ __device__ __forceinline__ void seg_fetch(const ScanArgs& a, u32 t, SegRegs& r, 
                                                         0x00020000);
 #pragma unroll
     for (int k = 0; k < SEG / 16; ++k) {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, tid * SEG, k * 16, 0);
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, tid * SEG, k * 16, FR_SEG_AUX);
         r.v[k] = make_uint4(v[0], v[1], v[2], v[3]);
     }
     r.nx = with_nx ? __builtin_amdgcn_raw_buffer_load_b32(rsrc, tid * SEG + SEG, 0, 0) : 0u;  // '\r' path only
@@ -949,10 +959,27 @@ __device__ __forceinline__ bool encode_pack(const u32 (&w)[8], u32 start, u32 n,
     return bad == 0;
 }
 
-__device__ __forceinline__ bool encode_glob(const ScanArgs& a, u64 tile0, u32 start, u32 n, u64& key) {
+// the code window from the tile's LDS copy: eight dwords from start & ~3 (bytes past the tile read the
+// struct's next fields; encode_pack masks them off)
+__device__ __forceinline__ void encode_load_lds(const ScanShared& sh, u32 start, u32 (&w)[8]) {
+#if FR_LDS_RAW
+    const __attribute__((address_space(3))) u32* p =
+        (const __attribute__((address_space(3))) u32*)(&sh.raw[0]) + (start >> 2);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) w[k] = p[k];
+#else
+    (void)sh; (void)start;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) w[k] = 0;
+#endif
+}
+
+__device__ __forceinline__ bool encode_glob(const ScanShared& sh, const ScanArgs& a, u64 tile0, u32 start, u32 n,
+                                            u64& key) {
     if (n < 1 || n > (u32)MAXSYM) return false;
     u32 w[8];
-    encode_load(a, tile0, start, w);
+    if (FR_LDS_RAW) encode_load_lds(sh, start, w);
+    else encode_load(a, tile0, start, w);
     return encode_pack(w, start, n, key);
 }
 
@@ -1016,8 +1043,8 @@ __device__ __forceinline__ void process_header_bm(ScanShared& sh, const ScanArgs
             asm volatile("" ::"v"(start), "v"(n));
             return;
         }
-        if ((u64)(start & ~3u) + 32u > a.avail - tile0) r = 2;  // the loads would straddle the data end
-        else fast = encode_glob(a, tile0, start, n, key);
+        if (!FR_LDS_RAW && (u64)(start & ~3u) + 32u > a.avail - tile0) r = 2;  // the loads would straddle the data end
+        else fast = encode_glob(sh, a, tile0, start, n, key);
     }
     if (fast) count_code(sh, a, tile0, p, key);
     else rare_push(sh, a, (u32)(tile0 + p), (u32)r, (u32)(tile0 + start), n);
@@ -1072,8 +1099,11 @@ __device__ __forceinline__ void parse_own_headers(ScanShared& sh, const ScanArgs
     u32 w[8];
     if (p1 >= 0) {
         rr = locate_code_bm(sh, (u32)p1, bl, start, n);
-        if (rr == 0 && (u64)(start & ~3u) + 32u > a.avail - tile0) rr = 2;  // loads would straddle the data end
-        if (rr == 0 && !(a.ablate & 2u)) encode_load(a, tile0, start, w);
+        if (!FR_LDS_RAW && rr == 0 && (u64)(start & ~3u) + 32u > a.avail - tile0) rr = 2;  // loads would straddle the data end
+        if (rr == 0 && !(a.ablate & 2u)) {
+            if (FR_LDS_RAW) encode_load_lds(sh, start, w);
+            else encode_load(a, tile0, start, w);
+        }
     }
     // always five loads (zeros when there is no next tile or it reaches the data end), so the
     // compiler's wait counts for the code bytes stay exact on every path
@@ -1108,7 +1138,10 @@ __device__ __forceinline__ u64 walk_chunk(ScanShared& sh, const ScanArgs& a, u32
     u64 tm0 = 0, tm1 = 0, tm2 = 0, tm3 = 0;
     const u64 w0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
 #endif
-#if FR_PREFETCH
+#if FR_LDS_RAW
+    SegRegs r;  // tile t's segment, loaded during tile t-1 (the chunk's first tile here)
+    if (tb < te) seg_prefetch_next(a, tb, r, tid);
+#elif FR_PREFETCH
     // the next tile's segment is loaded during this tile's parse (parse_own_headers), so its HBM
     // latency overlaps the parse; a tile reaching the data end is loaded bytewise instead
     SegRegs r;
@@ -1118,7 +1151,8 @@ __device__ __forceinline__ u64 walk_chunk(ScanShared& sh, const ScanArgs& a, u32
 #if FR_TIMING
         const u64 c0 = __builtin_amdgcn_s_memtime();
 #endif
-#if FR_PREFETCH
+#if FR_LDS_RAW
+#elif FR_PREFETCH
         if (!seg_in_range(a, t)) r = seg_load_tail(a, t, tid);
 #else
         SegRegs r;
@@ -1138,6 +1172,20 @@ __device__ __forceinline__ u64 walk_chunk(ScanShared& sh, const ScanArgs& a, u32
             done = tail;
         }
         seg_store(sh, sc, tid, lane, wid);
+#if FR_LDS_RAW
+        {  // this tile's bytes for the parse, then the next tile's loads (in flight through the parse)
+            typedef u32 u32x4 __attribute__((ext_vector_type(4)));
+            __attribute__((address_space(3))) u32x4* dst =
+                (__attribute__((address_space(3))) u32x4*)(&sh.raw[0]) + tid * (SEG / 16);
+#pragma unroll
+            for (int k = 0; k < SEG / 16; ++k) {
+                u32x4 v;
+                v.x = r.v[k].x; v.y = r.v[k].y; v.z = r.v[k].z; v.w = r.v[k].w;
+                dst[k] = v;
+            }
+            if (t + 1 < te) seg_prefetch_next(a, t + 1, r, tid);
+        }
+#endif
         lds_barrier();  // B2
 #if FR_TIMING
         const u64 c2 = __builtin_amdgcn_s_memtime();
@@ -1265,9 +1313,10 @@ __device__ __forceinline__ void chunk_bounds(const ScanArgs& a, u32 c, u32& tb, 
 }
 
 #ifndef FR_OCC
-#define FR_OCC 5  // workgroups (= waves per SIMD) per CU: 5 caps the kernel at 96 VGPRs (LDS would allow 7;
-                  // measured best at 5, with the '\r' path re-reading its segment so no class word stays live); fr_api
-                  // sizes the grid with fr_chunk_occupancy()
+#define FR_OCC 4  // workgroups (= waves per SIMD) per CU: the tile's LDS copy (FR_LDS_RAW) makes a workgroup
+                  // 39 KB, so 4 share a CU's 160 KB; 128 VGPRs hold the next tile's loads through the parse
+                  // (without the LDS copy 5 per CU at 96 VGPRs measured best); fr_api sizes the grid with
+                  // fr_chunk_occupancy()
 #endif
 __global__ __launch_bounds__(WG, FR_OCC) void chunk_kernel(ScanArgs args) {
     // every helper reads the arguments where they lie (the kernarg segment): the out-of-line

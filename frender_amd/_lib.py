@@ -41,7 +41,8 @@ class FileStats(C.Structure):
 
 class Timing(C.Structure):
     _fields_ = [("scan_launches", C.c_uint64), ("scan_bytes", C.c_uint64), ("scan_ms", C.c_double),
-                ("last_scan_ms", C.c_double), ("classify_ms", C.c_double), ("finalize_ms", C.c_double)]
+                ("last_scan_ms", C.c_double), ("classify_ms", C.c_double), ("finalize_ms", C.c_double),
+                ("log_ms", C.c_double)]
 
 
 if not os.path.exists(LIB_PATH):

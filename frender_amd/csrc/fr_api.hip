@@ -28,6 +28,13 @@ struct fr_ctx {
     u32 ablate = 0;
     u64* cold = nullptr;
     u32 cold_cap = 8192;
+    // launch log (fr_internal.h LogEntry): commits append, launch_log_aggregate folds it into the table
+    LogEntry* log = nullptr;
+    LogEntry* log_sorted = nullptr;
+    u64 log_cap = 0;
+    u32* log_hist = nullptr;
+    void* log_temp = nullptr;
+    size_t log_temp_bytes = 0;
     uint4* rare = nullptr;
 
     DevState* st = nullptr;
@@ -134,7 +141,7 @@ struct fr_ctx {
     int rc_names_cap = 0;
 
     // timing
-    std::vector<hipEvent_t> ev_a, ev_b;
+    std::vector<hipEvent_t> ev_a, ev_b, ev_l;
     size_t ev_used = 0;
     u64 scan_launches = 0, scan_bytes = 0;
     double classify_ms = 0, finalize_ms = 0;
@@ -363,6 +370,7 @@ static int replay_exotic(fr_ctx* ctx) {
     ScanArgs a = ctx->last_args;
     a.exo_only = 1;
     a.spec_commit = 0;
+    a.log = nullptr;
     a.epoch = ++ctx->epoch;
     a.tab = ctx->d_tab;
     CK(hipMemsetAsync(&ctx->st->ticket, 0, 2 * sizeof(u32), ctx->stream));  // ticket, chunks_done
@@ -438,11 +446,13 @@ static int launch_range(fr_ctx* ctx, const u8* dptr, u64 len, u64 avail, int own
     CK(hipMemsetAsync(&ctx->st->ticket, 0, 2 * sizeof(u32), ctx->stream));  // ticket, chunks_done
     ctx->st_fresh = false;
     if (ctx->ev_used == ctx->ev_a.size()) {
-        hipEvent_t e1, e2;
+        hipEvent_t e1, e2, e3;
         CK(hipEventCreate(&e1));
         CK(hipEventCreate(&e2));
+        CK(hipEventCreate(&e3));
         ctx->ev_a.push_back(e1);
         ctx->ev_b.push_back(e2);
+        ctx->ev_l.push_back(e3);
     }
     CK(hipEventRecord(ctx->ev_a[ctx->ev_used], ctx->stream));
     // chunking (chunk_bounds in fr_kernels.hip): ramped when the range holds both ramps and a full
@@ -462,6 +472,8 @@ static int launch_range(fr_ctx* ctx, const u8* dptr, u64 len, u64 avail, int own
     }
     a.cold_cap = ctx->cold_cap;
     a.cold = ctx->cold;
+    a.log = exo_only ? nullptr : ctx->log;
+    a.log_cap = ctx->log_cap;
     a.rare = ctx->rare;
     // workgroups take chunks by ticket; never more than the resident grid (cold lists are per block)
     const int grid = (int)std::min<u64>(a.num_chunks, G);
@@ -471,6 +483,10 @@ static int launch_range(fr_ctx* ctx, const u8* dptr, u64 len, u64 avail, int own
     ctx->last_grid = grid;
     ctx->last_valid = true;
     CK(hipEventRecord(ctx->ev_b[ctx->ev_used], ctx->stream));
+    if (a.log)
+        CK(launch_log_aggregate(ctx->tab, ctx->st, ctx->log, ctx->log_sorted, ctx->log_cap, ctx->log_hist,
+                                ctx->log_temp, ctx->log_temp_bytes, ctx->stream));
+    CK(hipEventRecord(ctx->ev_l[ctx->ev_used], ctx->stream));
     ctx->ev_used++;
     ctx->scan_launches++;
     ctx->scan_bytes += len;
@@ -507,6 +523,18 @@ fr_ctx* fr_create(int device, uint64_t chunk_bytes, uint64_t table_slots) {
     ctx->chunk_bytes = chunk_bytes ? ((chunk_bytes + TILE - 1) / TILE) * TILE : (256ull << 20);
     if (ctx->chunk_bytes > RANGE_MAX) ctx->chunk_bytes = RANGE_MAX;
     ctx->ring_bytes = std::min<u64>(ctx->chunk_bytes, HOST_CHUNK_MAX);
+    // launch log: room for one pair per 256 B of a launch (SYN-v1 needs one per 350-500 B; a
+    // commit that does not fit inserts into the table directly)
+    const char* fl = getenv("FR_LOG");  // off by default until the aggregation beats direct commits everywhere
+    if (fl && atoi(fl) != 0) {
+        ctx->log_cap = std::min<u64>(std::max<u64>(ctx->chunk_bytes / 256, 1ull << 16), 1ull << 26);
+        if ((e = dalloc(&ctx->log, ctx->log_cap)) != hipSuccess) return bad("launch log", e);
+        if ((e = dalloc(&ctx->log_sorted, ctx->log_cap)) != hipSuccess) return bad("launch log", e);
+        if ((e = dalloc(&ctx->log_hist, 2ull * AGG_NB * AGG_SLICES)) != hipSuccess) return bad("log histogram", e);
+        ctx->log_temp_bytes = log_aggregate_temp_bytes();
+        if ((e = hipMalloc(&ctx->log_temp, std::max<size_t>(ctx->log_temp_bytes, 16))) != hipSuccess)
+            return bad("log scan", e);
+    }
     if (const char* f = getenv("FR_CHUNK_TILES")) ctx->chunk_tiles = (u32)std::max(2, atoi(f));
     if (const char* f = getenv("FR_RAMP")) ctx->ramp = atoi(f) != 0;
     ctx->tiles_cap = RANGE_MAX / TSTEP + 2;
@@ -564,7 +592,7 @@ void fr_destroy(fr_ctx* ctx) {
                    ctx->d_keys, ctx->d_counts, ctx->d_first, ctx->d_keys_s, ctx->d_counts_s,
                    ctx->d_first_s, ctx->d_pos, ctx->d_perm, ctx->d_rank, ctx->d_counter, ctx->d_temp, ctx->d_pres_u,
                    ctx->d_pres_f, ctx->d_m1, ctx->d_m2, ctx->d_row, ctx->d_rm2, ctx->d_rrow, ctx->d_cls, ctx->d_rcls,
-                   ctx->d_errw, ctx->d_errf, ctx->d_rcf, ctx->d_rcr, ctx->cold, ctx->rare, ctx->chunk_info};
+                   ctx->d_errw, ctx->d_errf, ctx->d_rcf, ctx->d_rcr, ctx->cold, ctx->rare, ctx->chunk_info, ctx->log, ctx->log_sorted, ctx->log_hist, ctx->log_temp};
     for (void* p : dev)
         if (p) (void)hipFree(p);
     if (ctx->h_st) (void)hipHostFree(ctx->h_st);
@@ -578,6 +606,7 @@ void fr_destroy(fr_ctx* ctx) {
     }
     for (auto e : ctx->ev_a) (void)hipEventDestroy(e);
     for (auto e : ctx->ev_b) (void)hipEventDestroy(e);
+    for (auto e : ctx->ev_l) (void)hipEventDestroy(e);
     if (ctx->st_ev) (void)hipEventDestroy(ctx->st_ev);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->copy) (void)hipStreamDestroy(ctx->copy);
@@ -605,13 +634,16 @@ int fr_sync(fr_ctx* ctx) {
 
 int fr_get_timing(fr_ctx* ctx, fr_timing* out) {
     CK(hipStreamSynchronize(ctx->stream));
-    double tot = 0, last = 0;
+    double tot = 0, last = 0, lg = 0;
     for (size_t i = 0; i < ctx->ev_used; ++i) {
-        float ms = 0;
+        float ms = 0, ml = 0;
         CK(hipEventElapsedTime(&ms, ctx->ev_a[i], ctx->ev_b[i]));
+        CK(hipEventElapsedTime(&ml, ctx->ev_b[i], ctx->ev_l[i]));
         tot += ms;
         last = ms;
+        lg += ml;
     }
+    out->log_ms = lg;
     out->scan_launches = ctx->scan_launches;
     out->scan_bytes = ctx->scan_bytes;
     out->scan_ms = tot;

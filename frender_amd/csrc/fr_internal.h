@@ -69,6 +69,20 @@ struct alignas(32) Overflow {
     u32 tag, pad;
 };
 
+// One tallied (code, count) pair on its way to the HBM table: a chunk's LDS-table slots and cold-list
+// misses are appended to the launch's log at the chunk's commit; after the launch the log is
+// bucketed by key hash and each bucket is aggregated in LDS, so the HBM table sees one insert per
+// distinct code per launch instead of one per commit and miss.
+struct alignas(8) LogEntry {
+    u64 key;
+    u64 ord;             // min ordinal of the entry's records
+    u32 cnt;
+    u32 tag;             // file tag
+};
+constexpr int AGG_LOG_NB = 12;             // log2 of the buckets of the launch-log aggregation
+constexpr int AGG_NB = 1 << AGG_LOG_NB;
+constexpr int AGG_SLICES = 256;            // histogram / scatter workgroups (slices of the log)
+
 struct DevState {
     u64 lines[2];        // terminators before the current range (launch parity)
     u32 ticket;          // chunk ticket, zeroed before every launch
@@ -86,6 +100,7 @@ struct DevState {
     u32 cap_flags;       // 1 presence, 2 overflow list, 4 exotic pool
     u32 spin_max;        // diagnostics: longest look-back wait (polls)
     u64 spin_total;      // diagnostics: total look-back polls that found a window not ready
+    u64 log_n;           // entries appended to the launch log (may exceed its capacity: the rest went to HBM)
     u64 stamp[8];        // diagnostics (FR_STAMPS builds only): per-phase shader cycles, summed over workgroups
 };
 
@@ -129,6 +144,8 @@ struct ScanArgs {
     u64* cold;           // chunk kernel: cold lists, [grid][cold_cap] x {key, ordinal}
     uint4* rare;         // chunk kernel: rare-event rings, [grid][RARE_RING] (fr_kernels.hip)
     u64* chunk_info;     // chunk kernel: per chunk {line count, spec flag + guessed phase << 1 in the high word}
+    LogEntry* log;       // the launch log (nullptr: commits insert into the HBM table directly)
+    u64 log_cap;
     u32 exo_only;        // replay of a launch whose exotic list overflowed: capture exotic records only (no
                          // table updates), every chunk with its exact line phase
     u32 spec_commit;     // commit speculative chunks without waiting for their exact prefix (checked at the
@@ -201,6 +218,10 @@ hipError_t launch_presence_scan(const GSlot* slots, u64 n, u32 tag, Presence* pr
                                 hipStream_t s);
 hipError_t launch_merge(Table t, DevState* st, const u64* keys, const u64* counts, const u64* first, u64 n,
                         hipStream_t s);
+// aggregate the launch log into the table and empty it (stream-ordered; reads log_n on the device)
+hipError_t launch_log_aggregate(Table t, DevState* st, LogEntry* log, LogEntry* sorted, u64 cap, u32* hist,
+                                void* temp, size_t temp_bytes, hipStream_t s);
+size_t log_aggregate_temp_bytes();
 hipError_t launch_synth(u8* out, u64 r0, u64 n, int R, u64 seed, const u8* idx1, const u8* idx2, int S, int L1,
                         int L2, hipStream_t s);
 

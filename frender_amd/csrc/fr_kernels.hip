@@ -32,6 +32,9 @@ namespace fr {
 #define FR_LDS_RAW 1  // keep each tile's raw bytes in LDS for the parse (code bytes read from LDS, not L2);
                       // the next tile's segment loads are issued right after this tile's bytes are stored
 #endif
+#ifndef FR_PF_DEPTH
+#define FR_PF_DEPTH 1  // FR_LDS_RAW: tiles of segment loads each wave keeps in flight (1 or 2 register sets)
+#endif
 #ifndef FR_SEG_AUX
 #define FR_SEG_AUX 0  // cache policy bits of the segment stream loads (2 = nt)
 #endif
@@ -186,6 +189,8 @@ struct ScanShared {
     u32 flags;
     u32 rq_tail;      // rare-event ring: events pushed by this workgroup (monotonic)
     u32 last;         // this workgroup published the launch's last chunk count (runs verify_launch)
+    u32 log_pos;      // commit: next free entry of this commit's launch-log block
+    u64 log_base;     // commit: the block's first entry (~0: the block did not fit, insert directly)
     // ---- chunk kernel state ----
     u32 buffered;     // LDS-table misses go to this workgroup's cold list (committed later)
     u32 spec;         // speculating on the line phase: exotic records / errors are buffered
@@ -838,7 +843,31 @@ __device__ __attribute__((noinline)) void commit_buffers(ScanShared& sh, const S
     }
     const bool flush = table && !(a.ablate & 8u);  // ablation 8: no HBM flush of the LDS table / cold list
     const u32 nc = (a.ablate & 8u) ? 0u : min(sh.ncold, a.cold_cap);
-    if (flush) {
+    const u32 nl = flush ? sh.nkeys : 0u;  // claimed LDS slots = the live ones
+    bool logged = false;
+    if (a.log && nl + nc) {
+        // one block of the launch log for this commit's pairs (aggregated after the launch:
+        // launch_log_aggregate); a block past the log's end is blanked and the pairs inserted below
+        if (tid == 0) {
+            const u64 base = atomicAdd((unsigned long long*)&a.st->log_n, (unsigned long long)(nl + nc));
+            sh.log_base = base + nl + nc <= a.log_cap ? base : ~0ull;
+            sh.log_pos = 0;
+            if (base + nl + nc > a.log_cap)
+                for (u64 i = base; i < a.log_cap; ++i) a.log[i] = LogEntry{0, 0, 0, 0};
+        }
+        __syncthreads();
+        logged = sh.log_base != ~0ull;
+    }
+    if (logged) {
+        LogEntry* out = a.log + sh.log_base;
+        if (flush)
+            for (int i = tid; i < NS; i += WG) {
+                const LSlot e = sh.ls[i];
+                if (e.key) out[atomicAdd(&sh.log_pos, 1u)] = LogEntry{e.key, make_ord(a, e.mino), e.cnt, a.file_tag};
+            }
+        const u64* cl = a.cold + 2ull * (u64)blockIdx.x * a.cold_cap;
+        for (u32 i = tid; i < nc; i += WG) out[nl + i] = LogEntry{cl[2 * i], cl[2 * i + 1], 1u, a.file_tag};
+    } else if (flush) {
         for (int i0 = tid; i0 < NS; i0 += CB * WG) {
             u64 key[CB], cnt[CB], ord[CB];
             bool v[CB];
@@ -855,7 +884,7 @@ __device__ __attribute__((noinline)) void commit_buffers(ScanShared& sh, const S
         }
     }
     const u64* cl = a.cold + 2ull * (u64)blockIdx.x * a.cold_cap;
-    for (u32 i0 = tid; i0 < nc; i0 += CB * WG) {
+    for (u32 i0 = tid; i0 < (logged ? 0u : nc); i0 += CB * WG) {
         u64 key[CB], cnt[CB], ord[CB];
         bool v[CB];
 #pragma unroll
@@ -1139,9 +1168,66 @@ __device__ __forceinline__ u64 walk_chunk(ScanShared& sh, const ScanArgs& a, u32
     const u64 w0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
 #endif
 #if FR_LDS_RAW
-    SegRegs r;  // tile t's segment, loaded during tile t-1 (the chunk's first tile here)
-    if (tb < te) seg_prefetch_next(a, tb, r, tid);
-#elif FR_PREFETCH
+    // Each lane's segment of tile t arrives in registers FR_PF_DEPTH tiles ahead: its loads are
+    // issued while tile t-FR_PF_DEPTH is parsed, so a wave keeps that many tiles of HBM reads in
+    // flight through its barriers and its parse.  After B1 the segment goes to the tile's LDS copy
+    // (the parse reads code bytes there) and the registers take the loads of tile t+FR_PF_DEPTH.
+    auto step = [&](u32 t, SegRegs& r) {
+#if FR_TIMING
+        const u64 c0 = __builtin_amdgcn_s_memtime();
+#endif
+        const SegClass sc = seg_classify(a, t, r, tid);
+#if FR_TIMING
+        __builtin_amdgcn_s_waitcnt(0);
+        const u64 c1 = __builtin_amdgcn_s_memtime();
+#endif
+        if (sc.hi) rare_push(sh, a, (u32)((u64)t * TSTEP) + tid * SEG, 4u,
+                             min((u32)min((u64)TSTEP, a.len - (u64)t * TSTEP) - tid * SEG, (u32)SEG), 0u);
+        lds_barrier();  // B1: the previous tile's parse is done with the bitmaps and the LDS copy
+        const u32 tail = sh.rq_tail;
+        if (tail != done) {  // uniform: nothing is pushed between B1 and B2
+            drain_rare(sh, a, done, tail, tid);
+            done = tail;
+        }
+        seg_store(sh, sc, tid, lane, wid);
+        {
+            typedef u32 u32x4 __attribute__((ext_vector_type(4)));
+            __attribute__((address_space(3))) u32x4* dst =
+                (__attribute__((address_space(3))) u32x4*)(&sh.raw[0]) + tid * (SEG / 16);
+#pragma unroll
+            for (int k = 0; k < SEG / 16; ++k) {
+                u32x4 v;
+                v.x = r.v[k].x; v.y = r.v[k].y; v.z = r.v[k].z; v.w = r.v[k].w;
+                dst[k] = v;
+            }
+            if (t + FR_PF_DEPTH < te) seg_prefetch_next(a, t + FR_PF_DEPTH, r, tid);
+        }
+        lds_barrier();  // B2
+#if FR_TIMING
+        const u64 c2 = __builtin_amdgcn_s_memtime();
+#endif
+        const TileCount tc = seg_count(sh, sc, wid);
+        if (parse && !uniform_flag(sh.spec_bad) && !(a.ablate & 1u))
+            parse_own_headers(sh, a, t, tc, L0 + lines, tid, r, false);
+        lines += tc.tot;
+#if FR_TIMING
+        __builtin_amdgcn_s_waitcnt(0);
+        const u64 c3 = __builtin_amdgcn_s_memtime();
+        tm0 += c1 - c0;  // load + classify
+        tm1 += c2 - c1;  // B1 + drain + store + B2
+        tm2 += c3 - c2;  // parse
+        tm3 += 1;
+#endif
+    };
+    SegRegs rA, rB;
+    if (tb < te) seg_prefetch_next(a, tb, rA, tid);
+    if (FR_PF_DEPTH == 2 && tb + 1 < te) seg_prefetch_next(a, tb + 1, rB, tid);
+    for (u32 t = tb; t < te; t += FR_PF_DEPTH) {
+        step(t, rA);
+        if (FR_PF_DEPTH == 2 && t + 1 < te) step(t + 1, rB);
+    }
+#else
+#if FR_PREFETCH
     // the next tile's segment is loaded during this tile's parse (parse_own_headers), so its HBM
     // latency overlaps the parse; a tile reaching the data end is loaded bytewise instead
     SegRegs r;
@@ -1151,8 +1237,7 @@ __device__ __forceinline__ u64 walk_chunk(ScanShared& sh, const ScanArgs& a, u32
 #if FR_TIMING
         const u64 c0 = __builtin_amdgcn_s_memtime();
 #endif
-#if FR_LDS_RAW
-#elif FR_PREFETCH
+#if FR_PREFETCH
         if (!seg_in_range(a, t)) r = seg_load_tail(a, t, tid);
 #else
         SegRegs r;
@@ -1172,20 +1257,6 @@ __device__ __forceinline__ u64 walk_chunk(ScanShared& sh, const ScanArgs& a, u32
             done = tail;
         }
         seg_store(sh, sc, tid, lane, wid);
-#if FR_LDS_RAW
-        {  // this tile's bytes for the parse, then the next tile's loads (in flight through the parse)
-            typedef u32 u32x4 __attribute__((ext_vector_type(4)));
-            __attribute__((address_space(3))) u32x4* dst =
-                (__attribute__((address_space(3))) u32x4*)(&sh.raw[0]) + tid * (SEG / 16);
-#pragma unroll
-            for (int k = 0; k < SEG / 16; ++k) {
-                u32x4 v;
-                v.x = r.v[k].x; v.y = r.v[k].y; v.z = r.v[k].z; v.w = r.v[k].w;
-                dst[k] = v;
-            }
-            if (t + 1 < te) seg_prefetch_next(a, t + 1, r, tid);
-        }
-#endif
         lds_barrier();  // B2
 #if FR_TIMING
         const u64 c2 = __builtin_amdgcn_s_memtime();
@@ -1206,6 +1277,7 @@ __device__ __forceinline__ u64 walk_chunk(ScanShared& sh, const ScanArgs& a, u32
         tm3 += 1;
 #endif
     }
+#endif
 #if FR_TIMING
     if ((tid & 63) == 0) {  // diagnostic build only: per-phase shader cycles summed over waves
         atomicAdd((unsigned long long*)&a.st->stamp[0], (unsigned long long)tm0);
@@ -1481,6 +1553,160 @@ hipError_t launch_rehash(Table dst, DevState* st, const GSlot* src, u64 nsrc, hi
     const int grid = (int)std::min<u64>((nsrc + 255) / 256, 8192);
     hipLaunchKernelGGL(rehash_kernel, dim3(grid), dim3(256), 0, s, dst, src, nsrc);
     return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------
+// launch-log aggregation: the tally kernel's commits append (code, count, first, tag) pairs to the
+// log instead of inserting each into the HBM table (one dependent slot load plus memory-side
+// atomics per pair).  After the launch the log is bucketed by key hash (histogram per slice of the
+// log, one exclusive scan, scatter), each bucket's pairs are aggregated in LDS by one workgroup,
+// and only the distinct codes reach the HBM table -- batched, with every slot load in flight at
+// once and nothing else competing for the memory system.
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ u32 log_bucket(u64 key) { return (u32)(mix64(key) >> (64 - AGG_LOG_NB)); }
+
+__device__ __forceinline__ void log_slice(u64 n, u32 s, u64& lo, u64& hi) {
+    const u64 per = (n + AGG_SLICES - 1) / AGG_SLICES;
+    lo = min(n, (u64)s * per);
+    hi = min(n, lo + per);
+}
+
+__global__ __launch_bounds__(256) void log_hist_kernel(const LogEntry* log, const DevState* st, u64 cap, u32* hist) {
+    __shared__ u32 h[AGG_NB];
+    for (int i = threadIdx.x; i < AGG_NB; i += 256) h[i] = 0;
+    __syncthreads();
+    const u64 n = min(st->log_n, cap);
+    u64 lo, hi;
+    log_slice(n, blockIdx.x, lo, hi);
+    for (u64 i = lo + threadIdx.x; i < hi; i += 256) {
+        const u64 k = log[i].key;
+        if (k) atomicAdd(&h[log_bucket(k)], 1u);
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < AGG_NB; b += 256) hist[(u64)b * AGG_SLICES + blockIdx.x] = h[b];
+}
+
+__global__ __launch_bounds__(256) void log_scatter_kernel(const LogEntry* log, const DevState* st, u64 cap,
+                                                          const u32* offs, LogEntry* sorted) {
+    __shared__ u32 o[AGG_NB];
+    for (int b = threadIdx.x; b < AGG_NB; b += 256) o[b] = offs[(u64)b * AGG_SLICES + blockIdx.x];
+    __syncthreads();
+    const u64 n = min(st->log_n, cap);
+    u64 lo, hi;
+    log_slice(n, blockIdx.x, lo, hi);
+    for (u64 i = lo + threadIdx.x; i < hi; i += 256) {
+        const LogEntry e = log[i];
+        if (e.key) sorted[atomicAdd(&o[log_bucket(e.key)], 1u)] = e;
+    }
+}
+
+constexpr int AGG_LNS = 2048;  // LDS slots of one bucket's aggregation
+constexpr int AGG_PROBE = 64;
+struct AggSlot {
+    u64 key, first;
+    u32 cnt, tag;
+};
+
+// up to B distinct codes into the HBM table with their slot loads in flight together
+template <int B>
+__device__ __forceinline__ u32 insert_batch(const Table& T, DevState* st, const u64 (&key)[B], const u64 (&cnt)[B],
+                                            const u64 (&ord)[B], const u32 (&tag)[B], const bool (&valid)[B]) {
+    uint4 w0[B], w1[B];
+    u64 h[B];
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+        h[b] = mix64(key[b]) & T.mask;
+        if (valid[b]) {
+            const GSlot* sl = &T.slots[h[b]];
+            w0[b] = *(const uint4*)sl;
+            w1[b] = *((const uint4*)sl + 1);
+        }
+    }
+    u32 made = 0;
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+        if (!valid[b]) continue;
+        const u64 k = ((u64)w0[b].y << 32) | w0[b].x;
+        if (k == key[b]) {
+            GSlot* sl = &T.slots[h[b]];
+            atomicAdd((unsigned long long*)&sl->count, (unsigned long long)cnt[b]);
+            const u64 first = ((u64)w1[b].y << 32) | w1[b].x;
+            if (ord[b] < first) atomicMin((unsigned long long*)&sl->first, (unsigned long long)ord[b]);
+            if (w1[b].z < tag[b]) atomicMax(&sl->last_tag, tag[b]);
+        } else {
+            made += global_insert(T, st, key[b], cnt[b], ord[b], tag[b]) ? 1u : 0u;
+        }
+    }
+    return made;
+}
+
+__global__ __launch_bounds__(256) void log_reduce_kernel(Table t, DevState* st, const LogEntry* sorted,
+                                                         const u32* hist, const u32* offs) {
+    __shared__ AggSlot ls[AGG_LNS];
+    for (int i = threadIdx.x; i < AGG_LNS; i += 256) ls[i] = AggSlot{0, ~0ull, 0, 0};
+    __syncthreads();
+    const u64 last = (u64)blockIdx.x * AGG_SLICES + AGG_SLICES - 1;
+    const u64 lo = offs[(u64)blockIdx.x * AGG_SLICES], hi = (u64)offs[last] + hist[last];
+    u32 made = 0;
+    for (u64 i = lo + threadIdx.x; i < hi; i += 256) {
+        const LogEntry e = sorted[i];
+        u32 h = (u32)mix64(e.key) & (AGG_LNS - 1);
+        bool done = false;
+        for (int pr = 0; pr < AGG_PROBE && !done; ++pr) {
+            u64 k = ls[h].key;
+            if (k == 0) {
+                const u64 old = atomicCAS((unsigned long long*)&ls[h].key, 0ull, (unsigned long long)e.key);
+                k = old == 0 ? e.key : old;
+            }
+            if (k == e.key) {
+                atomicAdd(&ls[h].cnt, e.cnt);
+                atomicMin((unsigned long long*)&ls[h].first, (unsigned long long)e.ord);
+                atomicMax(&ls[h].tag, e.tag);
+                done = true;
+            }
+            h = (h + 1) & (AGG_LNS - 1);
+        }
+        if (!done) made += global_insert(t, st, e.key, e.cnt, e.ord, e.tag) ? 1u : 0u;  // a full bucket table
+    }
+    __syncthreads();
+    for (int i0 = threadIdx.x; i0 < AGG_LNS; i0 += 4 * 256) {
+        u64 key[4], cnt[4], ord[4];
+        u32 tag[4];
+        bool v[4];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int i = i0 + b * 256;
+            const AggSlot e = i < AGG_LNS ? ls[i] : AggSlot{0, 0, 0, 0};
+            v[b] = e.key != 0;
+            key[b] = e.key;
+            cnt[b] = e.cnt;
+            ord[b] = e.first;
+            tag[b] = e.tag;
+        }
+        made += insert_batch<4>(t, st, key, cnt, ord, tag, v);
+    }
+    add_created(st, made);
+}
+
+size_t log_aggregate_temp_bytes() {
+    size_t tb = 0;
+    (void)rocprim::exclusive_scan(nullptr, tb, (const u32*)nullptr, (u32*)nullptr, 0u,
+                                  (size_t)AGG_NB * AGG_SLICES, rocprim::plus<u32>(), (hipStream_t)0);
+    return tb;
+}
+
+hipError_t launch_log_aggregate(Table t, DevState* st, LogEntry* log, LogEntry* sorted, u64 cap, u32* hist,
+                                void* temp, size_t temp_bytes, hipStream_t s) {
+    u32* offs = hist + (size_t)AGG_NB * AGG_SLICES;
+    hipLaunchKernelGGL(log_hist_kernel, dim3(AGG_SLICES), dim3(256), 0, s, log, st, cap, hist);
+    hipError_t e = rocprim::exclusive_scan(temp, temp_bytes, hist, offs, 0u, (size_t)AGG_NB * AGG_SLICES,
+                                           rocprim::plus<u32>(), s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(log_scatter_kernel, dim3(AGG_SLICES), dim3(256), 0, s, log, st, cap, offs, sorted);
+    hipLaunchKernelGGL(log_reduce_kernel, dim3(AGG_NB), dim3(256), 0, s, t, st, sorted, hist, offs);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return hipMemsetAsync(&st->log_n, 0, sizeof(u64), s);
 }
 
 // Stream compaction of table slots with one atomic per workgroup (single-address atomics

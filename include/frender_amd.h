@@ -62,6 +62,7 @@ typedef struct fr_timing {
     double last_scan_ms;     /* duration of the most recent launch */
     double classify_ms;      /* last classify pass */
     double finalize_ms;      /* last compaction + ordering */
+    double log_ms;           /* summed duration of the launch-log aggregations after those launches */
 } fr_timing;
 
 /* ---- lifecycle ------------------------------------------------------------------ */

@@ -25,6 +25,7 @@ LIB_PATH = os.environ.get("FRENDER_HIP_LIB", os.path.join(HERE, "libfrender_hip.
 
 FR_OK = 0
 FR_SAMPLE_DONE = 5
+FR_ERR_IO = 6
 FR_SCAN_OK, FR_SCAN_NO_SPACE, FR_SCAN_UTF8 = 0, 1, 2
 CLASS_NAMES = ("undetermined", "index_hop", "demuxable", "ambiguous")
 
@@ -81,6 +82,11 @@ _SIGS = {
     "fr_copy_to_device": (C.c_int, [P, P, P, C.c_uint64]),
     "fr_synth_device": (C.c_int, [P, P, C.c_uint64, C.c_uint64, C.c_int, C.c_uint64, C.c_char_p, C.c_char_p,
                                   C.c_int, C.c_int, C.c_int]),
+    # native inflate (row f-2)
+    "fr_gz_open": (P, [C.POINTER(C.c_char_p), C.c_int, C.c_int]),
+    "fr_gz_feed": (C.c_int, [P, C.c_int, P]),
+    "fr_gz_error": (C.c_char_p, [P]),
+    "fr_gz_close": (None, [P]),
     # demux (row f-1)
     "fr_dmx_create": (P, [C.c_int]),
     "fr_dmx_destroy": (None, [P]),
@@ -197,6 +203,46 @@ def pack_fast(codes) -> tuple:
             keys[i] = v
             ok[i] = True
     return keys, ok
+
+
+class GzError(FrenderError):
+    """A .gz input the native inflate could not read (the caller replays it with Python's gzip)."""
+
+
+class GzPool:
+    """Native inflate of a scan's .gz files (fr_gz_*): `threads` host threads inflate the listed
+    files in order ahead of the consumer; feed(i, ctx) hands file i's bytes to ctx.feed."""
+
+    def __init__(self, paths, threads: int = 1):
+        self.paths = [str(p) for p in paths]
+        enc = [os.fsencode(p) for p in self.paths]
+        arr = (C.c_char_p * max(len(enc), 1))(*enc)
+        self.h = lib.fr_gz_open(arr, len(enc), max(1, int(threads)))
+        if not self.h:
+            raise FrenderError("fr_gz_open returned NULL")
+
+    def feed(self, i: int, ctx) -> bool:
+        """Feed file i into ctx's open file; True once the -s sample is complete."""
+        return ctx.feed_gz(self, i)
+
+    def _feed(self, i: int, ctx_handle) -> bool:
+        rc = lib.fr_gz_feed(self.h, i, ctx_handle)
+        if rc == FR_ERR_IO:
+            raise GzError(lib.fr_gz_error(self.h).decode(errors="replace"))
+        if rc not in (FR_OK, FR_SAMPLE_DONE):
+            raise FrenderError(f"fr_gz_feed failed ({rc}): {lib.fr_gz_error(self.h).decode(errors='replace')}")
+        return rc == FR_SAMPLE_DONE
+
+    def close(self):
+        if self.h:
+            lib.fr_gz_close(self.h)
+            self.h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class Demux:
@@ -353,6 +399,10 @@ class Context:
             a = np.frombuffer(data, dtype=np.uint8)
             rc = lib.fr_feed(self.h, _ptr(a), a.size)
         return self._ck(rc, "fr_feed") == FR_SAMPLE_DONE
+
+    def feed_gz(self, pool: "GzPool", i: int) -> bool:
+        """Feed file i of a native inflate pool (GzPool); True once the -s sample is complete."""
+        return pool._feed(i, self.h)
 
     def feed_device(self, dev_ptr: int, nbytes: int):
         self._ck(lib.fr_feed_device(self.h, P(dev_ptr), nbytes), "fr_feed_device")

@@ -1,0 +1,248 @@
+// fr_gz.cpp — native inflate for the scan's input.
+//
+// The reference reads each file with gzip.open(file, "rt") (frender.py:159): one Python process
+// per file (its Pool, :189-193).  Here a pool of host threads inflates the scan's .gz files with
+// zlib, up to `threads` files at a time in scan order, into 16 MiB blocks queued per file; the
+// consumer (the scan's host thread) hands each file's blocks to fr_feed in order, which copies them
+// through the pinned ring to HBM while the next blocks inflate.  No GIL, no Python bytes objects.
+//
+// Stream rules follow Python's gzip module (3.10, _GzipReader): members are inflated one after
+// another (multi-member files), NUL padding after a member is skipped, anything else after a
+// member must start a new member, and an empty file is empty.  Any other deviation (bad magic,
+// truncated member, CRC/length mismatch, deflate error) stops that file with FR_ERR_IO: the host
+// then re-reads the file through Python's gzip to raise the reference's own exception.
+#include <zlib.h>
+
+#include <algorithm>
+#include <condition_variable>
+#include <cstdio>
+#include <cstring>
+#include <deque>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/frender_amd.h"
+
+namespace {
+
+struct GzFile {
+    std::string path;
+    std::deque<std::vector<uint8_t>> q;
+    bool done = false;
+    bool cancel = false;
+    std::string err;
+};
+
+}  // namespace
+
+struct fr_gz {
+    std::vector<GzFile> files;
+    int threads = 1;
+    size_t block = 16u << 20;
+    size_t depth = 3;  // blocks queued per file (set by fr_gz_open)
+    std::mutex m;
+    std::condition_variable cv;
+    std::vector<std::thread> workers;
+    std::vector<std::vector<uint8_t>> spare;  // consumed blocks for reuse (no page faults per block)
+    int next = 0;     // next file a worker starts
+    int consume = 0;  // file the consumer reads (workers stay within [consume, consume + threads))
+    bool stop = false;
+    std::string err;
+};
+
+namespace {
+
+// inflate one file into g->files[i].q (blocks of g->block bytes); returns "" or an error text
+std::string inflate_file(fr_gz* g, int i) {
+    GzFile& f = g->files[i];
+    FILE* fp = fopen(f.path.c_str(), "rb");
+    if (!fp) return "cannot open " + f.path;
+    std::vector<uint8_t> in(4u << 20);
+    z_stream zs;
+    std::memset(&zs, 0, sizeof(zs));
+    if (inflateInit2(&zs, 16 + MAX_WBITS) != Z_OK) {
+        fclose(fp);
+        return "inflateInit2 failed";
+    }
+    auto fresh = [&]() {
+        std::lock_guard<std::mutex> lk(g->m);
+        if (g->spare.empty()) return std::vector<uint8_t>(g->block);
+        std::vector<uint8_t> v = std::move(g->spare.back());
+        g->spare.pop_back();
+        v.resize(g->block);
+        return v;
+    };
+    std::vector<uint8_t> out = fresh();
+    size_t have = 0;  // bytes of `out` filled
+    std::string err;
+    bool in_member = false;  // a member has started and not ended
+    bool eof = false;
+    auto push = [&](bool last) -> bool {  // queue `out` (partial only at the end); false: cancelled
+        if (!have && !last) return true;
+        std::unique_lock<std::mutex> lk(g->m);
+        g->cv.wait(lk, [&] { return f.q.size() < g->depth || f.cancel || g->stop; });
+        if (f.cancel || g->stop) return false;
+        if (have) {
+            out.resize(have);
+            f.q.push_back(std::move(out));
+            have = 0;
+            g->cv.notify_all();
+            lk.unlock();
+            if (!last) out = fresh();
+            return true;
+        }
+        g->cv.notify_all();
+        return true;
+    };
+    for (;;) {
+        if (zs.avail_in == 0 && !eof) {
+            const size_t n = fread(in.data(), 1, in.size(), fp);
+            if (n == 0) eof = true;
+            zs.next_in = in.data();
+            zs.avail_in = (uInt)n;
+        }
+        if (!in_member) {  // between members: NUL padding, then a member or the end of the file
+            while (zs.avail_in && *zs.next_in == 0) {
+                ++zs.next_in;
+                --zs.avail_in;
+            }
+            if (zs.avail_in == 0) {
+                if (eof) break;
+                continue;
+            }
+            if (*zs.next_in != 0x1f) {
+                err = "not a gzip member";
+                break;
+            }
+            in_member = true;
+        }
+        if (zs.avail_in == 0 && eof) {
+            err = "compressed file ended before the end-of-stream marker was reached";
+            break;
+        }
+        zs.next_out = out.data() + have;
+        zs.avail_out = (uInt)(out.size() - have);
+        const int rc = inflate(&zs, Z_NO_FLUSH);
+        have = out.size() - zs.avail_out;
+        if (rc == Z_STREAM_END) {
+            in_member = false;
+            if (inflateReset(&zs) != Z_OK) {
+                err = "inflateReset failed";
+                break;
+            }
+        } else if (rc == Z_BUF_ERROR) {
+            if (zs.avail_in == 0 && eof) {
+                err = "compressed file ended before the end-of-stream marker was reached";
+                break;
+            }
+        } else if (rc != Z_OK) {
+            err = std::string("inflate: ") + (zs.msg ? zs.msg : "error");
+            break;
+        }
+        if (have == out.size() && !push(false)) break;
+        {
+            std::lock_guard<std::mutex> lk(g->m);
+            if (f.cancel || g->stop) break;
+        }
+    }
+    inflateEnd(&zs);
+    fclose(fp);
+    if (err.empty()) push(true);
+    return err;
+}
+
+void worker(fr_gz* g) {
+    for (;;) {
+        int i;
+        {
+            std::unique_lock<std::mutex> lk(g->m);
+            g->cv.wait(lk, [&] {
+                return g->stop || (g->next < (int)g->files.size() && g->next < g->consume + g->threads);
+            });
+            if (g->stop) return;
+            i = g->next++;
+        }
+        std::string err = inflate_file(g, i);
+        std::lock_guard<std::mutex> lk(g->m);
+        g->files[i].err = err;
+        g->files[i].done = true;
+        g->cv.notify_all();
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+fr_gz* fr_gz_open(const char* const* paths, int n_files, int threads) {
+    fr_gz* g = new fr_gz();
+    g->files.resize(n_files > 0 ? n_files : 0);
+    for (int i = 0; i < n_files; ++i) g->files[i].path = paths[i];
+    g->threads = threads < 1 ? 1 : threads;
+    // files inflating ahead of the consumer may buffer up to 2 GiB of decoded blocks in all, so a
+    // worker is not parked behind a short queue while the consumer is still on an earlier file
+    g->depth = std::max<size_t>(3, (2ull << 30) / ((size_t)g->threads * g->block));
+    const int nw = std::min(g->threads, std::max(n_files, 1));
+    for (int k = 0; k < nw; ++k) g->workers.emplace_back(worker, g);
+    return g;
+}
+
+const char* fr_gz_error(const fr_gz* g) { return g ? g->err.c_str() : "null inflate pool"; }
+
+int fr_gz_feed(fr_gz* g, int i, fr_ctx* ctx) {
+    if (i < 0 || i >= (int)g->files.size()) {
+        g->err = "fr_gz_feed: no such file";
+        return FR_ERR_INVALID;
+    }
+    GzFile& f = g->files[i];
+    {
+        std::lock_guard<std::mutex> lk(g->m);
+        g->consume = i;
+        g->cv.notify_all();
+    }
+    for (;;) {
+        std::vector<uint8_t> b;
+        {
+            std::unique_lock<std::mutex> lk(g->m);
+            g->cv.wait(lk, [&] { return !f.q.empty() || f.done; });
+            if (f.q.empty()) {  // done
+                if (!f.err.empty()) {
+                    g->err = f.path + ": " + f.err;
+                    return FR_ERR_IO;
+                }
+                return FR_OK;
+            }
+            b = std::move(f.q.front());
+            f.q.pop_front();
+            g->cv.notify_all();
+        }
+        const int rc = fr_feed(ctx, b.data(), b.size());
+        {
+            std::lock_guard<std::mutex> lk(g->m);
+            if (g->spare.size() < (size_t)g->threads * g->depth) g->spare.push_back(std::move(b));
+        }
+        if (rc != FR_OK) {  // the -s sample is complete, or a feed error: this file is finished
+            std::lock_guard<std::mutex> lk(g->m);
+            f.cancel = true;
+            f.q.clear();
+            g->cv.notify_all();
+            if (rc != FR_SAMPLE_DONE) g->err = fr_last_error(ctx);
+            return rc;
+        }
+    }
+}
+
+void fr_gz_close(fr_gz* g) {
+    if (!g) return;
+    {
+        std::lock_guard<std::mutex> lk(g->m);
+        g->stop = true;
+        g->cv.notify_all();
+    }
+    for (auto& t : g->workers) t.join();
+    delete g;
+}
+
+}  // extern "C"

@@ -117,7 +117,9 @@ class _GzReader:
 
 
 def _replay_decode_error(path, sample):
-    """Error path only, after the GPU flagged invalid UTF-8 in a file.  The reference's exception
+    """Error path only, after the GPU flagged invalid UTF-8 in a file (or the native inflate
+    rejected it: truncated or corrupt gzip, whose EOFError / BadGzipFile / zlib.error the same
+    re-read raises).  The reference's exception
     text (byte, position, reason) is relative to the chunk its text-mode reader handed the decoder
     (frender.py:159: gzip.open(..., "rt"), whose chunk boundaries depend on the compressed
     stream), and with -s it raises only if the bad bytes lie in a chunk read before the sample
@@ -146,39 +148,33 @@ def _file_done(st, path=None, sample=None):
 
 
 def scan_files(ctx, files, indices, sample, cores, on_file=None, after_file=None):
-    """scan_file (frender.py:154-181) for files[i], i in `indices` (increasing), into ctx's table:
-    up to `cores` files inflate ahead in helper threads while the GPU tallies them in order (the
-    reference's Pool over files, :189-193).  Every file is opened at its global index, so any
-    subset of a scan's files, on any GPU, yields the single-GPU ordinals.  on_file(i, name)
-    runs before a file is read (the reference's "Tallying barcodes from ..." line), after_file(i,
-    records, new barcodes) once it is tallied.  Returns {i: (records, new barcodes)}."""
+    """scan_file (frender.py:154-181) for files[i], i in `indices` (increasing), into ctx's table.
+    The bytes come from the library's native inflate (fr_gz_*): up to `cores` files inflate ahead
+    in host threads while the GPU tallies them in order (the reference's Pool over files,
+    :189-193).  Every file is opened at its global index, so any subset of a scan's files, on any
+    GPU, yields the single-GPU ordinals.  on_file(i, name) runs before a file is read (the
+    reference's "Tallying barcodes from ..." line), after_file(i, records, new barcodes) once it is
+    tallied.  Returns {i: (records, new barcodes)}."""
     out = {}
-    ahead = max(1, int(cores))
-    readers: dict = {}
+    pool = _lib.GzPool([files[i] for i in indices], threads=max(1, int(cores)))
     try:
         for k, fi in enumerate(indices):
-            for j in indices[k:k + ahead]:
-                if j not in readers:
-                    readers[j] = _GzReader(files[j])
             path = files[fi]
             if on_file:
                 on_file(fi, str(os.path.basename(path)))
             ctx.begin_file(sample, file_index=fi)
-            rd = readers.pop(fi)
             try:
-                for chunk in rd:
-                    if ctx.feed(chunk):
-                        break
-            finally:
-                rd.close()
+                pool.feed(k, ctx)
+            except _lib.GzError as e:  # not a valid gzip stream: the reference's reader fails on it
+                _replay_decode_error(path, sample)
+                raise RuntimeError(f"native inflate rejected {path} but Python's gzip reads it: {e}") from e
             st = ctx.end_file()
             _file_done(st, path, sample)
             out[fi] = (int(st.records), int(st.new_keys))
             if after_file:
                 after_file(fi, *out[fi])
     finally:
-        for rd in readers.values():
-            rd.close()
+        pool.close()
     return out
 
 

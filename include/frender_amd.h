@@ -30,6 +30,7 @@ extern "C" {
 #define FR_ERR_HIP 2       /* HIP runtime error */
 #define FR_ERR_CAPACITY 3  /* a device table or pool is full */
 #define FR_ERR_DEVICE 4    /* a kernel reported an internal failure (look-back spin bound) */
+#define FR_ERR_IO 6        /* a .gz input could not be inflated (fr_gz_feed; message in fr_gz_error) */
 
 /* scan-time data errors: reported in fr_file_stats.error, mirroring the reference's crash */
 #define FR_SCAN_OK 0
@@ -111,6 +112,19 @@ int fr_begin_file_at(fr_ctx* ctx, int64_t file_index, uint64_t byte_base, int64_
  * launches.  Returns FR_OK, or 5 (FR_SAMPLE_DONE) once -s records were seen. */
 #define FR_SAMPLE_DONE 5
 int fr_feed(fr_ctx* ctx, const uint8_t* data, uint64_t len);
+/* ---- native inflate: replaces gzip.open(file, "rt") (frender.py:159) as
+ * the source of the decoded bytes.  fr_gz_open starts `threads` host threads that inflate the
+ * listed .gz files (zlib; multi-member, NUL padding between members as Python's gzip) up to
+ * `threads` files ahead of the consumer, in list order, into 16 MiB blocks.  fr_gz_feed hands
+ * file i's blocks to fr_feed (call it between fr_begin_file[_at] and fr_end_file; files in list
+ * order) and returns FR_OK, FR_SAMPLE_DONE, or FR_ERR_IO when the stream is not valid gzip (the
+ * caller re-reads the file with Python's gzip to raise the reference's exception). */
+typedef struct fr_gz fr_gz;
+fr_gz* fr_gz_open(const char* const* paths, int n_files, int threads);
+int fr_gz_feed(fr_gz* g, int i, fr_ctx* ctx);
+const char* fr_gz_error(const fr_gz* g);
+void fr_gz_close(fr_gz* g);
+
 /* The whole current file is already resident in HBM (bench / device producers). */
 int fr_feed_device(fr_ctx* ctx, const uint8_t* dev_data, uint64_t len);
 int fr_end_file(fr_ctx* ctx, fr_file_stats* out);

@@ -56,7 +56,7 @@ def host_feed(n, R=8, piece=64 << 20):
             "M_reads_per_s": round(n / dt / 1e6, 1), "GB_per_s": round(n * reclen / dt / 1e9, 2)}
 
 
-def gz_scan(n, files=4):
+def gz_scan(n, files=4, cores=None):
     sheet = synth.make_sheet(96, 8, 8)
     with tempfile.TemporaryDirectory() as d:
         paths = synth.make_dataset(d, sheet, n, n_files=files, R=8, seed=1, level=1)
@@ -65,7 +65,8 @@ def gz_scan(n, files=4):
             f.write("Sample_ID,index,index2\n")
             for name, a, b in zip(sheet.ids, sheet.idx1, sheet.idx2):
                 f.write(f"{name},{a},{b}\n")
-        args = types.SimpleNamespace(files=paths, b=sheet_csv, n=1, c=files, s=None, rc=False, o=None, p=None)
+        cores = cores or files
+        args = types.SimpleNamespace(files=paths, b=sheet_csv, n=1, c=cores, s=None, rc=False, o=None, p=None)
         cwd = os.getcwd()
         os.chdir(d)
         try:
@@ -74,7 +75,7 @@ def gz_scan(n, files=4):
             dt = time.perf_counter() - t0
         finally:
             os.chdir(cwd)
-    return {"path": "gz_scan", "reads": n, "files": files, "s": round(dt, 3),
+    return {"path": "gz_scan", "reads": n, "files": files, "inflate_threads": cores, "s": round(dt, 3),
             "M_reads_per_s": round(n / dt / 1e6, 3)}
 
 
@@ -134,6 +135,8 @@ if __name__ == "__main__":
         print(json.dumps(host_feed(n)), flush=True)
     if gzn:
         print(json.dumps(gz_scan(gzn)), flush=True)
+        print(json.dumps(gz_scan(2 * gzn, files=8)), flush=True)
+        print(json.dumps(gz_scan(gzn, files=16)), flush=True)
     dmn = int(sys.argv[3]) if len(sys.argv) > 3 else 2_000_000
     if dmn:
         for lvl in (9, 1):

@@ -44,6 +44,11 @@ class FakeContext:
         self.buf += bytes(data)
         return False
 
+    def feed_gz(self, pool, i) -> bool:
+        import gzip
+        with gzip.open(pool.paths[i], "rb") as g:
+            return self.feed(g.read())
+
     def end_file(self):
         data = bytes(self.buf)
         st = types.SimpleNamespace(records=0, new_keys=0, exotic=0, error=0, utf8_bad=0, lines=0)

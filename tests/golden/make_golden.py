@@ -65,7 +65,15 @@ def hdr(code: str, i: int = 0, comment_prefix: str = "1:N:0:") -> str:
     return f"@M1:1:FC:1:1101:{1000 + i}:{2000 + i} {comment_prefix}{code}"
 
 
+class RawGz(bytes):
+    """A .gz input given as its exact file bytes (corrupt / truncated / padded streams)."""
+
+
 def write_gz(path: str, text_or_bytes, members: int = 1) -> None:
+    if isinstance(text_or_bytes, RawGz):
+        with open(path, "wb") as f:
+            f.write(bytes(text_or_bytes))
+        return
     data = text_or_bytes.encode() if isinstance(text_or_bytes, str) else text_or_bytes
     synth.write_fastq_gz(path, data, level=6, members=members)
 
@@ -260,6 +268,18 @@ def all_cases():
         hand_case("bad_utf8_in_sample_chunk", {"a_R1.fq.gz": "".join(rec(hdr(c, i)) for i, c in enumerate(mix[:40])).encode() +
                                                b"@M1:x 1:N:0:AAAACCCC+GGGGTTTT\xe2\x82\nAC\n+\nFF\n" + lines.encode()},
                   {"s": 30}),
+        # gzip stream edge cases (native inflate): the reference's gzip reader decides
+        hand_case("gz_truncated", {"a_R1.fq.gz": RawGz(gzip.compress(lines.encode(), 6)[:-900])}, {}),
+        hand_case("gz_corrupt", {"a_R1.fq.gz": RawGz(gzip.compress(lines.encode(), 6)[:300] + b"\xff" * 64 +
+                                                     gzip.compress(lines.encode(), 6)[364:])}, {}),
+        hand_case("gz_nul_padding", {"a_R1.fq.gz": RawGz(gzip.compress(lines.encode()[:9000], 6) + b"\0" * 4096 +
+                                                         gzip.compress(lines.encode()[9000:], 1) + b"\0" * 7)}, {}),
+        hand_case("gz_trailing_garbage", {"a_R1.fq.gz": RawGz(gzip.compress(lines.encode(), 6) + b"garbage")}, {}),
+        hand_case("gz_not_gzip", {"a_R1.fq.gz": RawGz(lines.encode()[:5000])}, {}),
+        hand_case("gz_empty_file", {"a_R1.fq.gz": RawGz(b""), "b_R1.fq.gz": lines},
+                  {"files": ["a_R1.fq.gz", "b_R1.fq.gz"]}),
+        hand_case("gz_bad_crc", {"a_R1.fq.gz": RawGz(gzip.compress(lines.encode(), 6)[:-8] + b"\0\0\0\0" +
+                                                     gzip.compress(lines.encode(), 6)[-4:])}, {}),
         hand_case("wide_codes_12", {"a_R1.fq.gz": "".join(rec(hdr(c, i)) for i, c in enumerate(
             ["AAAACCCCGGGG+TTTTAAAACCCC", "AAAACCCCGGGG+TTTTAAAACCCN", "aaaaccccgggg+ttttaaaacccc", "AAAACCCCGGGG+TTTTAAAACCCC",
              "CCCCGGGGTTTT+AAAACCCCGGGG", "ACGTACGTACGT+ACGTACGTACGT", "AAAACCCCGGGa+TTTTAAAACCCC", "NNNNNNNNNNNN+NNNNNNNNNNNN",

@@ -46,7 +46,7 @@ def parse():
     ap.add_argument("--nsubs", type=int, default=1)
     ap.add_argument("--rc", action="store_true")
     ap.add_argument("--combinatorial", action="store_true", help="12x8 combinatorial sheet (config 4 shape)")
-    ap.add_argument("--cpu-reads", type=int, default=40_000_000, help="bounded sample for the CPU baseline (~15-20 s on 8 cores)")
+    ap.add_argument("--cpu-reads", type=int, default=12_000_000, help="bounded sample for the CPU baseline (~10-25 s on 8 cores)")
     ap.add_argument("--cpu-cores", type=int, default=8)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--merge", choices=["a2a", "tree"], default="a2a",
@@ -88,12 +88,24 @@ def table_checksum(ctx, U):
     return int(h.sum().item())
 
 
+def _gz(chunk: bytes) -> bytes:
+    import gzip
+
+    return gzip.compress(chunk, compresslevel=1)
+
+
 def cpu_baseline(args, ctx, sheet, reclen):
-    """Oracle CPU port (tally + classify, same algorithm as the reference) on a bounded
-    sample of the same workload (the first --cpu-reads SYN-v1 records, generated by the device
-    generator, which the tests pin byte-identical to the host one), from decoded text in
-    memory, `cores` worker processes over `cores` shards as the reference parallelises over
-    files (frender.py:189-193)."""
+    """The reference's CPU path, as restated by the oracle port (oracle.frender_oracle.scan: a
+    Pool of `cores` workers over the input files, gzip text reader, tally, classify, CSV, exactly
+    the reference's frender_scan structure, frender.py:189-193, :606-630), timed on this box's host
+    cores over a bounded sample of the same workload: the first --cpu-reads SYN-v1 records
+    (generated by the device generator, which the tests pin byte-identical to the host one) split
+    into `cores` .fastq.gz files.  profiles/cpu_ref_vs_port.json (scripts/cpu_ref_vs_port.py, run
+    where the reference is importable) calibrates this port against the reference itself."""
+    import argparse
+    import contextlib
+    import io
+    import tempfile
     from multiprocessing import Pool
 
     from oracle import frender_oracle as O
@@ -105,22 +117,44 @@ def cpu_baseline(args, ctx, sheet, reclen):
     data = ctx.copy_to_host(dev, n * reclen)
     ctx.device_free(dev)
     cuts = [n * i // cores for i in range(cores + 1)]
-    shards = [data[cuts[i] * reclen:cuts[i + 1] * reclen].decode() for i in range(cores)]
-    del data
-    t0 = time.perf_counter()
-    with Pool(cores) as pool:
-        per = pool.starmap(O.tally_text, [(s, None) for s in shards])
-        total = {}
-        for counts, _ in per:
-            for k, v in counts.items():
-                total[k] = total.get(k, 0) + v
-        items = [(c, r, sheet.idx1, sheet.idx2, sheet.ids, args.nsubs, args.rc) for c, r in total.items()]
-        pool.starmap(O.classify_code, items, chunksize=max(1, len(items) // (4 * cores)))
-    dt = time.perf_counter() - t0
+    with tempfile.TemporaryDirectory() as d:
+        sheet.write_csv(os.path.join(d, "sheet.csv"))
+        with Pool(cores) as pool:
+            blobs = pool.map(_gz, [data[cuts[i] * reclen:cuts[i + 1] * reclen] for i in range(cores)])
+        del data
+        files = []
+        for i, blob in enumerate(blobs):
+            files.append(os.path.join(d, f"syn_L{i + 1:03d}_R1_001.fastq.gz"))
+            with open(files[-1], "wb") as f:
+                f.write(blob)
+        del blobs
+        out = os.path.join(d, "out")
+        os.mkdir(out)
+        ns = argparse.Namespace(n=args.nsubs, rc=args.rc, c=float(cores), s=None, o="cpu", p=None,
+                                b=os.path.join(d, "sheet.csv"), files=files)
+        cwd = os.getcwd()
+        os.chdir(out)
+        try:
+            with contextlib.redirect_stdout(io.StringIO()):
+                t0 = time.perf_counter()
+                O.scan(ns)
+                dt = time.perf_counter() - t0
+        finally:
+            os.chdir(cwd)
+    cal = ""
+    try:
+        with open(os.path.join(ROOT, "profiles", "cpu_ref_vs_port.json")) as f:
+            c = json.load(f)
+        cal = (f"; calibration (scripts/cpu_ref_vs_port.py, build container, {c['cores']} cores, {c['reads']} reads): "
+               f"reference {c['reference_scan_M_reads_per_s']} vs port {c['port_scan_M_reads_per_s']} M reads/s "
+               f"(port/reference time ratio {c['port_scan_over_reference']}, outputs identical: {c['outputs_identical']})")
+    except (OSError, KeyError, ValueError):
+        pass
     return {"value": round(n / dt / 1e6, 4), "unit": "M reads/s", "cores": cores, "kind": "port",
-            "sample": f"first {n} SYN-v1 reads of the workload ({args.samples} samples, {args.index_len}+"
-                      f"{args.index_len}bp, n={args.nsubs}, R={args.read_len}) decoded in memory, {cores} shards; "
-                      f"oracle tally + classify of {len(total)} uniques took {dt:.2f} s"}
+            "sample": f"the reference's scan command restated (oracle.frender_oracle.scan: Pool over files, gzip, "
+                      f"tally, classify, CSV) on the first {n} SYN-v1 reads of the workload ({args.samples} samples, "
+                      f"{args.index_len}+{args.index_len}bp, n={args.nsubs}, R={args.read_len}) as {cores} .fastq.gz "
+                      f"files (level 1), {cores} workers: {dt:.2f} s{cal}"}
 
 
 def main():

@@ -529,7 +529,7 @@ class Context:
         if v[8:16].any():  # FR_TIMING build / FR_ABLATE=64: per-phase cycles or commit counts
             names = (("lookback", "barrier", "headers", "parse", "stage", "count", "flush", "prologue")
                      if os.environ.get("FR_KERNEL") == "0" else
-                     ("collect", "parse", "stage", "count", "first_tile", "infer", "lookback", "commit"))
+                     ("classify", "barriers", "parse", "tiles", "walk", "kernel", "guess", "commit"))
             d["stamps"] = dict(zip(names, v[8:].tolist()))
         return d
 

@@ -19,7 +19,10 @@ constexpr int SEG = TILE / WG;       // 64 contiguous bytes per thread
 constexpr int TSTEP = TILE - SEG;    // tile stride: tiles overlap by one segment, so the bitmaps
                                      // of a tile's last own segment always have a successor
 constexpr int HALO = 0;              // bytes staged past the tile (lines past it are read from HBM)
-constexpr int LOG_NS = 10;
+#ifndef FR_LOG_NS
+#define FR_LOG_NS 10
+#endif
+constexpr int LOG_NS = FR_LOG_NS;
 constexpr int NS = 1 << LOG_NS;      // LDS hash slots per workgroup
 #ifndef FR_LPROBE
 #define FR_LPROBE 4

@@ -35,6 +35,9 @@ namespace fr {
 #ifndef FR_PF_DEPTH
 #define FR_PF_DEPTH 1  // FR_LDS_RAW: tiles of segment loads each wave keeps in flight (1 or 2 register sets)
 #endif
+#ifndef FR_PARSE2
+#define FR_PARSE2 1  // FR_LDS_RAW: header parse v2 (two 64-bit bitmap windows, wave-uniform code length encode)
+#endif
 #ifndef FR_SEG_AUX
 #define FR_SEG_AUX 0  // cache policy bits of the segment stream loads (2 = nt)
 #endif
@@ -180,7 +183,7 @@ struct ScanShared {
     u32 raw[TILE / 4];  // the current tile's bytes (stored after B1, read by the parse after B2)
 #endif
     LSlot ls[NS];     // LDS hash table of this workgroup's chunk
-    u32 wsum[WG / 64];
+    alignas(16) u32 wsum[WG / 64];
     u64 tile_excl;
     u32 tile;
     u32 next;
@@ -201,7 +204,7 @@ struct ScanShared {
     u32 chunk;
     int phase;        // guessed line phase (lines before the chunk, mod 4), -1 unsure
     u32 exo_p[EXO_BUF], exo_start[EXO_BUF], exo_len[EXO_BUF];
-    u64 bsp[WG + 1];  // per 64-B segment of the staged tile: ' ' bitmap (phase inference: the
+    u64 bsp[WG + 1];  // per 64-B segment of the staged tile: ' ' | line-end bitmap (phase inference: the
                       // line-terminator bitmap of a chunk's first tile)
     u64 bcol[WG + 1]; //                                      ':' bitmap
     u64 beol[WG + 1]; //                                      '\r' | '\n' bitmap
@@ -672,7 +675,7 @@ __device__ __forceinline__ SegClass seg_classify(const ScanArgs& a, u32 t, const
 
 // after B1: the segment's bitmaps into LDS, the wave's terminator count
 __device__ __forceinline__ void seg_store(ScanShared& sh, const SegClass& sc, int tid, int lane, int wid) {
-    sh.bsp[tid] = sc.sp;
+    sh.bsp[tid] = sc.sp | sc.eol;  // token ends: ' ' or line end
     sh.bcol[tid] = sc.col;
     sh.beol[tid] = sc.eol;
     if (lane == 0) sh.wsum[wid] = sc.wtot;
@@ -814,12 +817,112 @@ __device__ __forceinline__ u32 insert_many(const ScanArgs& a, const u64 (&key)[B
         const u64 k = ((u64)w0[b].y << 32) | w0[b].x;
         if (k == key[b]) {  // the common case: the code is already in the table
             GSlot* sl = &T.slots[h[b]];
+            if (a.ablate & 128u) {  // timing ablation: plain stores instead of atomics (wrong counts)
+                sl->count = cnt[b];
+                continue;
+            }
             atomicAdd((unsigned long long*)&sl->count, (unsigned long long)cnt[b]);
             const u64 first = ((u64)w1[b].y << 32) | w1[b].x;
             if (ord[b] < first) atomicMin((unsigned long long*)&sl->first, (unsigned long long)ord[b]);
             if (w1[b].z < a.file_tag) atomicMax(&sl->last_tag, a.file_tag);
         } else {
             made += global_insert(T, a.st, key[b], cnt[b], ord[b], a.file_tag) ? 1u : 0u;
+        }
+    }
+    return made;
+}
+
+// Insert B (key, count, min ordinal) entries into the HBM table in rounds: each round loads the
+// current probe slot of every pending entry together, then settles hits with fire-and-forget atomics
+// and claims empty slots with CASes issued together, so a lane waits for max-probe-depth round trips,
+// not for the sum over its entries (insert_many + global_insert walk each miss serially).
+#ifndef FR_COMMIT2
+#define FR_COMMIT2 0
+#endif
+#ifndef FR_CB2
+#define FR_CB2 4
+#endif
+constexpr int CB2 = FR_CB2;
+template <int B>
+__device__ __forceinline__ u32 insert_rounds(const ScanArgs& a, const u64 (&key)[B], const u32 (&cnt)[B],
+                                             const u64 (&ord)[B], const bool (&valid)[B]) {
+    const Table& T = *a.tab;
+    const u64 mask = T.mask;
+    GSlot* const slots = T.slots;
+    u32 h[B];  // slot index (tables stay below 2^32 slots)
+    bool pend[B];
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+        h[b] = (u32)(mix64(key[b]) & mask);
+        pend[b] = valid[b];
+    }
+    u32 made = 0;
+    for (int round = 0; round < GPROBE; ++round) {
+        bool any = false;
+#pragma unroll
+        for (int b = 0; b < B; ++b) any |= pend[b];
+        if (!any) break;
+        u64 k[B], first[B];
+        u32 tag[B];
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            if (pend[b]) {
+                const GSlot* sl = &slots[h[b]];
+                k[b] = *(const u64*)&sl->key;
+                first[b] = *(const u64*)&sl->first;
+                tag[b] = *(const u32*)&sl->last_tag;
+            }
+        }
+        bool cas[B];
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            cas[b] = false;
+            if (!pend[b]) continue;
+            GSlot* sl = &slots[h[b]];
+            if (k[b] == key[b]) {
+                atomicAdd((unsigned long long*)&sl->count, (unsigned long long)cnt[b]);
+                if (ord[b] < first[b]) atomicMin((unsigned long long*)&sl->first, (unsigned long long)ord[b]);
+                if (tag[b] < a.file_tag) atomicMax(&sl->last_tag, a.file_tag);
+                pend[b] = false;
+            } else if (k[b] == 0) {
+                cas[b] = true;
+            } else {
+                h[b] = (u32)((h[b] + 1ull) & mask);
+            }
+        }
+        u64 old[B];
+#pragma unroll
+        for (int b = 0; b < B; ++b)
+            if (cas[b]) old[b] = atomicCAS((unsigned long long*)&slots[h[b]].key, 0ull, (unsigned long long)key[b]);
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            if (!cas[b]) continue;
+            if (old[b] == 0 || old[b] == key[b]) {
+                GSlot* sl = &slots[h[b]];
+                made += old[b] == 0 ? 1u : 0u;
+                atomicAdd((unsigned long long*)&sl->count, (unsigned long long)cnt[b]);
+                atomicMin((unsigned long long*)&sl->first, (unsigned long long)ord[b]);
+                atomicMax(&sl->last_tag, a.file_tag);
+                pend[b] = false;
+            } else {
+                h[b] = (u32)((h[b] + 1ull) & mask);
+            }
+        }
+    }
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+        if (!pend[b]) continue;  // probe bound exceeded: the overflow list (reinserted after a rehash)
+        const u64 i = atomicAdd((unsigned long long*)&a.st->n_overflow, 1ull);
+        if (i < T.ovf_cap) {
+            Overflow o;
+            o.key = key[b];
+            o.count = cnt[b];
+            o.first = ord[b];
+            o.tag = a.file_tag;
+            o.pad = 0;
+            T.ovf[i] = o;
+        } else {
+            atomicOr(&a.st->cap_flags, 2u);
         }
     }
     return made;
@@ -832,7 +935,13 @@ __device__ __forceinline__ u32 insert_many(const ScanArgs& a, const u64 (&key)[B
 #endif
 constexpr int CB = FR_CB;
 __device__ __attribute__((noinline)) void commit_buffers(ScanShared& sh, const ScanArgs& a, bool table, int tid) {
+#if FR_TIMING == 2
+    const u64 q0 = __builtin_amdgcn_s_memtime();
+#endif
     __syncthreads();
+#if FR_TIMING == 2
+    const u64 q1 = __builtin_amdgcn_s_memtime();
+#endif
     u32 made = 0;
     if (a.ablate & 64u) {  // diag: flushed LDS slots and cold entries per commit
         u32 live = 0;
@@ -867,7 +976,37 @@ __device__ __attribute__((noinline)) void commit_buffers(ScanShared& sh, const S
             }
         const u64* cl = a.cold + 2ull * (u64)blockIdx.x * a.cold_cap;
         for (u32 i = tid; i < nc; i += WG) out[nl + i] = LogEntry{cl[2 * i], cl[2 * i + 1], 1u, a.file_tag};
-    } else if (flush) {
+    } else if (FR_COMMIT2) {
+        // LDS slots and cold entries together: CB2 per lane per round of round-based inserts
+        const u64* cl = a.cold + 2ull * (u64)blockIdx.x * a.cold_cap;
+        const u32 nlds = flush ? (u32)NS : 0u;
+        for (u32 i0 = tid; i0 < nlds + nc; i0 += CB2 * WG) {
+            u64 key[CB2], ord[CB2];
+            u32 cnt[CB2];
+            bool v[CB2];
+#pragma unroll
+            for (int b = 0; b < CB2; ++b) {
+                const u32 i = i0 + b * WG;
+                v[b] = false;
+                key[b] = 0;
+                ord[b] = 0;
+                cnt[b] = 1;
+                if (i < nlds) {
+                    const LSlot e = sh.ls[i];
+                    v[b] = e.key != 0;
+                    key[b] = e.key;
+                    cnt[b] = e.cnt;
+                    ord[b] = make_ord(a, e.mino);
+                } else if (i < nlds + nc) {
+                    v[b] = true;
+                    key[b] = cl[2 * (i - nlds)];
+                    ord[b] = cl[2 * (i - nlds) + 1];
+                }
+            }
+            made += insert_rounds<CB2>(a, key, cnt, ord, v);
+        }
+    }
+    if (!FR_COMMIT2 && !logged && flush) {
         for (int i0 = tid; i0 < NS; i0 += CB * WG) {
             u64 key[CB], cnt[CB], ord[CB];
             bool v[CB];
@@ -883,8 +1022,11 @@ __device__ __attribute__((noinline)) void commit_buffers(ScanShared& sh, const S
             made += insert_many<CB>(a, key, cnt, ord, v);
         }
     }
+#if FR_TIMING == 2
+    const u64 q15 = __builtin_amdgcn_s_memtime();
+#endif
     const u64* cl = a.cold + 2ull * (u64)blockIdx.x * a.cold_cap;
-    for (u32 i0 = tid; i0 < (logged ? 0u : nc); i0 += CB * WG) {
+    for (u32 i0 = tid; i0 < ((logged || FR_COMMIT2) ? 0u : nc); i0 += CB * WG) {
         u64 key[CB], cnt[CB], ord[CB];
         bool v[CB];
 #pragma unroll
@@ -897,6 +1039,9 @@ __device__ __attribute__((noinline)) void commit_buffers(ScanShared& sh, const S
         }
         made += insert_many<CB>(a, key, cnt, ord, v);
     }
+#if FR_TIMING == 2
+    const u64 q2 = __builtin_amdgcn_s_memtime();
+#endif
     if (made) atomicAdd(&sh.created, made);
     // buffered exotic records and the first "no space" error
     const u32 ne = min(sh.nexo, (u32)EXO_BUF);
@@ -916,6 +1061,15 @@ __device__ __attribute__((noinline)) void commit_buffers(ScanShared& sh, const S
     if (tid == 0 && sh.err_off != 0xFFFFFFFFu)
         atomicMin((unsigned long long*)&a.st->err_nospace, (unsigned long long)(a.file_offset + sh.err_off));
     __syncthreads();
+#if FR_TIMING == 2
+    const u64 q3 = __builtin_amdgcn_s_memtime();
+    if ((tid & 63) == 0) {  // diagnostic build only: commit phases (entry barrier, inserts, exit barrier)
+        atomicAdd((unsigned long long*)&a.st->stamp[0], (unsigned long long)(q1 - q0));
+        atomicAdd((unsigned long long*)&a.st->stamp[1], (unsigned long long)(q2 - q1));
+        atomicAdd((unsigned long long*)&a.st->stamp[2], (unsigned long long)(q3 - q2));
+        atomicAdd((unsigned long long*)&a.st->stamp[3], (unsigned long long)(q15 - q1));  // of which the LDS-table part
+    }
+#endif
     if (table)
         for (int i = tid; i < NS; i += WG) {
             sh.ls[i] = LSlot{0, 0, 0xFFFFFFFFu};
@@ -1155,6 +1309,161 @@ __device__ __forceinline__ void parse_own_headers(ScanShared& sh, const ScanArgs
     }
 }
 
+// ---- header parse v2 (FR_PARSE2): fewer VALU instructions per header ------------------------
+// v_ffbl / v_ffbh return ~0 for 0, which the min tricks below rely on; the builtins add a
+// compare and select per word (or make the zero case undefined).
+__device__ __forceinline__ u32 ffbl32(u32 x) {
+    u32 r;
+    asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+__device__ __forceinline__ u32 ffbh32(u32 x) {
+    u32 r;
+    asm("v_ffbh_u32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+__device__ __forceinline__ u32 ctz64x(u64 x) { return min(ffbl32((u32)x), ffbl32((u32)(x >> 32)) | 32u); }  // ~0: none
+// index of the highest set bit; negative (-64) when none
+__device__ __forceinline__ int hsb64x(u64 x) { return (int)(min(ffbh32((u32)(x >> 32)), ffbh32((u32)x) | 32u) ^ 63u); }
+
+// bits [b, b + 64) of the 128-bit (x0, x1), b in [0, 63]
+__device__ __forceinline__ u64 window64(u64 x0, u64 x1, u32 b) { return (x0 >> b) | ((x1 << 1) << (63u - b)); }
+
+// R2 on the tile's bitmaps in two 64-bit windows: from the line start p the first ' ' or line end
+// f1 (a line end first: no ' ', IndexError); from the token start q = f1 + 1 the token end f2 and
+// the last ':' before it.  0: code at [start, start + n); 1: no ' '; 2: word-scan fallback (the
+// first ' ' or the token end lies 64 or more bytes on, or the token starts past the tile).
+__device__ __forceinline__ int locate_code2(const ScanShared& sh, u32 p, u32 bl, u32& start, u32& n) {
+    if (p >= bl) return 2;
+    const u32 w = p >> 6, b = p & 63u;
+    const u64 se = window64(sh.bsp[w], sh.bsp[w + 1], b);
+    const u64 eo = window64(sh.beol[w], sh.beol[w + 1], b);
+    const u32 f1 = ctz64x(se);
+    const u32 q = p + f1 + 1u;
+    if (f1 >= 64u) return 2;
+    if (ctz64x(eo) == f1) return 1;
+    if (q >= bl) return 2;
+    const u32 w2 = q >> 6, b2 = q & 63u;
+    const u64 se2 = window64(sh.bsp[w2], sh.bsp[w2 + 1], b2);
+    const u64 co2 = window64(sh.bcol[w2], sh.bcol[w2 + 1], b2);
+    const u32 f2 = ctz64x(se2);
+    if (f2 >= 64u) return 2;
+    const int hc = hsb64x(co2 & ((1ull << f2) - 1ull));  // the last ':' of the token, < 0 none
+    const u32 cs = (u32)max(hc + 1, 0);
+    start = q + cs;
+    n = f2 - cs;
+    return 0;
+}
+
+// code bytes [start, start + n) from the tile's LDS copy -> fast key, n wave-uniform (nu): the
+// per-word byte masks are scalars and only the words the code reaches are packed
+__device__ __forceinline__ bool encode_uniform(const ScanShared& sh, u32 start, u32 nu, u64& key) {
+    u32 w[8];
+    encode_load_lds(sh, start, w);
+    const u32 al = start & 3u;
+    u32 bad = 0, lo = 0, hi = 0;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        if ((u32)(4 * k) >= nu) break;  // uniform
+        const u32 x = __builtin_amdgcn_alignbyte(w[k + 1], w[k], al);
+        const u32 idx = (x >> 1) & 0x07070707u;
+        const u32 expect = __builtin_amdgcn_perm(0x4E002B00u, 0x47544341u, idx);
+        u32 sym = __builtin_amdgcn_perm(0x05000600u, 0x03040201u, idx);
+        const u32 left = nu - 4u * k;
+        if (left >= 4u) {
+            bad |= expect ^ x;
+        } else {
+            const u32 vm = 0xFFFFFFFFu >> (32u - 8u * left);  // uniform
+            bad |= (expect ^ x) & vm;
+            sym &= vm;
+        }
+        const u32 packed = __builtin_amdgcn_udot4(sym, 0x00400801u, (sym >> 15) & 0xE00u, false);
+        if (k == 0) lo = packed;
+        else if (k == 1) lo |= packed << 12;
+        else if (k == 2) { lo |= packed << 24; hi = packed >> 8; }
+        else hi |= packed << (12 * k - 32);
+    }
+    key = ((u64)hi << 32) | lo;
+    return bad == 0;
+}
+
+__device__ __forceinline__ void parse_header2(ScanShared& sh, const ScanArgs& a, u64 tile0, u32 p, u32 bl) {
+    u32 start = 0, n = 0;
+    const int r = locate_code2(sh, p, bl, start, n);
+    if (a.ablate & 2u) {
+        asm volatile("" ::"v"(start), "v"(n), "v"(r));
+        return;
+    }
+    u64 key = 0;
+    bool fast = false;
+    if (r == 0 && n >= 1u && n <= (u32)MAXSYM) {
+        const u32 nu = __builtin_amdgcn_readfirstlane(n);
+        if (__ballot(n != nu) == 0) fast = encode_uniform(sh, start, nu, key);  // the common case
+        else fast = encode_glob(sh, a, tile0, start, n, key);
+    }
+    if (fast) count_code(sh, a, tile0, p, key);
+    else rare_push(sh, a, (u32)(tile0 + p), (u32)r, (u32)(tile0 + start), n);
+}
+
+// the line starts after every 4th terminator (lines ≡ 0 mod 4) in this lane's segment, parsed
+// where they lie.  The first header needs the skip-th set bit of the terminator mask; a second
+// one in the same segment (records shorter than 64 B) takes the loop at the end.
+__device__ __forceinline__ void parse_own_headers2(ScanShared& sh, const ScanArgs& a, u32 t, const SegClass& sc,
+                                                   u64 L0, int tid, int wid) {
+    const u64 tile0 = (u64)t * TSTEP;
+    const u32 nb = (u32)min((u64)(TILE + HALO), a.avail - tile0);
+    const u32 bl = min((u32)TILE, nb);
+    const u64 rem64 = a.len - tile0;  // line starts p < pend are this launch's (uniform)
+    const u32 pend = rem64 >= 0xFFFFFFFFull ? 0xFFFFFFFFu : (u32)rem64 + ((a.own_end && a.len < a.avail) ? 1u : 0u);
+    // terminators in earlier waves of the tile: wave sums from LDS, summed on the scalar unit
+    typedef u32 u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 ws = *(const __attribute__((address_space(3))) u32x4*)&sh.wsum[0];
+    const u32 w0 = __builtin_amdgcn_readfirstlane(ws.x), w1 = __builtin_amdgcn_readfirstlane(ws.y),
+              w2 = __builtin_amdgcn_readfirstlane(ws.z);
+    const u32 wexcl = (wid > 0 ? w0 : 0u) + (wid > 1 ? w1 : 0u) + (wid > 2 ? w2 : 0u);
+    const u32 lb = (u32)L0 + wexcl + (sc.x - sc.c);  // terminators before this segment (low bits)
+    const u32 skip = (3u - lb) & 3u;
+    const u32 s0 = tid * SEG;
+    u64 m = sc.tmask;
+#pragma unroll
+    for (u32 q = 0; q < 3; ++q) {
+        const u64 d = m & (m - 1ull);
+        m = q < skip ? d : m;
+    }
+    const bool limited = a.max_records > 0;  // -s: uniform
+    u64 rec = 0;
+    if (limited) rec = (L0 + wexcl + (sc.x - sc.c) + skip + 1u) >> 2;
+    const bool own0 = t == 0 && tid == 0 && a.own_start && (L0 & 3ull) == 0 && a.avail > 0 &&
+                      (!limited || (i64)(L0 >> 2) < a.max_records);
+    // m's lowest set bit: the first header terminator.  own0's header at position 0 comes first.
+    const u32 p = own0 ? 0u : s0 + ctz64x(m) + 1u;
+    const bool ok = own0 || (m != 0 && p < pend && (!limited || (i64)rec < a.max_records));
+    if (ok) parse_header2(sh, a, tile0, p, bl);
+    // another header in this segment (records shorter than 64 B; never at R=8's 74 B): uniform check
+    bool more = ok && (own0 ? m != 0 : __popcll(m) > 4);
+    if (!__ballot(more)) return;
+    if (!own0) {
+        m &= m - 1ull;
+        m &= m - 1ull;
+        m &= m - 1ull;
+        m &= m - 1ull;
+        ++rec;
+    }
+    while (__ballot(more)) {
+        if (more) {
+            const u32 pn = s0 + ctz64x(m) + 1u;
+            more = pn < pend && (!limited || (i64)rec < a.max_records);
+            if (more) parse_header2(sh, a, tile0, pn, bl);
+            ++rec;
+            m &= m - 1ull;
+            m &= m - 1ull;
+            m &= m - 1ull;
+            m &= m - 1ull;
+            more = more && m != 0;
+        }
+    }
+}
+
 // walk tiles [tb, te) of the range; L0 = line index (absolute, or mod-4 guess) at tile tb.
 // parse = false: count only.  (exact is kept for symmetry: with an exact phase a full cold
 // list falls back to direct HBM inserts inside lds_insert.)
@@ -1163,9 +1472,9 @@ __device__ __forceinline__ u64 walk_chunk(ScanShared& sh, const ScanArgs& a, u32
                           int lane, int wid) {
     u64 lines = 0;
     u32 done = sh.rq_tail;  // the caller synchronised: every thread reads the same value
-#if FR_TIMING
+#if FR_TIMING == 1
     u64 tm0 = 0, tm1 = 0, tm2 = 0, tm3 = 0;
-    const u64 w0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+    const u64 w0 = __builtin_amdgcn_s_memtime();
 #endif
 #if FR_LDS_RAW
     // Each lane's segment of tile t arrives in registers FR_PF_DEPTH tiles ahead: its loads are
@@ -1173,11 +1482,11 @@ __device__ __forceinline__ u64 walk_chunk(ScanShared& sh, const ScanArgs& a, u32
     // flight through its barriers and its parse.  After B1 the segment goes to the tile's LDS copy
     // (the parse reads code bytes there) and the registers take the loads of tile t+FR_PF_DEPTH.
     auto step = [&](u32 t, SegRegs& r) {
-#if FR_TIMING
+#if FR_TIMING == 1
         const u64 c0 = __builtin_amdgcn_s_memtime();
 #endif
         const SegClass sc = seg_classify(a, t, r, tid);
-#if FR_TIMING
+#if FR_TIMING == 1
         __builtin_amdgcn_s_waitcnt(0);
         const u64 c1 = __builtin_amdgcn_s_memtime();
 #endif
@@ -1203,14 +1512,24 @@ __device__ __forceinline__ u64 walk_chunk(ScanShared& sh, const ScanArgs& a, u32
             if (t + FR_PF_DEPTH < te) seg_prefetch_next(a, t + FR_PF_DEPTH, r, tid);
         }
         lds_barrier();  // B2
-#if FR_TIMING
+#if FR_TIMING == 1
         const u64 c2 = __builtin_amdgcn_s_memtime();
 #endif
+#if FR_PARSE2
+        if (parse && !uniform_flag(sh.spec_bad) && !(a.ablate & 1u))
+            parse_own_headers2(sh, a, t, sc, L0 + lines, tid, wid);
+        {
+            typedef u32 u32x4 __attribute__((ext_vector_type(4)));
+            const u32x4 ws = *(const __attribute__((address_space(3))) u32x4*)&sh.wsum[0];
+            lines += __builtin_amdgcn_readfirstlane(ws.x + ws.y + ws.z + ws.w);
+        }
+#else
         const TileCount tc = seg_count(sh, sc, wid);
         if (parse && !uniform_flag(sh.spec_bad) && !(a.ablate & 1u))
             parse_own_headers(sh, a, t, tc, L0 + lines, tid, r, false);
         lines += tc.tot;
-#if FR_TIMING
+#endif
+#if FR_TIMING == 1
         __builtin_amdgcn_s_waitcnt(0);
         const u64 c3 = __builtin_amdgcn_s_memtime();
         tm0 += c1 - c0;  // load + classify
@@ -1234,7 +1553,7 @@ __device__ __forceinline__ u64 walk_chunk(ScanShared& sh, const ScanArgs& a, u32
     seg_fetch(a, tb, r, tid, tb < te && seg_in_range(a, tb));
 #endif
     for (u32 t = tb; t < te; ++t) {
-#if FR_TIMING
+#if FR_TIMING == 1
         const u64 c0 = __builtin_amdgcn_s_memtime();
 #endif
 #if FR_PREFETCH
@@ -1244,7 +1563,7 @@ __device__ __forceinline__ u64 walk_chunk(ScanShared& sh, const ScanArgs& a, u32
         seg_prefetch_next(a, t, r, tid);
 #endif
         const SegClass sc = seg_classify(a, t, r, tid);
-#if FR_TIMING
+#if FR_TIMING == 1
         __builtin_amdgcn_s_waitcnt(0);
         const u64 c1 = __builtin_amdgcn_s_memtime();
 #endif
@@ -1258,7 +1577,7 @@ __device__ __forceinline__ u64 walk_chunk(ScanShared& sh, const ScanArgs& a, u32
         }
         seg_store(sh, sc, tid, lane, wid);
         lds_barrier();  // B2
-#if FR_TIMING
+#if FR_TIMING == 1
         const u64 c2 = __builtin_amdgcn_s_memtime();
 #endif
         const TileCount tc = seg_count(sh, sc, wid);
@@ -1268,7 +1587,7 @@ __device__ __forceinline__ u64 walk_chunk(ScanShared& sh, const ScanArgs& a, u32
         else if (FR_PREFETCH)
             seg_fetch(a, t + 1, r, tid, pf);
         lines += tc.tot;
-#if FR_TIMING
+#if FR_TIMING == 1
         __builtin_amdgcn_s_waitcnt(0);
         const u64 c3 = __builtin_amdgcn_s_memtime();
         tm0 += c1 - c0;  // load + classify
@@ -1278,14 +1597,13 @@ __device__ __forceinline__ u64 walk_chunk(ScanShared& sh, const ScanArgs& a, u32
 #endif
     }
 #endif
-#if FR_TIMING
+#if FR_TIMING == 1
     if ((tid & 63) == 0) {  // diagnostic build only: per-phase shader cycles summed over waves
         atomicAdd((unsigned long long*)&a.st->stamp[0], (unsigned long long)tm0);
         atomicAdd((unsigned long long*)&a.st->stamp[1], (unsigned long long)tm1);
         atomicAdd((unsigned long long*)&a.st->stamp[2], (unsigned long long)tm2);
         atomicAdd((unsigned long long*)&a.st->stamp[3], (unsigned long long)tm3);
         atomicAdd((unsigned long long*)&a.st->stamp[4], (unsigned long long)(__builtin_amdgcn_s_memtime() - w0));
-        atomicAdd((unsigned long long*)&a.st->stamp[5], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - r0));
     }
 #endif
     __syncthreads();  // the bitmaps are free for the caller; the last tile's events are queued
@@ -1418,6 +1736,10 @@ __global__ __launch_bounds__(WG, FR_OCC) void chunk_kernel(ScanArgs args) {
         sh.rq_tail = 0;
     }
     const u64 base_lines = a.st->lines[a.par];
+#if FR_TIMING
+    u64 tguess = 0, tcommit = 0;
+    const u64 k0 = __builtin_amdgcn_s_memtime();
+#endif
     for (;;) {
         if (tid == 0) sh.chunk = atomicAdd(&a.st->ticket, 1u);
         __syncthreads();
@@ -1431,7 +1753,13 @@ __global__ __launch_bounds__(WG, FR_OCC) void chunk_kernel(ScanArgs args) {
         if (c == 0) {
             P = (int)(base_lines & 3ull);
         } else if (a.max_records <= 0 && !empty && !a.exo_only) {
+#if FR_TIMING
+            const u64 g0 = __builtin_amdgcn_s_memtime();
+#endif
             P = guess_phase(sh, a, tb, tid, lane, wid);
+#if FR_TIMING
+            tguess += __builtin_amdgcn_s_memtime() - g0;
+#endif
         }
         // pass 0: exact (chunk 0) / speculative (guessed phase) / count-only (unsure, -s);
         // pass 1 (only when pass 0 cannot be kept): exact, after the chunk-level look-back
@@ -1469,12 +1797,25 @@ __global__ __launch_bounds__(WG, FR_OCC) void chunk_kernel(ScanArgs args) {
             parse = true;
             exact = true;
         }
+#if FR_TIMING
+        const u64 c0 = __builtin_amdgcn_s_memtime();
+#endif
         commit_buffers(sh, a, true, tid);  // starts and ends with a barrier: sh.last is visible
+#if FR_TIMING
+        tcommit += __builtin_amdgcn_s_memtime() - c0;
+#endif
         if (sh.last) {
             __atomic_thread_fence(__ATOMIC_ACQUIRE);
             verify_launch(sh, a, base_lines, tid);
         }
     }
+#if FR_TIMING
+    if ((tid & 63) == 0) {  // diagnostic build only: guess / commit / whole-kernel wave cycles
+        atomicAdd((unsigned long long*)&a.st->stamp[6], (unsigned long long)tguess);
+        atomicAdd((unsigned long long*)&a.st->stamp[7], (unsigned long long)tcommit);
+        atomicAdd((unsigned long long*)&a.st->stamp[5], (unsigned long long)(__builtin_amdgcn_s_memtime() - k0));
+    }
+#endif
     __syncthreads();
     if (tid == 0) {
         if (sh.created) atomicAdd((unsigned long long*)&a.st->n_keys, (unsigned long long)sh.created);

@@ -32,9 +32,11 @@ struct fr_ctx {
     LogEntry* log = nullptr;
     LogEntry* log_sorted = nullptr;
     u64 log_cap = 0;
-    u32* log_hist = nullptr;
+    u32* log_hist = nullptr;       // aggregation scratch, (AGG_SLICES + 3) x AGG_NB
     void* log_temp = nullptr;
     size_t log_temp_bytes = 0;
+    u32 log_min = 2600;            // pairs from which a commit logs (SYN-v1 config 2's full chunks commit ~1740 pairs
+                                   // and are faster inserted directly; config 3's ~2680 are faster logged)
     uint4* rare = nullptr;
 
     DevState* st = nullptr;
@@ -474,6 +476,7 @@ static int launch_range(fr_ctx* ctx, const u8* dptr, u64 len, u64 avail, int own
     a.cold = ctx->cold;
     a.log = exo_only ? nullptr : ctx->log;
     a.log_cap = ctx->log_cap;
+    a.log_min = ctx->log_min;
     a.rare = ctx->rare;
     // workgroups take chunks by ticket; never more than the resident grid (cold lists are per block)
     const int grid = (int)std::min<u64>(a.num_chunks, G);
@@ -484,8 +487,8 @@ static int launch_range(fr_ctx* ctx, const u8* dptr, u64 len, u64 avail, int own
     ctx->last_valid = true;
     CK(hipEventRecord(ctx->ev_b[ctx->ev_used], ctx->stream));
     if (a.log)
-        CK(launch_log_aggregate(ctx->tab, ctx->st, ctx->log, ctx->log_sorted, ctx->log_cap, ctx->log_hist,
-                                ctx->log_temp, ctx->log_temp_bytes, ctx->stream));
+        CK(launch_log_aggregate(ctx->tab, ctx->st, ctx->log, ctx->log_sorted, ctx->log_cap, ctx->log_hist, a.file_tag,
+                                a.file_offset, ctx->ablate, ctx->stream));
     CK(hipEventRecord(ctx->ev_l[ctx->ev_used], ctx->stream));
     ctx->ev_used++;
     ctx->scan_launches++;
@@ -523,18 +526,19 @@ fr_ctx* fr_create(int device, uint64_t chunk_bytes, uint64_t table_slots) {
     ctx->chunk_bytes = chunk_bytes ? ((chunk_bytes + TILE - 1) / TILE) * TILE : (256ull << 20);
     if (ctx->chunk_bytes > RANGE_MAX) ctx->chunk_bytes = RANGE_MAX;
     ctx->ring_bytes = std::min<u64>(ctx->chunk_bytes, HOST_CHUNK_MAX);
-    // launch log: room for one pair per 256 B of a launch (SYN-v1 needs one per 350-500 B; a
-    // commit that does not fit inserts into the table directly)
-    const char* fl = getenv("FR_LOG");  // off by default until the aggregation beats direct commits everywhere
-    if (fl && atoi(fl) != 0) {
+    // launch log: room for one pair per 256 B of a launch (SYN-v1 needs one per 350-500 B; a commit
+    // that does not fit inserts into the table directly).  Only heavy commits log (ScanArgs::log_min);
+    // FR_LOG=0 turns the log off, FR_LOG_MIN sets the threshold (pairs per commit)
+    const char* fl = getenv("FR_LOG");
+    if (!fl || atoi(fl) != 0) {
         ctx->log_cap = std::min<u64>(std::max<u64>(ctx->chunk_bytes / 256, 1ull << 16), 1ull << 26);
         if ((e = dalloc(&ctx->log, ctx->log_cap)) != hipSuccess) return bad("launch log", e);
         if ((e = dalloc(&ctx->log_sorted, ctx->log_cap)) != hipSuccess) return bad("launch log", e);
-        if ((e = dalloc(&ctx->log_hist, 2ull * AGG_NB * AGG_SLICES)) != hipSuccess) return bad("log histogram", e);
-        ctx->log_temp_bytes = log_aggregate_temp_bytes();
-        if ((e = hipMalloc(&ctx->log_temp, std::max<size_t>(ctx->log_temp_bytes, 16))) != hipSuccess)
-            return bad("log scan", e);
+        const u64 nh = (u64)(AGG_SLICES + 3) * AGG_NB;
+        if ((e = dalloc(&ctx->log_hist, nh)) != hipSuccess) return bad("log histogram", e);
+        if ((e = hipMemset(ctx->log_hist, 0, nh * sizeof(u32))) != hipSuccess) return bad("log histogram", e);
     }
+    if (const char* f = getenv("FR_LOG_MIN")) ctx->log_min = (u32)std::max(0, atoi(f));
     if (const char* f = getenv("FR_CHUNK_TILES")) ctx->chunk_tiles = (u32)std::max(2, atoi(f));
     if (const char* f = getenv("FR_RAMP")) ctx->ramp = atoi(f) != 0;
     ctx->tiles_cap = RANGE_MAX / TSTEP + 2;

@@ -76,15 +76,17 @@ struct alignas(32) Overflow {
 // misses are appended to the launch's log at the chunk's commit; after the launch the log is
 // bucketed by key hash and each bucket is aggregated in LDS, so the HBM table sees one insert per
 // distinct code per launch instead of one per commit and miss.
-struct alignas(8) LogEntry {
+struct alignas(16) LogEntry {
     u64 key;
-    u64 ord;             // min ordinal of the entry's records
+    u32 off;             // min range offset of the entry's records (the launch's file tag / offset complete the ordinal)
     u32 cnt;
-    u32 tag;             // file tag
 };
-constexpr int AGG_LOG_NB = 12;             // log2 of the buckets of the launch-log aggregation
+#ifndef FR_AGG_LOG_NB
+#define FR_AGG_LOG_NB 12
+#endif
+constexpr int AGG_LOG_NB = FR_AGG_LOG_NB;  // log2 of the buckets of the launch-log aggregation
 constexpr int AGG_NB = 1 << AGG_LOG_NB;
-constexpr int AGG_SLICES = 256;            // histogram / scatter workgroups (slices of the log)
+constexpr int AGG_SLICES = 512;            // count / scatter workgroups (slices of the log)
 
 struct DevState {
     u64 lines[2];        // terminators before the current range (launch parity)
@@ -149,6 +151,7 @@ struct ScanArgs {
     u64* chunk_info;     // chunk kernel: per chunk {line count, spec flag + guessed phase << 1 in the high word}
     LogEntry* log;       // the launch log (nullptr: commits insert into the HBM table directly)
     u64 log_cap;
+    u32 log_min;         // a commit of at least log_min pairs goes to the log, smaller ones straight into the table
     u32 exo_only;        // replay of a launch whose exotic list overflowed: capture exotic records only (no
                          // table updates), every chunk with its exact line phase
     u32 spec_commit;     // commit speculative chunks without waiting for their exact prefix (checked at the
@@ -222,8 +225,8 @@ hipError_t launch_presence_scan(const GSlot* slots, u64 n, u32 tag, Presence* pr
 hipError_t launch_merge(Table t, DevState* st, const u64* keys, const u64* counts, const u64* first, u64 n,
                         hipStream_t s);
 // aggregate the launch log into the table and empty it (stream-ordered; reads log_n on the device)
-hipError_t launch_log_aggregate(Table t, DevState* st, LogEntry* log, LogEntry* sorted, u64 cap, u32* hist,
-                                void* temp, size_t temp_bytes, hipStream_t s);
+hipError_t launch_log_aggregate(Table t, DevState* st, LogEntry* log, LogEntry* sorted, u64 cap, u32* hist, u32 file_tag,
+                                u64 file_offset, u32 ablate, hipStream_t s);
 size_t log_aggregate_temp_bytes();
 hipError_t launch_synth(u8* out, u64 r0, u64 n, int R, u64 seed, const u8* idx1, const u8* idx2, int S, int L1,
                         int L2, hipStream_t s);

@@ -14,6 +14,7 @@
 // LDS (lane per header), packs the code 3 bits/char and counts it in an LDS-private
 // open-addressing table that is flushed to the HBM table with 64-bit atomics.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #include <rocprim/rocprim.hpp>
@@ -934,7 +935,8 @@ __device__ __forceinline__ u32 insert_rounds(const ScanArgs& a, const u64 (&key)
 #define FR_CB 4
 #endif
 constexpr int CB = FR_CB;
-__device__ __attribute__((noinline)) void commit_buffers(ScanShared& sh, const ScanArgs& a, bool table, int tid) {
+__device__ __attribute__((noinline)) void commit_buffers(ScanShared& sh, const ScanArgs& a, bool table, int tid,
+                                                        u32 ntiles) {
 #if FR_TIMING == 2
     const u64 q0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -954,7 +956,10 @@ __device__ __attribute__((noinline)) void commit_buffers(ScanShared& sh, const S
     const u32 nc = (a.ablate & 8u) ? 0u : min(sh.ncold, a.cold_cap);
     const u32 nl = flush ? sh.nkeys : 0u;  // claimed LDS slots = the live ones
     bool logged = false;
-    if (a.log && nl + nc) {
+    // heavy commits (at least log_min pairs: many distinct codes per chunk) go to the launch log,
+    // aggregated after the launch; lighter ones insert straight into the table
+    (void)ntiles;
+    if (a.log && nl + nc && nl + nc >= a.log_min) {
         // one block of the launch log for this commit's pairs (aggregated after the launch:
         // launch_log_aggregate); a block past the log's end is blanked and the pairs inserted below
         if (tid == 0) {
@@ -962,7 +967,7 @@ __device__ __attribute__((noinline)) void commit_buffers(ScanShared& sh, const S
             sh.log_base = base + nl + nc <= a.log_cap ? base : ~0ull;
             sh.log_pos = 0;
             if (base + nl + nc > a.log_cap)
-                for (u64 i = base; i < a.log_cap; ++i) a.log[i] = LogEntry{0, 0, 0, 0};
+                for (u64 i = base; i < a.log_cap; ++i) a.log[i] = LogEntry{0, 0, 0};
         }
         __syncthreads();
         logged = sh.log_base != ~0ull;
@@ -972,10 +977,10 @@ __device__ __attribute__((noinline)) void commit_buffers(ScanShared& sh, const S
         if (flush)
             for (int i = tid; i < NS; i += WG) {
                 const LSlot e = sh.ls[i];
-                if (e.key) out[atomicAdd(&sh.log_pos, 1u)] = LogEntry{e.key, make_ord(a, e.mino), e.cnt, a.file_tag};
+                if (e.key) out[atomicAdd(&sh.log_pos, 1u)] = LogEntry{e.key, e.mino, e.cnt};
             }
         const u64* cl = a.cold + 2ull * (u64)blockIdx.x * a.cold_cap;
-        for (u32 i = tid; i < nc; i += WG) out[nl + i] = LogEntry{cl[2 * i], cl[2 * i + 1], 1u, a.file_tag};
+        for (u32 i = tid; i < nc; i += WG) out[nl + i] = LogEntry{cl[2 * i], (u32)(cl[2 * i + 1] - make_ord(a, 0)), 1u};
     } else if (FR_COMMIT2) {
         // LDS slots and cold entries together: CB2 per lane per round of round-based inserts
         const u64* cl = a.cold + 2ull * (u64)blockIdx.x * a.cold_cap;
@@ -1800,7 +1805,7 @@ __global__ __launch_bounds__(WG, FR_OCC) void chunk_kernel(ScanArgs args) {
 #if FR_TIMING
         const u64 c0 = __builtin_amdgcn_s_memtime();
 #endif
-        commit_buffers(sh, a, true, tid);  // starts and ends with a barrier: sh.last is visible
+        commit_buffers(sh, a, true, tid, te - tb);  // starts and ends with a barrier: sh.last is visible
 #if FR_TIMING
         tcommit += __builtin_amdgcn_s_memtime() - c0;
 #endif
@@ -1904,7 +1909,11 @@ hipError_t launch_rehash(Table dst, DevState* st, const GSlot* src, u64 nsrc, hi
 // and only the distinct codes reach the HBM table -- batched, with every slot load in flight at
 // once and nothing else competing for the memory system.
 // ------------------------------------------------------------------------------------
-__device__ __forceinline__ u32 log_bucket(u64 key) { return (u32)(mix64(key) >> (64 - AGG_LOG_NB)); }
+// bucket of a logged code: the top bits of a multiplicative hash of the key folded to 32 bits (the
+// LDS table of log_reduce_kernel indexes by mix64's low bits, independent of these)
+__device__ __forceinline__ u32 log_bucket(u64 key) {
+    return (((u32)key ^ (u32)(key >> 29)) * 0x9E3779B1u) >> (32 - AGG_LOG_NB);
+}
 
 __device__ __forceinline__ void log_slice(u64 n, u32 s, u64& lo, u64& hi) {
     const u64 per = (n + AGG_SLICES - 1) / AGG_SLICES;
@@ -1912,140 +1921,309 @@ __device__ __forceinline__ void log_slice(u64 n, u32 s, u64& lo, u64& hi) {
     hi = min(n, lo + per);
 }
 
-__global__ __launch_bounds__(256) void log_hist_kernel(const LogEntry* log, const DevState* st, u64 cap, u32* hist) {
+// aggregation scratch (fr_api allocates (AGG_SLICES + 3) * AGG_NB u32, zeroed once):
+//   sh[s][b]  per-slice bucket counts        total[b]  entries per bucket (zeroed again by log_base_kernel)
+//   base[b]   first entry of bucket b         cur[b]    scatter cursor (starts at base[b])
+struct AggScratch {
+    u32* sh;
+    u32* total;
+    u32* base;
+    u32* cur;
+    __host__ __device__ static AggScratch at(u32* p) {
+        return AggScratch{p, p + (size_t)AGG_SLICES * AGG_NB, p + (size_t)(AGG_SLICES + 1) * AGG_NB,
+                          p + (size_t)(AGG_SLICES + 2) * AGG_NB};
+    }
+};
+
+// pass 1: bucket counts per slice of the log, summed per bucket with one atomic per (slice, bucket)
+__global__ __launch_bounds__(256) void log_count_kernel(const LogEntry* log, const DevState* st, u64 cap, AggScratch g) {
+    const u64 n = min(st->log_n, cap);
+    if (n == 0) return;
     __shared__ u32 h[AGG_NB];
     for (int i = threadIdx.x; i < AGG_NB; i += 256) h[i] = 0;
     __syncthreads();
-    const u64 n = min(st->log_n, cap);
     u64 lo, hi;
     log_slice(n, blockIdx.x, lo, hi);
-    for (u64 i = lo + threadIdx.x; i < hi; i += 256) {
-        const u64 k = log[i].key;
-        if (k) atomicAdd(&h[log_bucket(k)], 1u);
+    for (u64 i0 = lo + threadIdx.x; i0 < hi; i0 += 8 * 256) {  // eight loads in flight per thread
+        u64 k[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const u64 i = i0 + (u64)q * 256;
+            k[q] = i < hi ? log[i].key : 0ull;
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            if (k[q]) atomicAdd(&h[log_bucket(k[q])], 1u);
     }
     __syncthreads();
-    for (int b = threadIdx.x; b < AGG_NB; b += 256) hist[(u64)b * AGG_SLICES + blockIdx.x] = h[b];
+    u32* row = g.sh + (size_t)blockIdx.x * AGG_NB;
+    for (int b = threadIdx.x; b < AGG_NB; b += 256) {
+        const u32 c = h[b];
+        row[b] = c;
+        if (c) atomicAdd(&g.total[b], c);
+    }
 }
 
-__global__ __launch_bounds__(256) void log_scatter_kernel(const LogEntry* log, const DevState* st, u64 cap,
-                                                          const u32* offs, LogEntry* sorted) {
+// pass 2 (one workgroup): bucket bases = exclusive scan of the totals; cursors start there
+__global__ __launch_bounds__(1024) void log_base_kernel(const DevState* st, AggScratch g) {
+    if (st->log_n == 0) return;
+    constexpr int PER = AGG_NB / 1024;
+    __shared__ u32 ws[16];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    u32 v[PER], sum = 0;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        v[j] = g.total[tid * PER + j];
+        sum += v[j];
+    }
+    u32 x = sum;  // inclusive wave scan, then across the 16 waves
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const u32 y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) ws[wid] = x;
+    __syncthreads();
+    u32 before = 0;
+    for (int w = 0; w < wid; ++w) before += ws[w];
+    u32 run = before + x - sum;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int b = tid * PER + j;
+        g.base[b] = run;
+        g.cur[b] = run;
+        g.total[b] = 0;  // ready for the next launch's pass 1
+        run += v[j];
+    }
+}
+
+// pass 3: each slice claims its run of every bucket (one atomic per non-empty bucket) and scatters
+__global__ __launch_bounds__(256) void log_scatter_kernel(const LogEntry* log, const DevState* st, u64 cap, AggScratch g,
+                                                          LogEntry* sorted) {
+    const u64 n = min(st->log_n, cap);
+    if (n == 0) return;
     __shared__ u32 o[AGG_NB];
-    for (int b = threadIdx.x; b < AGG_NB; b += 256) o[b] = offs[(u64)b * AGG_SLICES + blockIdx.x];
+    const u32* row = g.sh + (size_t)blockIdx.x * AGG_NB;
+    for (int b = threadIdx.x; b < AGG_NB; b += 256) {
+        const u32 c = row[b];
+        o[b] = c ? atomicAdd(&g.cur[b], c) : 0u;
+    }
     __syncthreads();
-    const u64 n = min(st->log_n, cap);
     u64 lo, hi;
     log_slice(n, blockIdx.x, lo, hi);
-    for (u64 i = lo + threadIdx.x; i < hi; i += 256) {
-        const LogEntry e = log[i];
-        if (e.key) sorted[atomicAdd(&o[log_bucket(e.key)], 1u)] = e;
+    for (u64 i0 = lo + threadIdx.x; i0 < hi; i0 += 8 * 256) {  // eight loads in flight per thread
+        LogEntry e[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const u64 i = i0 + (u64)q * 256;
+            e[q] = i < hi ? log[i] : LogEntry{0, 0, 0};
+        }
+        u32 pos[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) pos[q] = e[q].key ? atomicAdd(&o[log_bucket(e[q].key)], 1u) : 0u;
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            if (e[q].key) sorted[pos[q]] = e[q];
     }
 }
 
-constexpr int AGG_LNS = 2048;  // LDS slots of one bucket's aggregation
+#ifndef FR_AGG_LNS
+#define FR_AGG_LNS 2048
+#endif
+constexpr int AGG_LNS = FR_AGG_LNS;  // LDS slots of one bucket's aggregation
 constexpr int AGG_PROBE = 64;
-struct AggSlot {
-    u64 key, first;
-    u32 cnt, tag;
+struct alignas(16) AggSlot {
+    u64 key;
+    u32 mino, cnt;  // min range offset, records
 };
 
-// up to B distinct codes into the HBM table with their slot loads in flight together
-template <int B>
-__device__ __forceinline__ u32 insert_batch(const Table& T, DevState* st, const u64 (&key)[B], const u64 (&cnt)[B],
-                                            const u64 (&ord)[B], const u32 (&tag)[B], const bool (&valid)[B]) {
-    uint4 w0[B], w1[B];
-    u64 h[B];
+// distinct (key, count, first, last tag) rows into the HBM table in rounds: every pending row's probe
+// slot is loaded together, hits take fire-and-forget atomics, empty slots are claimed by CASes issued
+// together (a lane waits for max-probe-depth round trips, not the sum over its rows)
+// EXCL: no other thread touches these keys' slots while this kernel runs (log_reduce_kernel's buckets
+// partition the keys and nothing else updates the table): a found or claimed slot takes plain stores of
+// the updated count / first / tag instead of three memory-side atomics.
+template <int B, bool EXCL = false>
+__device__ __forceinline__ u32 insert_rows(const Table& T, DevState* st, const u64 (&key)[B], const u32 (&cnt)[B],
+                                           const u64 (&ord)[B], const u32 (&tag)[B], const bool (&valid)[B]) {
+    u32 h[B];
+    bool pend[B];
 #pragma unroll
     for (int b = 0; b < B; ++b) {
-        h[b] = mix64(key[b]) & T.mask;
-        if (valid[b]) {
-            const GSlot* sl = &T.slots[h[b]];
-            w0[b] = *(const uint4*)sl;
-            w1[b] = *((const uint4*)sl + 1);
-        }
+        h[b] = (u32)(mix64(key[b]) & T.mask);
+        pend[b] = valid[b];
     }
     u32 made = 0;
+    for (int round = 0; round < GPROBE; ++round) {
+        bool any = false;
+#pragma unroll
+        for (int b = 0; b < B; ++b) any |= pend[b];
+        if (!any) break;
+        uint4 w0[B], w1[B];
+#pragma unroll
+        for (int b = 0; b < B; ++b)
+            if (pend[b]) {
+                const GSlot* sl = &T.slots[h[b]];
+                w0[b] = *(const uint4*)sl;
+                w1[b] = *((const uint4*)sl + 1);
+            }
+        bool cas[B];
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            cas[b] = false;
+            if (!pend[b]) continue;
+            const u64 k = ((u64)w0[b].y << 32) | w0[b].x;
+            if (k == key[b]) {
+                GSlot* sl = &T.slots[h[b]];
+                const u64 first = ((u64)w1[b].y << 32) | w1[b].x;
+                if (EXCL) {
+                    const u64 c = (((u64)w0[b].w << 32) | w0[b].z) + cnt[b];
+                    const u64 f = min(first, ord[b]);
+                    *((uint4*)sl) = make_uint4(w0[b].x, w0[b].y, (u32)c, (u32)(c >> 32));
+                    *((uint4*)sl + 1) = make_uint4((u32)f, (u32)(f >> 32), max(w1[b].z, tag[b]), w1[b].w);
+                } else {
+                    atomicAdd((unsigned long long*)&sl->count, (unsigned long long)cnt[b]);
+                    if (ord[b] < first) atomicMin((unsigned long long*)&sl->first, (unsigned long long)ord[b]);
+                    if (w1[b].z < tag[b]) atomicMax(&sl->last_tag, tag[b]);
+                }
+                pend[b] = false;
+            } else if (k == 0) {
+                cas[b] = true;
+            } else {
+                h[b] = (u32)((h[b] + 1ull) & T.mask);
+            }
+        }
+        u64 old[B];
+#pragma unroll
+        for (int b = 0; b < B; ++b)
+            if (cas[b]) old[b] = atomicCAS((unsigned long long*)&T.slots[h[b]].key, 0ull, (unsigned long long)key[b]);
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            if (!cas[b]) continue;
+            if (old[b] == 0 || old[b] == key[b]) {
+                GSlot* sl = &T.slots[h[b]];
+                made += old[b] == 0 ? 1u : 0u;
+                if (EXCL && old[b] == 0) {  // claimed an initialised slot (count 0, first ~0, tag 0): ours alone
+                    *((u64*)&sl->count) = cnt[b];
+                    *((uint4*)sl + 1) = make_uint4((u32)ord[b], (u32)(ord[b] >> 32), tag[b], w1[b].w);
+                } else {
+                    atomicAdd((unsigned long long*)&sl->count, (unsigned long long)cnt[b]);
+                    atomicMin((unsigned long long*)&sl->first, (unsigned long long)ord[b]);
+                    atomicMax(&sl->last_tag, tag[b]);
+                }
+                pend[b] = false;
+            } else {
+                h[b] = (u32)((h[b] + 1ull) & T.mask);
+            }
+        }
+    }
 #pragma unroll
     for (int b = 0; b < B; ++b) {
-        if (!valid[b]) continue;
-        const u64 k = ((u64)w0[b].y << 32) | w0[b].x;
-        if (k == key[b]) {
-            GSlot* sl = &T.slots[h[b]];
-            atomicAdd((unsigned long long*)&sl->count, (unsigned long long)cnt[b]);
-            const u64 first = ((u64)w1[b].y << 32) | w1[b].x;
-            if (ord[b] < first) atomicMin((unsigned long long*)&sl->first, (unsigned long long)ord[b]);
-            if (w1[b].z < tag[b]) atomicMax(&sl->last_tag, tag[b]);
+        if (!pend[b]) continue;  // probe bound exceeded: the overflow list
+        const u64 i = atomicAdd((unsigned long long*)&st->n_overflow, 1ull);
+        if (i < T.ovf_cap) {
+            Overflow o;
+            o.key = key[b];
+            o.count = cnt[b];
+            o.first = ord[b];
+            o.tag = tag[b];
+            o.pad = 0;
+            T.ovf[i] = o;
         } else {
-            made += global_insert(T, st, key[b], cnt[b], ord[b], tag[b]) ? 1u : 0u;
+            atomicOr(&st->cap_flags, 2u);
         }
     }
     return made;
 }
 
-__global__ __launch_bounds__(256) void log_reduce_kernel(Table t, DevState* st, const LogEntry* sorted,
-                                                         const u32* hist, const u32* offs) {
+// pass 4: each bucket's rows aggregated in LDS (records summed, min offset), then its distinct codes
+// inserted into the HBM table with the launch's ordinal base and file tag.  Persistent grid over the
+// buckets.
+__global__ __launch_bounds__(256) void log_reduce_kernel(Table t, DevState* st, const LogEntry* sorted, AggScratch g,
+                                                         u32 file_tag, u64 ord0, u32 ablate) {
+    if (st->log_n == 0) return;
     __shared__ AggSlot ls[AGG_LNS];
-    for (int i = threadIdx.x; i < AGG_LNS; i += 256) ls[i] = AggSlot{0, ~0ull, 0, 0};
-    __syncthreads();
-    const u64 last = (u64)blockIdx.x * AGG_SLICES + AGG_SLICES - 1;
-    const u64 lo = offs[(u64)blockIdx.x * AGG_SLICES], hi = (u64)offs[last] + hist[last];
     u32 made = 0;
-    for (u64 i = lo + threadIdx.x; i < hi; i += 256) {
-        const LogEntry e = sorted[i];
-        u32 h = (u32)mix64(e.key) & (AGG_LNS - 1);
-        bool done = false;
-        for (int pr = 0; pr < AGG_PROBE && !done; ++pr) {
-            u64 k = ls[h].key;
-            if (k == 0) {
-                const u64 old = atomicCAS((unsigned long long*)&ls[h].key, 0ull, (unsigned long long)e.key);
-                k = old == 0 ? e.key : old;
-            }
-            if (k == e.key) {
-                atomicAdd(&ls[h].cnt, e.cnt);
-                atomicMin((unsigned long long*)&ls[h].first, (unsigned long long)e.ord);
-                atomicMax(&ls[h].tag, e.tag);
-                done = true;
-            }
-            h = (h + 1) & (AGG_LNS - 1);
-        }
-        if (!done) made += global_insert(t, st, e.key, e.cnt, e.ord, e.tag) ? 1u : 0u;  // a full bucket table
-    }
+    for (int i = threadIdx.x; i < AGG_LNS; i += 256) ls[i] = AggSlot{0, 0xFFFFFFFFu, 0};
     __syncthreads();
-    for (int i0 = threadIdx.x; i0 < AGG_LNS; i0 += 4 * 256) {
-        u64 key[4], cnt[4], ord[4];
-        u32 tag[4];
-        bool v[4];
+    for (u32 bk = blockIdx.x; bk < (u32)AGG_NB; bk += gridDim.x) {
+        const u64 lo = g.base[bk], hi = bk + 1 < (u32)AGG_NB ? (u64)g.base[bk + 1] : (u64)g.cur[bk];
+        if (lo == hi) continue;  // uniform: nothing logged for this bucket (its LDS table is still clean)
+        // four rows per thread in flight per step (a step's loads are independent of its LDS work)
+        for (u64 i0 = lo + threadIdx.x; i0 < ((ablate & 512u) ? lo : hi); i0 += 4 * 256) {  // 512: timing ablation
+            LogEntry ev[4];
 #pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            const int i = i0 + b * 256;
-            const AggSlot e = i < AGG_LNS ? ls[i] : AggSlot{0, 0, 0, 0};
-            v[b] = e.key != 0;
-            key[b] = e.key;
-            cnt[b] = e.cnt;
-            ord[b] = e.first;
-            tag[b] = e.tag;
+            for (int q = 0; q < 4; ++q) {
+                const u64 i = i0 + (u64)q * 256;
+                ev[q] = i < hi ? sorted[i] : LogEntry{0, 0, 0};
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const LogEntry e = ev[q];
+                if (!e.key) continue;
+                u32 h = (u32)mix64(e.key) & (AGG_LNS - 1);
+                bool done = false;
+                for (int pr = 0; pr < AGG_PROBE && !done; ++pr) {
+                    u64 k = ls[h].key;
+                    if (k == 0) {
+                        const u64 old = atomicCAS((unsigned long long*)&ls[h].key, 0ull, (unsigned long long)e.key);
+                        k = old == 0 ? e.key : old;
+                    }
+                    if (k == e.key) {
+                        atomicAdd(&ls[h].cnt, e.cnt);
+                        if (e.off < ls[h].mino) atomicMin(&ls[h].mino, e.off);
+                        done = true;
+                    }
+                    h = (h + 1) & (AGG_LNS - 1);
+                }
+                if (!done) {  // a full bucket table: this row goes in on its own
+                    const u64 key1[1] = {e.key};
+                    const u32 cnt1[1] = {e.cnt};
+                    const u64 ord1[1] = {ord0 + e.off};
+                    const u32 tag1[1] = {file_tag};
+                    const bool v1[1] = {true};
+                    made += insert_rows<1>(t, st, key1, cnt1, ord1, tag1, v1);
+                }
+            }
         }
-        made += insert_batch<4>(t, st, key, cnt, ord, tag, v);
+        __syncthreads();
+        for (int i0 = threadIdx.x; i0 < ((ablate & 256u) ? 0 : AGG_LNS); i0 += 4 * 256) {  // 256: timing ablation
+            u64 key[4], ord[4];
+            u32 cnt[4], tag[4];
+            bool v[4];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int i = i0 + b * 256;
+                const AggSlot e = i < AGG_LNS ? ls[i] : AggSlot{0, 0, 0};
+                v[b] = e.key != 0;
+                key[b] = e.key;
+                cnt[b] = e.cnt;
+                ord[b] = ord0 + e.mino;
+                tag[b] = file_tag;
+            }
+            made += insert_rows<4, true>(t, st, key, cnt, ord, tag, v);
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < AGG_LNS; i += 256) ls[i] = AggSlot{0, 0xFFFFFFFFu, 0};
+        __syncthreads();
     }
     add_created(st, made);
 }
 
-size_t log_aggregate_temp_bytes() {
-    size_t tb = 0;
-    (void)rocprim::exclusive_scan(nullptr, tb, (const u32*)nullptr, (u32*)nullptr, 0u,
-                                  (size_t)AGG_NB * AGG_SLICES, rocprim::plus<u32>(), (hipStream_t)0);
-    return tb;
-}
+size_t log_aggregate_temp_bytes() { return 0; }
 
-hipError_t launch_log_aggregate(Table t, DevState* st, LogEntry* log, LogEntry* sorted, u64 cap, u32* hist,
-                                void* temp, size_t temp_bytes, hipStream_t s) {
-    u32* offs = hist + (size_t)AGG_NB * AGG_SLICES;
-    hipLaunchKernelGGL(log_hist_kernel, dim3(AGG_SLICES), dim3(256), 0, s, log, st, cap, hist);
-    hipError_t e = rocprim::exclusive_scan(temp, temp_bytes, hist, offs, 0u, (size_t)AGG_NB * AGG_SLICES,
-                                           rocprim::plus<u32>(), s);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(log_scatter_kernel, dim3(AGG_SLICES), dim3(256), 0, s, log, st, cap, offs, sorted);
-    hipLaunchKernelGGL(log_reduce_kernel, dim3(AGG_NB), dim3(256), 0, s, t, st, sorted, hist, offs);
-    e = hipGetLastError();
+hipError_t launch_log_aggregate(Table t, DevState* st, LogEntry* log, LogEntry* sorted, u64 cap, u32* hist, u32 file_tag,
+                                u64 file_offset, u32 ablate, hipStream_t s) {
+    const AggScratch g = AggScratch::at(hist);
+    // every pass reads log_n on the device and returns at once when no commit logged (the usual case
+    // for low-cardinality runs: only commits past ScanArgs::log_min pairs per 16 tiles log)
+    hipLaunchKernelGGL(log_count_kernel, dim3(AGG_SLICES), dim3(256), 0, s, log, st, cap, g);
+    hipLaunchKernelGGL(log_base_kernel, dim3(1), dim3(1024), 0, s, st, g);
+    hipLaunchKernelGGL(log_scatter_kernel, dim3(AGG_SLICES), dim3(256), 0, s, log, st, cap, g, sorted);
+    const u64 ord0 = ((u64)file_tag << ORD_SHIFT) | file_offset;
+    static const int rgrid = getenv("FR_AGG_GRID") ? atoi(getenv("FR_AGG_GRID")) : 1024;
+    hipLaunchKernelGGL(log_reduce_kernel, dim3(rgrid), dim3(256), 0, s, t, st, sorted, g, file_tag, ord0, ablate);
+    const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     return hipMemsetAsync(&st->log_n, 0, sizeof(u64), s);
 }

@@ -162,6 +162,28 @@ def test_speculative_commit_replay(lib):
         c.close()
 
 
+@pytest.mark.parametrize("log_min", ["0", "150", "100000000"])
+def test_launch_log_commits(lib, monkeypatch, log_min):
+    """Commits of at least FR_LOG_MIN pairs go to the launch log and are aggregated after the launch
+    (count / scatter / LDS reduce / round-based table inserts); smaller ones insert directly.  Every
+    commit logged (0), a mix (150: these 1-tile chunks commit ~100-250 pairs), and none must give the
+    oracle's tally, including a table that has to grow between launches."""
+    from frender_amd import synth
+    monkeypatch.setenv("FR_LOG_MIN", log_min)
+    rng = random.Random(int(log_min) + 7)
+    sheet = synth.make_sheet(384, 10, 10)
+    files = [synth.generate_bytes(sheet, 0, 300000, R=8, seed=3), random_fastq(rng, 20000, blank_seq=True),
+             synth.generate_bytes(sheet, 300000, 5000, R=8, seed=3)]
+    exp = oracle_tally(files)
+    for mode, slots in (("device", 1 << 12), ("host", 1 << 20)):
+        c = lib.Context(device=0, chunk_bytes=1 << 22, table_slots=slots)
+        try:
+            assert_same(gpu_tally(c, lib, files, mode=mode, pieces=lambda r: r.choice([4096, 1 << 20, 1 << 23]),
+                                  rng=rng), exp)
+        finally:
+            c.close()
+
+
 def test_table_growth_and_overflow(lib):
     """Start from a 1024-slot table with ~60k distinct codes: the table must grow
     between launches (overflow list absorbs in-flight inserts) and stay exact."""

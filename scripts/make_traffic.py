@@ -4,7 +4,7 @@ Reads gpurun_out/prof_trace (kernel-trace --stats) and gpurun_out/prof_fetch / p
 (--pmc FETCH_SIZE / --pmc WRITE_SIZE, separate runs), writes
   profiles/<tag>_kernel_stats.csv       the --stats summary
   profiles/<tag>_pmc_<kernel>.csv       per-dispatch FETCH_SIZE / WRITE_SIZE rows of the kernel
-  profiles/traffic_r01.json             HBM bytes per launch, corrected per MI355X_MICROARCH.md:
+  profiles/traffic_r02.json             HBM bytes per launch, corrected per MI355X_MICROARCH.md:
                                         FETCH_SIZE counts 1/2 of 16-B/lane streaming reads on
                                         gfx950 (x2), both counters in KiB.
 usage: python scripts/make_traffic.py <tag> [reads] [read_len] [launches_per_step]
@@ -56,7 +56,7 @@ def main():
     wkb = sum(write.values()) / len(write)
     alg = reads * reclen / launches
     out = {
-        "round": 1,
+        "round": int(os.environ.get("ROUND", "2")),
         "kernel": KERNEL,
         "reads": reads,
         "read_len": read_len,
@@ -71,7 +71,7 @@ def main():
         "source": f"profiles/{tag}_pmc_chunk_kernel.csv (rocprofv3 --pmc FETCH_SIZE, then --pmc WRITE_SIZE, "
                   f"separate runs of bench.py --steps 5 --warmup 1 --no-cpu)",
     }
-    with open(os.path.join(prof, "traffic_r01.json"), "w") as fh:
+    with open(os.path.join(prof, os.environ.get("TRAFFIC_JSON", "traffic_r02.json")), "w") as fh:
         json.dump(out, fh, indent=1)
     print(json.dumps(out, indent=1))
 

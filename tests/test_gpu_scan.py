@@ -143,10 +143,14 @@ def test_no_trailing_newline_and_truncated(ctx, lib):
         assert_same(gpu_tally(ctx, lib, files, mode=mode), oracle_tally(files))
 
 
-def test_speculative_commit_replay(lib):
+@pytest.mark.parametrize("log_min", [None, "0"])
+def test_speculative_commit_replay(lib, monkeypatch, log_min):
     """A file whose chunks look like 4-line FASTQ one line off the true phase: every chunk after
     the first guesses the wrong line phase, commits at once, the launch-end check catches it and
-    the feed is replayed with every chunk waiting for its exact prefix (fr_feed_device)."""
+    the feed is replayed with every chunk waiting for its exact prefix (fr_feed_device).  With
+    FR_LOG_MIN=0 the failed attempt's commits went through the launch log and its aggregation."""
+    if log_min is not None:
+        monkeypatch.setenv("FR_LOG_MIN", log_min)
     recs = ["L 1:N:0:AAAA+CCCC\n"] + [f"@r{i} 1:N:0:ACGT+ACGT\nACGT\n+\nA AC\n" for i in range(60000)]
     data = "".join(recs).encode()
     exp = oracle_tally([data])

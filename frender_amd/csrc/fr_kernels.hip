@@ -122,8 +122,15 @@ __device__ __forceinline__ u64 wave_sum_u64(u64 v) {
 // load only ever over-estimates `first` / under-estimates `last_tag`, so skipping is safe).
 // Returns true when this call created the slot.  No global counters are touched here.
 // ------------------------------------------------------------------------------------
+// Home slot of a key: the TOP bits of mix64(key).  The launch-log buckets (log_bucket) are its top
+// AGG_LOG_NB bits too, so for tables of >= AGG_NB slots each bucket owns one contiguous slot region and
+// log_reduce_kernel's inserts stay inside it (DRAM-page and L2 locality instead of random lines).
+__device__ __forceinline__ u64 table_home(u64 key, u64 mask) {
+    return mask ? mix64(key) >> __builtin_clzll(mask) : 0ull;
+}
+
 __device__ bool global_insert(const Table& T, DevState* st, u64 key, u64 cnt, u64 ord, u32 tag) {
-    u64 h = mix64(key) & T.mask;
+    u64 h = table_home(key, T.mask);
     for (int probe = 0; probe < GPROBE; ++probe) {
         GSlot* s = &T.slots[h];
         const uint4 w0 = *(const uint4*)s;
@@ -804,7 +811,7 @@ __device__ __forceinline__ u32 insert_many(const ScanArgs& a, const u64 (&key)[B
     u64 h[B];
 #pragma unroll
     for (int b = 0; b < B; ++b) {
-        h[b] = mix64(key[b]) & T.mask;
+        h[b] = table_home(key[b], T.mask);
         if (valid[b]) {
             const GSlot* sl = &T.slots[h[b]];
             w0[b] = *(const uint4*)sl;
@@ -854,7 +861,7 @@ __device__ __forceinline__ u32 insert_rounds(const ScanArgs& a, const u64 (&key)
     bool pend[B];
 #pragma unroll
     for (int b = 0; b < B; ++b) {
-        h[b] = (u32)(mix64(key[b]) & mask);
+        h[b] = (u32)table_home(key[b], mask);
         pend[b] = valid[b];
     }
     u32 made = 0;
@@ -1880,7 +1887,7 @@ __global__ void rehash_kernel(Table t, const GSlot* src, u64 nsrc) {
     for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i < nsrc; i += (u64)gridDim.x * blockDim.x) {
         const GSlot g = src[i];
         if (!g.key) continue;
-        u64 h = mix64(g.key) & t.mask;
+        u64 h = table_home(g.key, t.mask);
         for (;;) {
             const u64 old = atomicCAS((unsigned long long*)&t.slots[h].key, 0ull, (unsigned long long)g.key);
             if (old == 0) {
@@ -1909,11 +1916,9 @@ hipError_t launch_rehash(Table dst, DevState* st, const GSlot* src, u64 nsrc, hi
 // and only the distinct codes reach the HBM table -- batched, with every slot load in flight at
 // once and nothing else competing for the memory system.
 // ------------------------------------------------------------------------------------
-// bucket of a logged code: the top bits of a multiplicative hash of the key folded to 32 bits (the
-// LDS table of log_reduce_kernel indexes by mix64's low bits, independent of these)
-__device__ __forceinline__ u32 log_bucket(u64 key) {
-    return (((u32)key ^ (u32)(key >> 29)) * 0x9E3779B1u) >> (32 - AGG_LOG_NB);
-}
+// bucket of a logged code: the top bits of mix64, as the table's home slot (table_home); the LDS table
+// of log_reduce_kernel indexes by mix64's low bits, independent of these
+__device__ __forceinline__ u32 log_bucket(u64 key) { return (u32)(mix64(key) >> (64 - AGG_LOG_NB)); }
 
 __device__ __forceinline__ void log_slice(u64 n, u32 s, u64& lo, u64& hi) {
     const u64 per = (n + AGG_SLICES - 1) / AGG_SLICES;
@@ -2050,7 +2055,7 @@ __device__ __forceinline__ u32 insert_rows(const Table& T, DevState* st, const u
     bool pend[B];
 #pragma unroll
     for (int b = 0; b < B; ++b) {
-        h[b] = (u32)(mix64(key[b]) & T.mask);
+        h[b] = (u32)table_home(key[b], T.mask);
         pend[b] = valid[b];
     }
     u32 made = 0;
@@ -2326,7 +2331,7 @@ hipError_t launch_gather(const u32* perm, u64 n, const u64* keys, const u64* cou
 }
 
 __device__ __forceinline__ const GSlot* table_find(const GSlot* slots, u64 mask, u64 key) {
-    u64 h = mix64(key) & mask;
+    u64 h = table_home(key, mask);
     for (u64 probe = 0; probe <= mask; ++probe) {
         const GSlot* s = &slots[h];
         if (s->key == key) return s;
@@ -2426,6 +2431,9 @@ __device__ __forceinline__ int mism(u64 q, u64 s) {  // Hamming distance of two 
 }
 
 constexpr int CLS_WG = 256;
+#ifndef FR_CLS_SCALAR
+#define FR_CLS_SCALAR 1  // sheet rows by scalar loads from HBM (class_pair_s), not broadcast from LDS
+#endif
 constexpr int CLS_LDS_BYTES = 48 * 1024;  // dynamic LDS cap: sheet images + per-name rc sums
 
 __device__ __forceinline__ int mism32(u32 q, u32 s) {  // <= 10 symbols: 30 bits
@@ -2458,6 +2466,54 @@ __device__ __forceinline__ void class_pair(W q1, W q2, const W* s1, const W* s2,
         both += (a && b) ? 1 : 0;
         if (rc) {
             const bool c = mism_w<W>(q2, s2rc[i]) <= nsubs;
+            rm2 = (c && rm2 < 0) ? i : rm2;
+            rr = (a && c && rboth == 0) ? i : rr;
+            rboth += (a && c) ? 1 : 0;
+        }
+    }
+    if (m1 >= 0 && m2 >= 0) {
+        cls = both == 0 ? CLS_HOP : both == 1 ? CLS_DEMUX : CLS_AMBIG;
+        row = both == 1 ? r : -1;
+    } else {
+        cls = CLS_UNDET;
+        row = -1;
+    }
+    if (m1 >= 0 && rm2 >= 0) {
+        rcls = rboth == 0 ? CLS_HOP : rboth == 1 ? CLS_DEMUX : CLS_AMBIG;
+        rrow = rboth == 1 ? rr : -1;
+    } else {
+        rcls = CLS_UNDET;
+        rm2 = -1;
+        rrow = -1;
+    }
+    if (cls == CLS_UNDET) {
+        m1 = -1;
+        m2 = -1;
+    }
+}
+
+// class_pair with the rows read straight from the u64 sheet arrays in HBM:
+// the row index is uniform, so every row arrives by scalar loads and the distance ops take it as a
+// scalar operand (no LDS read per row), and the bookkeeping runs only on rows some lane matches
+// (a code matches one or two rows of a well-separated sheet: the wave skips ~2/3 of the updates).
+template <typename W, bool RC>
+__device__ __forceinline__ void class_pair_s(W q1, W q2, const u64* __restrict__ s1, const u64* __restrict__ s2,
+                                             const u64* __restrict__ s2rc, int S, int nsubs, int& m1, int& m2,
+                                             int& cls, int& row, int& rm2, int& rcls, int& rrow) {
+    m1 = -1;
+    m2 = -1;
+    rm2 = -1;
+    int both = 0, r = -1, rboth = 0, rr = -1;
+#pragma unroll 8
+    for (int i = 0; i < S; ++i) {
+        const bool a = mism_w<W>(q1, (W)s1[i]) <= nsubs;
+        const bool b = mism_w<W>(q2, (W)s2[i]) <= nsubs;
+        const bool c = RC && mism_w<W>(q2, (W)s2rc[i]) <= nsubs;
+        if (a || b || c) {
+            m1 = (a && m1 < 0) ? i : m1;
+            m2 = (b && m2 < 0) ? i : m2;
+            r = (a && b && both == 0) ? i : r;
+            both += (a && b) ? 1 : 0;
             rm2 = (c && rm2 < 0) ? i : rm2;
             rr = (a && c && rboth == 0) ? i : rr;
             rboth += (a && c) ? 1 : 0;
@@ -2570,7 +2626,14 @@ __global__ __launch_bounds__(CLS_WG) void classify_kernel(const u64* keys, const
             if (sh.S > 0 && (sh.L1u == -2 || sh.L1u != n1)) err = 1;
             else if (sh.S > 0 && (sh.L2u == -2 || sh.L2u != n2)) err = 2;
             else {
-                class_pair<W>((W)q1, (W)q2, S1, S2, S2rc, sh.S, nsubs, rc != 0, m1, m2, cls, row, rm2, rcls, rrow);
+                if (FR_CLS_SCALAR && rc)
+                    class_pair_s<W, true>((W)q1, (W)q2, sh.i1, sh.i2, sh.i2rc, sh.S, nsubs, m1, m2, cls, row, rm2,
+                                          rcls, rrow);
+                else if (FR_CLS_SCALAR)
+                    class_pair_s<W, false>((W)q1, (W)q2, sh.i1, sh.i2, sh.i2rc, sh.S, nsubs, m1, m2, cls, row, rm2,
+                                           rcls, rrow);
+                else
+                    class_pair<W>((W)q1, (W)q2, S1, S2, S2rc, sh.S, nsubs, rc != 0, m1, m2, cls, row, rm2, rcls, rrow);
                 // both calls demuxable to different sample NAMES -> ambiguous (frender.py:336-349)
                 if (rc && cls == CLS_DEMUX && rcls == CLS_DEMUX && sh.name[row] != sh.name[rrow]) {
                     cls = CLS_AMBIG;
@@ -2627,9 +2690,10 @@ hipError_t launch_classify(const u64* keys, const u64* counts, u64 n, SheetArgs 
     const size_t sheet_bytes = 3 * wb * (size_t)std::max(sh.S, 0);
     const int names_in_lds = (rc && names_bytes <= CLS_LDS_BYTES / 2) ? 1 : 0;
     const size_t nb = names_in_lds ? names_bytes : 0;
-    const int sheet_in_lds = (nb + sheet_bytes <= CLS_LDS_BYTES) ? 1 : 0;
+    // the scalar-load path (FR_CLS_SCALAR) reads the rows from HBM; only the name sums use LDS then
+    const int sheet_in_lds = (!FR_CLS_SCALAR && nb + sheet_bytes <= CLS_LDS_BYTES) ? 1 : 0;
     const size_t lds = nb + (sheet_in_lds ? sheet_bytes : 0) + 16;
-    if (narrow && sheet_in_lds)
+    if (narrow && (sheet_in_lds || FR_CLS_SCALAR))
         hipLaunchKernelGGL(classify_kernel<u32>, dim3((u32)grid), dim3(CLS_WG), lds, s, keys, counts, n, sh, nsubs, rc,
                            o, sheet_in_lds, names_in_lds);
     else

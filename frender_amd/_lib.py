@@ -305,10 +305,10 @@ class Demux:
                  "fr_dmx_route")
         return fe.value, ev.value, b1, b2
 
-    def fetch(self, mate: int, nbytes: int) -> bytes:
+    def fetch(self, mate: int, nbytes: int) -> np.ndarray:
         out = np.empty(nbytes, np.uint8)
         self._ck(lib.fr_dmx_fetch(self.h, mate, _ptr(out), nbytes), "fr_dmx_fetch")
-        return out.tobytes()
+        return out
 
 
 class Context:

@@ -47,12 +47,95 @@ def parse_results_file(result_file) -> dict:
         return {line[0] + "+" + line[1]: (line[ti], line[si]) for line in rd}
 
 
+def _load_libdeflate():
+    """libdeflate (whole-buffer DEFLATE, 2-4x zlib's speed), when the image has it; None otherwise."""
+    import ctypes
+
+    try:
+        ld = ctypes.CDLL("libdeflate.so.0")
+    except OSError:
+        return None
+    ld.libdeflate_alloc_compressor.restype = ctypes.c_void_p
+    ld.libdeflate_alloc_compressor.argtypes = [ctypes.c_int]
+    ld.libdeflate_gzip_compress_bound.restype = ctypes.c_size_t
+    ld.libdeflate_gzip_compress_bound.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    ld.libdeflate_gzip_compress.restype = ctypes.c_size_t
+    ld.libdeflate_gzip_compress.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                            ctypes.c_size_t]
+    return ld
+
+
+_LD = _load_libdeflate()
+_LD_TLS = threading.local()
+
+
+class _GzMembers:
+    """A .fq.gz writer that compresses every write into its own gzip member with libdeflate (ctypes
+    releases the GIL, so the writers of one window compress in parallel threads).  A multi-member
+    gzip file decompresses to the concatenation of its members, which is how gzip.open -- and the
+    reference -- read it; the writes of one file arrive in order (the caller waits for a window's
+    jobs before it submits the next window's).  A file nothing was written to gets one empty member,
+    as gzip.open's writer leaves it."""
+
+    def __init__(self, path: str, level: int):
+        self.f = open(path, "wb")
+        self.level = level
+        self.wrote = False
+
+    def _compressor(self):
+        c = getattr(_LD_TLS, "c", None)
+        if c is None:
+            c = _LD_TLS.c = {}
+        h = c.get(self.level)
+        if h is None:
+            h = c[self.level] = _LD.libdeflate_alloc_compressor(self.level)
+            if not h:
+                raise MemoryError("libdeflate_alloc_compressor")
+        return h
+
+    def write_from(self, arr: np.ndarray, start: int, end: int) -> None:
+        import ctypes
+
+        n = end - start
+        if n <= 0:
+            return
+        comp = self._compressor()
+        bound = _LD.libdeflate_gzip_compress_bound(comp, n)
+        out = np.empty(bound, dtype=np.uint8)
+        k = _LD.libdeflate_gzip_compress(comp, ctypes.c_void_p(arr.ctypes.data + start), n,
+                                         ctypes.c_void_p(out.ctypes.data), bound)
+        if k == 0:
+            raise RuntimeError("libdeflate_gzip_compress: output bound too small")
+        self.f.write(memoryview(out)[:k])
+        self.wrote = True
+
+    def close(self) -> None:
+        if not self.wrote:
+            self.f.write(gzip.compress(b"", compresslevel=self.level))
+        self.f.close()
+
+
+class _GzFile:
+    """gzip.open writer with the same write_from interface (the image has no libdeflate)."""
+
+    def __init__(self, path: str, level: int):
+        self.f = gzip.open(path, "wb", compresslevel=level)
+
+    def write_from(self, arr: np.ndarray, start: int, end: int) -> None:
+        if end > start:
+            self.f.write(memoryview(arr)[start:end])
+
+    def close(self) -> None:
+        self.f.close()
+
+
 def open_files(name, out_dir, infix, level):
     """frender.py:667-676."""
     if not out_dir.endswith("/"):
         out_dir += "/"
-    return {read: gzip.open(f"{out_dir}{name}_frender-demux_{infix + '_' if infix else ''}{read}.fq.gz", "wb",
-                            compresslevel=level) for read in ("R1", "R2")}
+    kind = _GzMembers if _LD is not None and os.environ.get("FR_DEMUX_ZLIB", "0") == "0" else _GzFile
+    return {read: kind(f"{out_dir}{name}_frender-demux_{infix + '_' if infix else ''}{read}.fq.gz", level)
+            for read in ("R1", "R2")}
 
 
 _MATE_TAG = re.compile("_R([12])_")
@@ -180,9 +263,9 @@ def _demux_pair(dmx, pool, read1_file, read2_file, results, route_of, writers, w
             pending = []
             for k, w in enumerate(writers):
                 if b1[k]:
-                    pending.append(pool.submit(w["R1"].write, memoryview(o1)[c1[k]:c1[k + 1]]))
+                    pending.append(pool.submit(w["R1"].write_from, o1, int(c1[k]), int(c1[k + 1])))
                 if b2[k]:
-                    pending.append(pool.submit(w["R2"].write, memoryview(o2)[c2[k]:c2[k + 1]]))
+                    pending.append(pool.submit(w["R2"].write_from, o2, int(c2[k]), int(c2[k + 1])))
             # carry the bytes after the routed records
             cut = []
             for m in (0, 1):

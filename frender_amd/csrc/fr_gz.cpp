@@ -22,6 +22,7 @@
 #include <zlib.h>
 
 #include <algorithm>
+#include <atomic>
 #include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
@@ -87,6 +88,73 @@ const Libdeflate* libdeflate() {
 
 constexpr size_t LD_MAX_IN = 256ull << 20;   // compressed bytes a file may have for the fast path
 constexpr size_t LD_MAX_OUT = 1ull << 30;    // decoded bytes it may produce
+constexpr size_t BGZF_MAX_IN = 1ull << 30;   // BGZF files: compressed bytes for the parallel path
+
+struct Member {
+    size_t off, len, dst, isize;
+};
+
+inline uint32_t le16(const uint8_t* p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8); }
+inline uint32_t le32(const uint8_t* p) { return le16(p) | (le16(p + 2) << 16); }
+
+// BGZF: every member carries its own compressed length in a 'BC' extra subfield (BSIZE + 1 bytes)
+// and its decoded length in the trailer, so the members of one file are found by walking headers
+// alone and decode independently.  True with the member list when the whole file is such members
+// (NUL padding at the end allowed); anything else is not BGZF.
+bool bgzf_members(const std::vector<uint8_t>& in, std::vector<Member>& ms) {
+    const size_t n = in.size();
+    size_t pos = 0, dst = 0;
+    ms.clear();
+    while (pos < n) {
+        if (in[pos] == 0) {  // trailing NUL padding only
+            while (pos < n && in[pos] == 0) ++pos;
+            if (pos != n) return false;
+            break;
+        }
+        if (n - pos < 18 || in[pos] != 0x1f || in[pos + 1] != 0x8b || in[pos + 2] != 8 || !(in[pos + 3] & 4))
+            return false;
+        const size_t xlen = le16(&in[pos + 10]);
+        if (n - pos < 12 + xlen) return false;
+        size_t bsize = 0;
+        for (size_t q = pos + 12; q + 4 <= pos + 12 + xlen;) {
+            const size_t slen = le16(&in[q + 2]);
+            if (in[q] == 'B' && in[q + 1] == 'C' && slen == 2) bsize = le16(&in[q + 4]) + 1;
+            q += 4 + slen;
+        }
+        if (bsize < 12 + xlen + 8 || n - pos < bsize) return false;
+        const size_t isize = le32(&in[pos + bsize - 4]);
+        ms.push_back(Member{pos, bsize, dst, isize});
+        dst += isize;
+        pos += bsize;
+    }
+    return !ms.empty();
+}
+
+// decode BGZF members in parallel (`threads` helpers, each with its own decompressor) into out
+bool bgzf_decode(const Libdeflate* ld, const std::vector<uint8_t>& in, const std::vector<Member>& ms,
+                 std::vector<uint8_t>& out, int threads) {
+    std::atomic<size_t> next{0};
+    std::atomic<bool> ok{true};
+    auto run = [&]() {
+        void* d = ld->alloc();
+        if (!d) {
+            ok = false;
+            return;
+        }
+        for (size_t k; ok && (k = next.fetch_add(1)) < ms.size();) {
+            const Member& m = ms[k];
+            size_t used = 0, produced = 0;
+            const int r = ld->gzip_ex(d, in.data() + m.off, m.len, out.data() + m.dst, m.isize, &used, &produced);
+            if (r != 0 || used != m.len || produced != m.isize) ok = false;
+        }
+        ld->release(d);
+    };
+    std::vector<std::thread> helpers;
+    for (int t = 1; t < threads; ++t) helpers.emplace_back(run);
+    run();
+    for (auto& h : helpers) h.join();
+    return ok;
+}
 
 // the libdeflate fast path: true when the whole file was decoded and queued (or the scan cancelled
 // it); false leaves nothing queued and the zlib stream takes the file from its start
@@ -94,7 +162,7 @@ bool inflate_whole(fr_gz* g, GzFile& f) {
     const Libdeflate* ld = libdeflate();
     if (!ld) return false;
     struct stat sb;
-    if (stat(f.path.c_str(), &sb) != 0 || (size_t)sb.st_size > LD_MAX_IN) return false;
+    if (stat(f.path.c_str(), &sb) != 0 || (size_t)sb.st_size > std::max(LD_MAX_IN, BGZF_MAX_IN)) return false;
     const size_t n = (size_t)sb.st_size;
     std::vector<uint8_t> in(n);
     FILE* fp = fopen(f.path.c_str(), "rb");
@@ -102,6 +170,17 @@ bool inflate_whole(fr_gz* g, GzFile& f) {
     const size_t got = n ? fread(in.data(), 1, n, fp) : 0;
     fclose(fp);
     if (got != n) return false;
+    std::vector<Member> ms;
+    if (bgzf_members(in, ms)) {  // members split across the pool's thread count
+        std::vector<uint8_t> out(ms.back().dst + ms.back().isize);
+        if (!bgzf_decode(ld, in, ms, out, g->threads)) return false;
+        std::unique_lock<std::mutex> lk(g->m);
+        if (f.cancel || g->stop) return true;
+        if (!out.empty()) f.q.push_back(std::move(out));
+        g->cv.notify_all();
+        return true;
+    }
+    if (n > LD_MAX_IN) return false;
     void* d = ld->alloc();
     if (!d) return false;
     std::vector<uint8_t> out(std::min(LD_MAX_OUT, std::max<size_t>(4 * n, 1u << 20)));

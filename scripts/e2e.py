@@ -56,10 +56,33 @@ def host_feed(n, R=8, piece=64 << 20):
             "M_reads_per_s": round(n / dt / 1e6, 1), "GB_per_s": round(n * reclen / dt / 1e9, 2)}
 
 
-def gz_scan(n, files=4, cores=None):
+def _bgzf(data: bytes, block: int = 65280, level: int = 1) -> bytes:
+    import struct
+    import zlib
+    out = []
+    for i in range(0, len(data), block):
+        chunk = data[i:i + block]
+        c = zlib.compressobj(level, zlib.DEFLATED, -15)
+        body = c.compress(chunk) + c.flush()
+        bsize = 18 + len(body) + 8
+        out.append(b"\x1f\x8b\x08\x04" + b"\x00" * 4 + b"\x00\xff" + struct.pack("<HBBHH", 6, 66, 67, 2, bsize - 1)
+                   + body + struct.pack("<II", zlib.crc32(chunk), len(chunk)))
+    out.append(bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000"))
+    return b"".join(out)
+
+
+def gz_scan(n, files=4, cores=None, bgzf=False):
     sheet = synth.make_sheet(96, 8, 8)
     with tempfile.TemporaryDirectory() as d:
-        paths = synth.make_dataset(d, sheet, n, n_files=files, R=8, seed=1, level=1)
+        if bgzf:  # BGZF members: the native inflate splits each file across threads
+            paths = []
+            for f in range(files):
+                p = os.path.join(d, f"syn_L{f + 1:03d}_R1_001.fastq.gz")
+                with open(p, "wb") as fh:
+                    fh.write(_bgzf(synth.generate_bytes(sheet, f * (n // files), n // files, R=8, seed=1)))
+                paths.append(p)
+        else:
+            paths = synth.make_dataset(d, sheet, n, n_files=files, R=8, seed=1, level=1)
         sheet_csv = os.path.join(d, "sheet.csv")
         with open(sheet_csv, "w") as f:
             f.write("Sample_ID,index,index2\n")
@@ -75,8 +98,8 @@ def gz_scan(n, files=4, cores=None):
             dt = time.perf_counter() - t0
         finally:
             os.chdir(cwd)
-    return {"path": "gz_scan", "reads": n, "files": files, "inflate_threads": cores, "s": round(dt, 3),
-            "M_reads_per_s": round(n / dt / 1e6, 3)}
+    return {"path": "gz_scan" + ("_bgzf" if bgzf else ""), "reads": n, "files": files, "inflate_threads": cores,
+            "s": round(dt, 3), "M_reads_per_s": round(n / dt / 1e6, 3)}
 
 
 def gz_demux(n, files=2, level=9):
@@ -137,6 +160,8 @@ if __name__ == "__main__":
         print(json.dumps(gz_scan(gzn)), flush=True)
         print(json.dumps(gz_scan(2 * gzn, files=8)), flush=True)
         print(json.dumps(gz_scan(gzn, files=16)), flush=True)
+        print(json.dumps(gz_scan(gzn, files=4, bgzf=True)), flush=True)
+        print(json.dumps(gz_scan(2 * gzn, files=1, cores=16, bgzf=True)), flush=True)
     dmn = int(sys.argv[3]) if len(sys.argv) > 3 else 2_000_000
     if dmn:
         for lvl in (9, 1):

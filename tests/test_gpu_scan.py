@@ -649,3 +649,65 @@ def test_byte_shards_merge_to_whole_file(lib):
     finally:
         for c in [whole, merged] + shards:
             c.close()
+
+
+def bgzf(data: bytes, block: int = 65280, pad: int = 0) -> bytes:
+    """BGZF: independent gzip members of <= 64 KiB input, each with a 'BC' extra subfield holding
+    its compressed size - 1, then the empty EOF member (and optional NUL padding)."""
+    import struct
+    import zlib
+    out = []
+    for i in range(0, len(data), block):
+        chunk = data[i:i + block]
+        c = zlib.compressobj(6, zlib.DEFLATED, -15)
+        body = c.compress(chunk) + c.flush()
+        bsize = 18 + len(body) + 8
+        out.append(b"\x1f\x8b\x08\x04" + b"\x00" * 4 + b"\x00\xff" + struct.pack("<HBBHH", 6, 66, 67, 2, bsize - 1)
+                   + body + struct.pack("<II", zlib.crc32(chunk), len(chunk) & 0xFFFFFFFF))
+    out.append(bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000"))  # EOF member
+    return b"".join(out) + b"\x00" * pad
+
+
+@pytest.mark.parametrize("corrupt", [False, True])
+def test_bgzf_scan_matches_oracle(tmp_path, corrupt):
+    """BGZF inputs decode member-parallel in the native inflate (fr_gz.cpp): the scan's CSVs equal
+    the oracle's (Python gzip reads BGZF as multi-member gzip, as the reference does); a member with
+    a bad CRC fails with the reference's exception."""
+    import argparse
+    import contextlib
+    import io
+    import os
+
+    from frender_amd import scan, synth
+    from oracle import frender_oracle
+
+    sheet = synth.make_sheet(24, 8, 8, seed=5)
+    sheet.write_csv(str(tmp_path / "sheet.csv"))
+    files = []
+    for f in range(3):
+        raw = synth.generate_bytes(sheet, f * 120000, 120000, R=8, seed=9)
+        blob = bytearray(bgzf(raw, pad=16 if f == 1 else 0))
+        if corrupt and f == 2:
+            blob[len(blob) // 2] ^= 0x40  # inside a member's deflate data or trailer
+        p = tmp_path / f"syn_L{f + 1:03d}_R1_001.fastq.gz"
+        p.write_bytes(bytes(blob))
+        files.append(str(p))
+    outs = {}
+    for label, fn in (("gpu", scan.frender_scan), ("oracle", frender_oracle.scan)):
+        sub = tmp_path / label
+        sub.mkdir()
+        args = argparse.Namespace(n=1, rc=False, c=3.0, s=None, o="bg", p=None, b=str(tmp_path / "sheet.csv"),
+                                  files=files)
+        cwd = os.getcwd()
+        os.chdir(sub)
+        try:
+            with contextlib.redirect_stdout(io.StringIO()):
+                fn(args)
+            outs[label] = {x: (sub / x).read_bytes() for x in sorted(os.listdir(sub))}
+        except Exception as e:  # noqa: BLE001 - compared below
+            outs[label] = (type(e).__name__, str(e))
+        finally:
+            os.chdir(cwd)
+    assert outs["gpu"] == outs["oracle"]
+    if not corrupt:
+        assert isinstance(outs["gpu"], dict) and outs["gpu"]

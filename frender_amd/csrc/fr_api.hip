@@ -42,6 +42,7 @@ struct fr_ctx {
     DevState* st = nullptr;
     DevState* h_st = nullptr;      // pinned snapshot
     DevState* h_zero = nullptr;    // pinned reset image (zero counters, no error), never modified
+    u8* h_byte = nullptr;          // pinned: a device feed's last byte, copied with the feed's state read
     bool st_fresh = false;         // h_st equals the device state (no device work on it since)
     Table* d_tab = nullptr;        // device copy of tab for the tally kernel
     Table* h_tab = nullptr;        // pinned staging of that copy (last uploaded value)
@@ -128,6 +129,12 @@ struct fr_ctx {
     u64* d_counter = nullptr;
     void* d_temp = nullptr;
     size_t temp_bytes = 0;
+    u32 *d_bins = nullptr, *d_binbase = nullptr;  // first-occurrence bins (fr_finalize)
+    u64 bins_cap = 0;
+    u32* d_arr = nullptr;  // per table slot: arrival index in its bin
+    u64 arr_cap = 0;
+    FinRow* d_rows = nullptr;  // live slots grouped by bin
+    u64 rows_cap = 0;
     u64 n_pres = 0;
     u64 pmap_cap = 0;
     u32 *d_pres_u = nullptr, *d_pres_f = nullptr;
@@ -550,6 +557,7 @@ fr_ctx* fr_create(int device, uint64_t chunk_bytes, uint64_t table_slots) {
     std::memset(ctx->h_tab, 0, sizeof(Table));
     if ((e = hipHostMalloc((void**)&ctx->h_st, sizeof(DevState), hipHostMallocDefault)) != hipSuccess)
         return bad("pinned state", e);
+    if ((e = hipHostMalloc((void**)&ctx->h_byte, 64, hipHostMallocDefault)) != hipSuccess) return bad("pinned byte", e);
     if ((e = hipHostMalloc((void**)&ctx->h_zero, sizeof(DevState), hipHostMallocDefault)) != hipSuccess)
         return bad("pinned reset state", e);
     std::memset(ctx->h_zero, 0, sizeof(DevState));
@@ -594,13 +602,14 @@ void fr_destroy(fr_ctx* ctx) {
     void* dev[] = {ctx->st, ctx->d_tab, ctx->tiles, ctx->tab.slots, ctx->tab.ovf, ctx->tab.pres, ctx->tab.exo_ord,
                    ctx->tab.exo_off, ctx->tab.exo_len, ctx->tab.exo_pool, ctx->dbuf[0], ctx->dbuf[1], ctx->d_sheet,
                    ctx->d_keys, ctx->d_counts, ctx->d_first, ctx->d_keys_s, ctx->d_counts_s,
-                   ctx->d_first_s, ctx->d_pos, ctx->d_perm, ctx->d_rank, ctx->d_counter, ctx->d_temp, ctx->d_pres_u,
+                   ctx->d_first_s, ctx->d_pos, ctx->d_perm, ctx->d_rank, ctx->d_counter, ctx->d_temp, ctx->d_bins, ctx->d_binbase, ctx->d_arr, ctx->d_rows, ctx->d_pres_u,
                    ctx->d_pres_f, ctx->d_m1, ctx->d_m2, ctx->d_row, ctx->d_rm2, ctx->d_rrow, ctx->d_cls, ctx->d_rcls,
                    ctx->d_errw, ctx->d_errf, ctx->d_rcf, ctx->d_rcr, ctx->cold, ctx->rare, ctx->chunk_info, ctx->log, ctx->log_sorted, ctx->log_hist, ctx->log_temp};
     for (void* p : dev)
         if (p) (void)hipFree(p);
     if (ctx->h_st) (void)hipHostFree(ctx->h_st);
     if (ctx->h_zero) (void)hipHostFree(ctx->h_zero);
+    if (ctx->h_byte) (void)hipHostFree(ctx->h_byte);
     if (ctx->h_sheet) (void)hipHostFree(ctx->h_sheet);
     if (ctx->h_tab) (void)hipHostFree(ctx->h_tab);
     for (int i = 0; i < 2; ++i) {
@@ -887,6 +896,8 @@ int fr_feed_device(fr_ctx* ctx, const uint8_t* dev_data, uint64_t len) {
             if (rc) break;
         }
         ctx->spec_commit = 0;
+        // the feed's last byte lands with the state read below (one host round trip for both)
+        if (!rc && len) CK(hipMemcpyAsync(ctx->h_byte, dev_data + len - 1, 1, hipMemcpyDeviceToHost, ctx->stream));
         if (!rc) rc = read_state(ctx);
         if (rc || !spec || attempt == 1 || !ctx->h_st->spec_fail) break;
         // roll back: the table as it was (its size too), the device state, the launch parity
@@ -944,16 +955,7 @@ int fr_feed_device(fr_ctx* ctx, const uint8_t* dev_data, uint64_t len) {
     }
     rc = drain_exotic(ctx);
     if (rc) return rc;
-    if (len) {
-        u8 b = 0;
-        CK(hipMemcpyAsync(&b, dev_data + len - 1, 1, hipMemcpyDeviceToHost, ctx->stream));
-        CK(hipStreamSynchronize(ctx->stream));
-        ctx->last_byte = b;
-        if (ctx->st_pending) {  // the snapshot queued after the last launch has landed
-            ctx->st_pending = false;
-            ctx->st_fresh = true;
-        }
-    }
+    if (len) ctx->last_byte = *ctx->h_byte;  // landed: read_state synchronised after the copy
     ctx->carry.clear();
     return FR_OK;
 }
@@ -1041,39 +1043,92 @@ int fr_finalize(fr_ctx* ctx, uint64_t* n_unique, uint64_t* n_presence, uint64_t*
         ctx->ucap = cap;
     }
     CK(hipEventRecord(e0, ctx->stream));
-    CK(hipMemsetAsync(ctx->d_counter, 0, sizeof(u64), ctx->stream));
-    CK(launch_compact(ctx->tab.slots, ctx->nslots, ctx->d_keys, ctx->d_counts, ctx->d_first, ctx->d_pos,
-                      ctx->d_counter, ctx->stream));
-    // ordinals are < (file_tag + 1) << ORD_SHIFT: sort only the bits that can be set.  Without
-    // merged rows every ordinal is a record start of this context's files, and records span at
-    // least 4 bytes (four line terminators), so bits [0, 2) never decide the order; with one file
-    // the ordinal is its byte offset (file tag 1 sits above every offset bit).  100M SYN-v1 reads
-    // (7.4 GB): bits [2, 33), 4 radix passes instead of 6.
-    int begin_bit = 0, end_bit = 64;
-    if (!ctx->merged) {
-        begin_bit = 2;
-        end_bit = ORD_SHIFT;
-        while (end_bit < 64 && ((u64)ctx->file_tag >> (end_bit - ORD_SHIFT)) != 0) ++end_bit;
-        if (ctx->file_tag == ctx->first_tag) {  // one file: its tag is a constant above every offset bit
-            end_bit = begin_bit + 1;
-            while (end_bit < ORD_SHIFT && (ctx->max_file_bytes >> end_bit) != 0) ++end_bit;
+    // one context's own ordinals: bin them (fin_* kernels); merged rows (any file tag): radix sort
+    BinMap bm{0, 0, 0, 0, 0};
+    u64 nbins = 0;
+    if (!ctx->merged && ctx->first_tag && ctx->file_tag >= ctx->first_tag) {
+        const u64 ntags = (u64)(ctx->file_tag - ctx->first_tag) + 1u;
+        bm.span = std::max<u64>(ctx->max_file_bytes, 1);
+        bm.first_tag = ctx->first_tag;
+        bm.shift = 13;
+        const u64 range = ntags * bm.span;  // < 2^19 tags x 2^44 bytes: no overflow
+        while (bm.shift < 20 && ((range >> bm.shift) + 1) > (1ull << 21)) ++bm.shift;
+        nbins = (range >> bm.shift) + 1;
+        if (nbins > (1ull << 21)) nbins = 0;  // more than 2^41 bytes of input: radix sort
+    }
+    if (nbins) {
+        bm.nbins = nbins;
+        bm.cap = ctx->ucap;
+        if (ctx->nslots > ctx->arr_cap) {
+            if (ctx->d_arr) CK(hipFree(ctx->d_arr));
+            ctx->d_arr = nullptr;
+            CK(hipMalloc(&ctx->d_arr, ctx->nslots * sizeof(u32)));
+            ctx->arr_cap = ctx->nslots;
         }
+        if (ctx->ucap > ctx->rows_cap) {
+            if (ctx->d_rows) CK(hipFree(ctx->d_rows));
+            ctx->d_rows = nullptr;
+            CK(hipMalloc(&ctx->d_rows, ctx->ucap * sizeof(FinRow)));
+            ctx->rows_cap = ctx->ucap;
+        }
+        if (nbins + 1 > ctx->bins_cap) {
+            if (ctx->d_bins) CK(hipFree(ctx->d_bins));
+            if (ctx->d_binbase) CK(hipFree(ctx->d_binbase));
+            ctx->d_bins = ctx->d_binbase = nullptr;
+            const u64 cap = std::max<u64>(nbins + 1, 1u << 16);
+            CK(hipMalloc(&ctx->d_bins, cap * sizeof(u32)));
+            CK(hipMalloc(&ctx->d_binbase, cap * sizeof(u32)));
+            ctx->bins_cap = cap;
+        }
+        size_t need = 0;
+        CK(launch_fin_scan(ctx->d_bins, ctx->d_binbase, nbins + 1, nullptr, &need, ctx->stream));
+        if (need > ctx->temp_bytes) {
+            if (ctx->d_temp) CK(hipFree(ctx->d_temp));
+            CK(hipMalloc(&ctx->d_temp, need));
+            ctx->temp_bytes = need;
+        }
+        size_t tb = ctx->temp_bytes;
+        CK(hipMemsetAsync(ctx->d_bins, 0, (nbins + 1) * sizeof(u32), ctx->stream));
+        CK(launch_fin_hist(ctx->tab.slots, ctx->nslots, bm, ctx->d_bins, ctx->d_arr, ctx->stream));
+        CK(launch_fin_scan(ctx->d_bins, ctx->d_binbase, nbins + 1, ctx->d_temp, &tb, ctx->stream));
+        CK(launch_fin_scatter(ctx->tab.slots, ctx->nslots, bm, ctx->d_binbase, ctx->d_arr, ctx->d_rows, ctx->stream));
+        CK(launch_fin_rank(ctx->tab.slots, nk, bm, ctx->d_binbase, ctx->d_rows, ctx->d_keys_s, ctx->d_counts_s,
+                           ctx->d_first_s, ctx->stream));
+    } else {
+        CK(hipMemsetAsync(ctx->d_counter, 0, sizeof(u64), ctx->stream));
+        CK(launch_compact(ctx->tab.slots, ctx->nslots, ctx->d_keys, ctx->d_counts, ctx->d_first, ctx->d_pos,
+                          ctx->d_counter, ctx->stream));
+        // ordinals are < (file_tag + 1) << ORD_SHIFT: sort only the bits that can be set.  Without
+        // merged rows every ordinal is a record start of this context's files, and records span at
+        // least 4 bytes (four line terminators), so bits [0, 2) never decide the order; with one file
+        // the ordinal is its byte offset (file tag 1 sits above every offset bit).  100M SYN-v1 reads
+        // (7.4 GB): bits [2, 33), 4 radix passes instead of 6.
+        int begin_bit = 0, end_bit = 64;
+        if (!ctx->merged) {
+            begin_bit = 2;
+            end_bit = ORD_SHIFT;
+            while (end_bit < 64 && ((u64)ctx->file_tag >> (end_bit - ORD_SHIFT)) != 0) ++end_bit;
+            if (ctx->file_tag == ctx->first_tag) {  // one file: its tag is a constant above every offset bit
+                end_bit = begin_bit + 1;
+                while (end_bit < ORD_SHIFT && (ctx->max_file_bytes >> end_bit) != 0) ++end_bit;
+            }
+        }
+        size_t need = 0;
+        CK(launch_order(ctx->d_first, ctx->d_pos, nk, ctx->d_first_s, ctx->d_perm, nullptr, &need, begin_bit, end_bit,
+                        ctx->stream));
+        if (need > ctx->temp_bytes) {
+            if (ctx->d_temp) CK(hipFree(ctx->d_temp));
+            CK(hipMalloc(&ctx->d_temp, need));
+            ctx->temp_bytes = need;
+        }
+        size_t tb = ctx->temp_bytes;
+        if (nk)
+            CK(launch_order(ctx->d_first, ctx->d_pos, nk, ctx->d_first_s, ctx->d_perm, ctx->d_temp, &tb, begin_bit,
+                            end_bit, ctx->stream));
+        CK(launch_gather(ctx->d_perm, nk, ctx->d_keys, ctx->d_counts, ctx->d_keys_s, ctx->d_counts_s, ctx->d_rank,
+                         ctx->stream));
+        CK(launch_set_uidx(ctx->tab.slots, ctx->tab.mask, ctx->d_keys_s, nk, ctx->d_rank, ctx->stream));
     }
-    size_t need = 0;
-    CK(launch_order(ctx->d_first, ctx->d_pos, nk, ctx->d_first_s, ctx->d_perm, nullptr, &need, begin_bit, end_bit,
-                    ctx->stream));
-    if (need > ctx->temp_bytes) {
-        if (ctx->d_temp) CK(hipFree(ctx->d_temp));
-        CK(hipMalloc(&ctx->d_temp, need));
-        ctx->temp_bytes = need;
-    }
-    size_t tb = ctx->temp_bytes;
-    if (nk)
-        CK(launch_order(ctx->d_first, ctx->d_pos, nk, ctx->d_first_s, ctx->d_perm, ctx->d_temp, &tb, begin_bit,
-                        end_bit, ctx->stream));
-    CK(launch_gather(ctx->d_perm, nk, ctx->d_keys, ctx->d_counts, ctx->d_keys_s, ctx->d_counts_s, ctx->d_rank,
-                     ctx->stream));
-    CK(launch_set_uidx(ctx->tab.slots, ctx->tab.mask, ctx->d_keys_s, nk, ctx->d_rank, ctx->stream));
     const u64 np = std::min<u64>(ctx->h_st->n_presence, ctx->tab.pres_cap);
     if (np > ctx->pmap_cap) {
         if (ctx->d_pres_u) CK(hipFree(ctx->d_pres_u));
@@ -1086,7 +1141,10 @@ int fr_finalize(fr_ctx* ctx, uint64_t* n_unique, uint64_t* n_presence, uint64_t*
                            ctx->stream));
     CK(hipEventRecord(e1, ctx->stream));
     u64 got = 0;
-    CK(hipMemcpyAsync(&got, ctx->d_counter, sizeof(u64), hipMemcpyDeviceToHost, ctx->stream));
+    if (nbins)  // the scan's last entry: every live slot counted once
+        CK(hipMemcpyAsync(&got, ctx->d_binbase + nbins, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
+    else
+        CK(hipMemcpyAsync(&got, ctx->d_counter, sizeof(u64), hipMemcpyDeviceToHost, ctx->stream));
     CK(hipStreamSynchronize(ctx->stream));
     float ms = 0;
     CK(hipEventElapsedTime(&ms, e0, e1));

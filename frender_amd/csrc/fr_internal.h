@@ -214,6 +214,24 @@ hipError_t launch_gather(const u32* perm, u64 n, const u64* keys, const u64* cou
                          u64* counts_o, u32* rank, hipStream_t s);
 hipError_t launch_presence_map(const GSlot* slots, u64 mask, const Presence* pres, u64 n, u32* uidx,
                                u32* file_idx, hipStream_t s);
+// first-occurrence order by binning (fr_finalize without merged rows)
+struct BinMap {
+    u64 span;       // byte span given to each file tag (>= every ordinal offset)
+    u32 first_tag;  // the context's first file tag
+    u32 shift;      // bin = linear offset >> shift
+    u64 nbins;      // bins (bin indices are clamped below it)
+    u64 cap;        // rows of the scatter arrays
+};
+struct alignas(32) FinRow {  // one live slot on its way to its first-occurrence index
+    u64 first, key, count;
+    u32 slot, pad;
+};
+hipError_t launch_fin_hist(const GSlot* slots, u64 nslots, const BinMap& m, u32* cnt, u32* arr, hipStream_t s);
+hipError_t launch_fin_scan(const u32* cnt, u32* base, u64 n, void* temp, size_t* temp_bytes, hipStream_t s);
+hipError_t launch_fin_scatter(const GSlot* slots, u64 nslots, const BinMap& m, const u32* base, const u32* arr,
+                              FinRow* rows, hipStream_t s);
+hipError_t launch_fin_rank(GSlot* slots, u64 nk, const BinMap& m, const u32* base, const FinRow* rows, u64* keys_o,
+                           u64* counts_o, u64* first_o, hipStream_t s);
 hipError_t launch_classify(const u64* keys, const u64* counts, u64 n, SheetArgs sh, int nsubs, int rc,
                            ClassOut o, hipStream_t s);
 hipError_t launch_classify_cp(int n, const u32* q1, const int32_t* q1len, const u32* q2, const int32_t* q2len,

@@ -2375,6 +2375,98 @@ hipError_t launch_presence_map(const GSlot* slots, u64 mask, const Presence* pre
     return hipGetLastError();
 }
 
+// ---- first-occurrence order by binning (fr_finalize, one context's own ordinals) -------------
+// An ordinal is a record start; records are four terminated lines, so two ordinals of one file
+// are >= 4 bytes apart and a bin of 2^shift bytes holds at most 2^(shift-2) codes (twice that
+// where a bin straddles two files).  Count per bin (each slot keeps its arrival index in uidx),
+// exclusive scan, scatter by bin, then each code's rank inside its bin gives its final index: the
+// table is read twice and nothing is sorted globally.
+__device__ __forceinline__ u64 ord_bin(const BinMap& m, u64 ord) {
+    const u64 tag = ord >> ORD_SHIFT, off = ord & ((1ull << ORD_SHIFT) - 1ull);
+    return min(((tag - m.first_tag) * m.span + off) >> m.shift, m.nbins - 1ull);  // clamp: never out of bounds
+}
+
+// One slot (one 32-B sector) per lane, the whole table in one grid.  Every store here is a whole
+// sector or part of a coalesced run: a random 4- or 8-B store is a partial-sector write, which HBM
+// turns into a read-modify-write (the first version of these kernels stored into table slots and
+// ran at half the speed).
+__global__ __launch_bounds__(256) void fin_hist_kernel(const GSlot* slots, u64 n, BinMap m, u32* cnt, u32* arr) {
+    const u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint4 w0 = *(const uint4*)&slots[i];
+    const uint4 w1 = *((const uint4*)&slots[i] + 1);
+    u32 v = 0xFFFFFFFFu;
+    if ((w0.x | w0.y) != 0u) v = atomicAdd(&cnt[ord_bin(m, ((u64)w1.y << 32) | w1.x)], 1u);
+    arr[i] = v;  // arrival index in the bin (coalesced: every lane stores)
+}
+
+// each live slot's row {ordinal, key, count, slot} to its bin's run, one 32-B sector per row
+__global__ __launch_bounds__(256) void fin_scatter_kernel(const GSlot* slots, u64 n, BinMap m, const u32* base,
+                                                          const u32* arr, FinRow* rows) {
+    const u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const u32 k = arr[i];
+    if (k == 0xFFFFFFFFu) return;
+    const uint4 w0 = *(const uint4*)&slots[i];
+    const uint4 w1 = *((const uint4*)&slots[i] + 1);
+    const u64 first = ((u64)w1.y << 32) | w1.x;
+    const u32 q = base[ord_bin(m, first)] + k;
+    if (q < m.cap) {
+        typedef u32 u32x4 __attribute__((ext_vector_type(4)));
+        u32x4* d = (u32x4*)&rows[q];
+        d[0] = u32x4{w1.x, w1.y, w0.x, w0.y};
+        d[1] = u32x4{w0.z, w0.w, (u32)i, 0u};
+    }
+}
+
+// final index = the bin's base + the codes of the bin with a smaller ordinal (ties: slot index,
+// never met for one context's ordinals); the row goes there and the slot's uidx becomes that index
+__global__ __launch_bounds__(256) void fin_rank_kernel(GSlot* slots, u64 nk, BinMap m, const u32* base,
+                                                       const FinRow* rows, u64* keys_o, u64* counts_o, u64* first_o) {
+    const u64 q = blockIdx.x * (u64)blockDim.x + threadIdx.x;
+    if (q >= nk) return;
+    const FinRow row = rows[q];
+    const u64 b = ord_bin(m, row.first);
+    const u32 lo = base[b], hi = (u32)min((u64)base[b + 1], m.cap);
+    u32 r = 0;
+    for (u32 j = lo; j < hi; ++j) {
+        const u64 fj = rows[j].first;
+        r += (fj < row.first || (fj == row.first && rows[j].slot < row.slot)) ? 1u : 0u;
+    }
+    const u32 out = lo + r;
+    if (out >= nk) return;  // only when the live count disagrees with n_keys (fr_finalize fails then)
+    keys_o[out] = row.key;
+    counts_o[out] = row.count;
+    first_o[out] = row.first;
+    slots[row.slot].uidx = out;
+}
+
+static unsigned lane_grid(u64 n) { return (unsigned)std::max<u64>(1, (n + 255) / 256); }
+
+hipError_t launch_fin_hist(const GSlot* slots, u64 nslots, const BinMap& m, u32* cnt, u32* arr, hipStream_t s) {
+    hipLaunchKernelGGL(fin_hist_kernel, dim3(lane_grid(nslots)), dim3(256), 0, s, slots, nslots, m, cnt, arr);
+    return hipGetLastError();
+}
+
+// exclusive scan of cnt[0, n) into base[0, n) (temp = nullptr: size query)
+hipError_t launch_fin_scan(const u32* cnt, u32* base, u64 n, void* temp, size_t* temp_bytes, hipStream_t s) {
+    return rocprim::exclusive_scan(temp, *temp_bytes, cnt, base, 0u, (size_t)n, rocprim::plus<u32>(), s);
+}
+
+hipError_t launch_fin_scatter(const GSlot* slots, u64 nslots, const BinMap& m, const u32* base, const u32* arr,
+                              FinRow* rows, hipStream_t s) {
+    hipLaunchKernelGGL(fin_scatter_kernel, dim3(lane_grid(nslots)), dim3(256), 0, s, slots, nslots, m, base, arr, rows);
+    return hipGetLastError();
+}
+
+hipError_t launch_fin_rank(GSlot* slots, u64 nk, const BinMap& m, const u32* base, const FinRow* rows, u64* keys_o,
+                           u64* counts_o, u64* first_o, hipStream_t s) {
+    if (!nk) return hipSuccess;
+    hipLaunchKernelGGL(fin_rank_kernel, dim3(lane_grid(nk)), dim3(256), 0, s, slots, nk, m, base, rows, keys_o,
+                       counts_o, first_o);
+    return hipGetLastError();
+}
+
 // merge another GPU's compacted table into this one (count +, first min); presence of
 // remote keys travels separately (fr_get_presence on each rank)
 __global__ void merge_kernel(Table t, DevState* st, const u64* keys, const u64* counts, const u64* first, u64 n) {
@@ -2385,31 +2477,62 @@ __global__ void merge_kernel(Table t, DevState* st, const u64* keys, const u64* 
 }
 
 // per-file presence (R10) and the per-file distinct-code count (frender.py:175): after a
-// file, exactly the slots whose last_tag is that file's tag hold a code seen in it
+// file, exactly the slots whose last_tag is that file's tag hold a code seen in it.  A workgroup
+// takes PS_K x 256 consecutive slots, one slot per lane per step with all the loads in flight
+// together, reserves its output run with one atomic and writes its hits in slot order.
+constexpr int PS_K = 16;
 __global__ __launch_bounds__(CWG) void presence_scan_kernel(const GSlot* slots, u64 n, u32 tag, Presence* pres,
                                                             u64 cap, DevState* st) {
-    __shared__ u32 red[8];
-    u64 lo, hi;
-    block_range(n, lo, hi);
-    auto pred = [&](u64 i) {
-        const uint4 w0 = *(const uint4*)&slots[i];
-        const uint4 w1 = *((const uint4*)&slots[i] + 1);
-        return (w0.x | w0.y) != 0u && w1.z == tag;
-    };
-    const u64 base = block_reserve(lo, hi, pred, &st->n_presence, red);
-    block_emit(lo, hi, base, pred, [&](u64 k, u64 i) {
-        if (k < cap) {
-            pres[k].key = slots[i].key;
-            pres[k].tag = tag;
-        } else {
-            atomicOr(&st->cap_flags, 1u);
+    __shared__ u32 wc[PS_K * (CWG / 64)];
+    __shared__ u64 bbase;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const u64 b0 = (u64)blockIdx.x * (PS_K * CWG);
+    u32 hits = 0;
+#pragma unroll
+    for (int k = 0; k < PS_K; ++k) {
+        const u64 i = b0 + (u64)k * CWG + tid;
+        if (i < n) {
+            const uint2 key = *(const uint2*)&slots[i];
+            const u32 lt = slots[i].last_tag;
+            hits |= ((key.x | key.y) != 0u && lt == tag) ? (1u << k) : 0u;
         }
-    }, red);
+    }
+    u64 m[PS_K];
+#pragma unroll
+    for (int k = 0; k < PS_K; ++k) {
+        m[k] = __ballot((hits >> k) & 1u);
+        if (lane == 0) wc[k * (CWG / 64) + wid] = (u32)__popcll(m[k]);
+    }
+    __syncthreads();
+    if (tid == 0) {  // exclusive scan over (step, wave) = slot order, and the block's output run
+        u32 run = 0;
+        for (int j = 0; j < PS_K * (CWG / 64); ++j) {
+            const u32 c = wc[j];
+            wc[j] = run;
+            run += c;
+        }
+        bbase = run ? atomicAdd((unsigned long long*)&st->n_presence, (unsigned long long)run) : 0ull;
+    }
+    __syncthreads();
+    if (!hits) return;
+    const u64 below = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int k = 0; k < PS_K; ++k) {
+        if ((hits >> k) & 1u) {
+            const u64 kk = bbase + wc[k * (CWG / 64) + wid] + (u64)__popcll(m[k] & below);
+            if (kk < cap) {
+                pres[kk].key = slots[b0 + (u64)k * CWG + tid].key;
+                pres[kk].tag = tag;
+            } else {
+                atomicOr(&st->cap_flags, 1u);
+            }
+        }
+    }
 }
 
 hipError_t launch_presence_scan(const GSlot* slots, u64 n, u32 tag, Presence* pres, u64 cap, DevState* st,
                                 hipStream_t s) {
-    const int grid = (int)std::max<u64>(1, std::min<u64>((n + 4095) / 4096, 2048));
+    const int grid = (int)std::max<u64>(1, (n + PS_K * CWG - 1) / (PS_K * CWG));
     hipLaunchKernelGGL(presence_scan_kernel, dim3(grid), dim3(CWG), 0, s, slots, n, tag, pres, cap, st);
     return hipGetLastError();
 }

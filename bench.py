@@ -54,7 +54,7 @@ def parse():
                          "partition) or a binary tree into rank 0")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, one GPU per rank); gloo only to rehearse N ranks on one GPU")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02f.json"),
                     help="per-launch HBM bytes of the tally kernel from rocprofv3 PMC (null if absent)")
     return ap.parse_args()
 

@@ -2036,6 +2036,10 @@ __global__ __launch_bounds__(256) void log_scatter_kernel(const LogEntry* log, c
 #define FR_AGG_LNS 2048
 #endif
 constexpr int AGG_LNS = FR_AGG_LNS;  // LDS slots of one bucket's aggregation
+#ifndef FR_AGG_LB
+#define FR_AGG_LB 4
+#endif
+constexpr int AGG_LB = FR_AGG_LB;  // log rows per thread in flight
 constexpr int AGG_PROBE = 64;
 struct alignas(16) AggSlot {
     u64 key;
@@ -2154,16 +2158,16 @@ __global__ __launch_bounds__(256) void log_reduce_kernel(Table t, DevState* st, 
     for (u32 bk = blockIdx.x; bk < (u32)AGG_NB; bk += gridDim.x) {
         const u64 lo = g.base[bk], hi = bk + 1 < (u32)AGG_NB ? (u64)g.base[bk + 1] : (u64)g.cur[bk];
         if (lo == hi) continue;  // uniform: nothing logged for this bucket (its LDS table is still clean)
-        // four rows per thread in flight per step (a step's loads are independent of its LDS work)
-        for (u64 i0 = lo + threadIdx.x; i0 < ((ablate & 512u) ? lo : hi); i0 += 4 * 256) {  // 512: timing ablation
-            LogEntry ev[4];
+        // AGG_LB rows per thread in flight per step (a step's loads are independent of its LDS work)
+        for (u64 i0 = lo + threadIdx.x; i0 < ((ablate & 512u) ? lo : hi); i0 += AGG_LB * 256) {  // 512: timing ablation
+            LogEntry ev[AGG_LB];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
+            for (int q = 0; q < AGG_LB; ++q) {
                 const u64 i = i0 + (u64)q * 256;
                 ev[q] = i < hi ? sorted[i] : LogEntry{0, 0, 0};
             }
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
+            for (int q = 0; q < AGG_LB; ++q) {
                 const LogEntry e = ev[q];
                 if (!e.key) continue;
                 u32 h = (u32)mix64(e.key) & (AGG_LNS - 1);

@@ -41,12 +41,13 @@ def main():
     reads = int(sys.argv[2]) if len(sys.argv) > 2 else 100_000_000
     read_len = int(sys.argv[3]) if len(sys.argv) > 3 else 8
     launches = int(sys.argv[4]) if len(sys.argv) > 4 else 7
-    reclen = 36 + 8 + 1 + 8 + 1 + 2 * read_len + 4
+    reclen = int(os.environ.get("RECLEN", 36 + 8 + 1 + 8 + 1 + 2 * read_len + 4))  # RECLEN: other index lengths
     prof = os.path.join(ROOT, "profiles")
-    stats = glob.glob(os.path.join(ROOT, "gpurun_out/prof_trace/**/*kernel_stats.csv"), recursive=True)
+    src = os.environ.get("PROF_DIR", "gpurun_out")
+    stats = glob.glob(os.path.join(ROOT, src, "prof_trace/**/*kernel_stats.csv"), recursive=True)
     shutil.copy(stats[0], os.path.join(prof, f"{tag}_kernel_stats.csv"))
-    fetch, frows = per_dispatch(rows("gpurun_out/prof_fetch/**/*counter_collection.csv"), "FETCH_SIZE")
-    write, wrows = per_dispatch(rows("gpurun_out/prof_write/**/*counter_collection.csv"), "WRITE_SIZE")
+    fetch, frows = per_dispatch(rows(src + "/prof_fetch/**/*counter_collection.csv"), "FETCH_SIZE")
+    write, wrows = per_dispatch(rows(src + "/prof_write/**/*counter_collection.csv"), "WRITE_SIZE")
     with open(os.path.join(prof, f"{tag}_pmc_chunk_kernel.csv"), "w", newline="") as fh:
         w = csv.DictWriter(fh, fieldnames=list(frows[0].keys()))
         w.writeheader()
@@ -69,7 +70,7 @@ def main():
         "hbm_bytes_per_launch": int(2 * fkb * 1024 + wkb * 1024),
         "traffic_over_algorithmic": round((2 * fkb * 1024 + wkb * 1024) / alg, 4),
         "source": f"profiles/{tag}_pmc_chunk_kernel.csv (rocprofv3 --pmc FETCH_SIZE, then --pmc WRITE_SIZE, "
-                  f"separate runs of bench.py --steps 5 --warmup 1 --no-cpu)",
+                  f"separate runs of bench.py {os.environ.get('PROF_ARGS', '--steps 5 --warmup 1 --no-cpu')})",
     }
     with open(os.path.join(prof, os.environ.get("TRAFFIC_JSON", "traffic_r02.json")), "w") as fh:
         json.dump(out, fh, indent=1)

@@ -32,7 +32,7 @@ struct fr_ctx {
     LogEntry* log = nullptr;
     LogEntry* log_sorted = nullptr;
     u64 log_cap = 0;
-    u32* log_hist = nullptr;       // aggregation scratch, (AGG_SLICES + 3) x AGG_NB
+    u32* log_hist = nullptr;       // aggregation scratch, (AGG_SLICES + 3) x AGG_NB + 64
     void* log_temp = nullptr;
     size_t log_temp_bytes = 0;
     u32 log_min = 2600;            // pairs from which a commit logs (SYN-v1 config 2's full chunks commit ~1740 pairs
@@ -43,6 +43,12 @@ struct fr_ctx {
     DevState* h_st = nullptr;      // pinned snapshot
     DevState* h_zero = nullptr;    // pinned reset image (zero counters, no error), never modified
     u8* h_byte = nullptr;          // pinned: a device feed's last byte, copied with the feed's state read
+    // fr_finalize returns without a host round trip; its live-count check and timing settle at the
+    // next call that synchronises (settle_finalize)
+    u64* h_fin = nullptr;          // pinned: the finalize's live-slot count
+    hipEvent_t fin_e0 = nullptr, fin_e1 = nullptr;
+    bool fin_pending = false;
+    u64 fin_expect = 0;
     bool st_fresh = false;         // h_st equals the device state (no device work on it since)
     Table* d_tab = nullptr;        // device copy of tab for the tally kernel
     Table* h_tab = nullptr;        // pinned staging of that copy (last uploaded value)
@@ -273,6 +279,19 @@ static int snapshot_async(fr_ctx* ctx) {
     CK(hipMemcpyAsync(ctx->h_st, ctx->st, sizeof(DevState), hipMemcpyDeviceToHost, ctx->stream));
     CK(hipEventRecord(ctx->st_ev, ctx->stream));
     ctx->st_pending = true;
+    return FR_OK;
+}
+
+// the last fr_finalize's check: every live slot was counted once (its pinned count has landed once
+// fin_e1 has: the copy is queued before the event), and its device time
+static int settle_finalize(fr_ctx* ctx) {
+    if (!ctx->fin_pending) return FR_OK;
+    ctx->fin_pending = false;
+    CK(hipEventSynchronize(ctx->fin_e1));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, ctx->fin_e0, ctx->fin_e1));
+    ctx->finalize_ms = ms;
+    if (*ctx->h_fin != ctx->fin_expect) return fail(ctx, FR_ERR_DEVICE, "compaction count mismatch");
     return FR_OK;
 }
 
@@ -541,7 +560,7 @@ fr_ctx* fr_create(int device, uint64_t chunk_bytes, uint64_t table_slots) {
         ctx->log_cap = std::min<u64>(std::max<u64>(ctx->chunk_bytes / 256, 1ull << 16), 1ull << 26);
         if ((e = dalloc(&ctx->log, ctx->log_cap)) != hipSuccess) return bad("launch log", e);
         if ((e = dalloc(&ctx->log_sorted, ctx->log_cap)) != hipSuccess) return bad("launch log", e);
-        const u64 nh = (u64)(AGG_SLICES + 3) * AGG_NB;
+        const u64 nh = (u64)(AGG_SLICES + 3) * AGG_NB + 64;  // + AggScratch::ctl
         if ((e = dalloc(&ctx->log_hist, nh)) != hipSuccess) return bad("log histogram", e);
         if ((e = hipMemset(ctx->log_hist, 0, nh * sizeof(u32))) != hipSuccess) return bad("log histogram", e);
     }
@@ -558,6 +577,9 @@ fr_ctx* fr_create(int device, uint64_t chunk_bytes, uint64_t table_slots) {
     if ((e = hipHostMalloc((void**)&ctx->h_st, sizeof(DevState), hipHostMallocDefault)) != hipSuccess)
         return bad("pinned state", e);
     if ((e = hipHostMalloc((void**)&ctx->h_byte, 64, hipHostMallocDefault)) != hipSuccess) return bad("pinned byte", e);
+    if ((e = hipHostMalloc((void**)&ctx->h_fin, 64, hipHostMallocDefault)) != hipSuccess) return bad("pinned count", e);
+    if ((e = hipEventCreate(&ctx->fin_e0)) != hipSuccess) return bad("event", e);
+    if ((e = hipEventCreate(&ctx->fin_e1)) != hipSuccess) return bad("event", e);
     if ((e = hipHostMalloc((void**)&ctx->h_zero, sizeof(DevState), hipHostMallocDefault)) != hipSuccess)
         return bad("pinned reset state", e);
     std::memset(ctx->h_zero, 0, sizeof(DevState));
@@ -610,6 +632,9 @@ void fr_destroy(fr_ctx* ctx) {
     if (ctx->h_st) (void)hipHostFree(ctx->h_st);
     if (ctx->h_zero) (void)hipHostFree(ctx->h_zero);
     if (ctx->h_byte) (void)hipHostFree(ctx->h_byte);
+    if (ctx->h_fin) (void)hipHostFree(ctx->h_fin);
+    if (ctx->fin_e0) (void)hipEventDestroy(ctx->fin_e0);
+    if (ctx->fin_e1) (void)hipEventDestroy(ctx->fin_e1);
     if (ctx->h_sheet) (void)hipHostFree(ctx->h_sheet);
     if (ctx->h_tab) (void)hipHostFree(ctx->h_tab);
     for (int i = 0; i < 2; ++i) {
@@ -629,6 +654,7 @@ void fr_destroy(fr_ctx* ctx) {
 const char* fr_last_error(const fr_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
 int fr_get_diag(fr_ctx* ctx, uint64_t* out, int n) {
+    if (int src = settle_finalize(ctx)) return src;
     int rc = read_state(ctx);
     if (rc) return rc;
     const DevState& s = *ctx->h_st;
@@ -642,11 +668,12 @@ int fr_get_diag(fr_ctx* ctx, uint64_t* out, int n) {
 int fr_sync(fr_ctx* ctx) {
     CK(hipStreamSynchronize(ctx->stream));
     CK(hipStreamSynchronize(ctx->copy));
-    return FR_OK;
+    return settle_finalize(ctx);
 }
 
 int fr_get_timing(fr_ctx* ctx, fr_timing* out) {
     CK(hipStreamSynchronize(ctx->stream));
+    if (int src = settle_finalize(ctx)) return src;
     double tot = 0, last = 0, lg = 0;
     for (size_t i = 0; i < ctx->ev_used; ++i) {
         float ms = 0, ml = 0;
@@ -738,6 +765,7 @@ int fr_set_sheet(fr_ctx* ctx, int S, const uint64_t* idx1_packed, const int32_t*
 }
 
 int fr_reset(fr_ctx* ctx) {
+    if (int src = settle_finalize(ctx)) return src;
     CK(hipSetDevice(ctx->device));
     CK(hipStreamSynchronize(ctx->copy));
     CK(launch_table_init(ctx->tab.slots, ctx->nslots, ctx->stream));
@@ -771,6 +799,7 @@ int fr_begin_file(fr_ctx* ctx, int64_t max_records) {
 }
 
 int fr_begin_file_at(fr_ctx* ctx, int64_t file_index, uint64_t byte_base, int64_t max_records) {
+    if (int src = settle_finalize(ctx)) return src;
     if (ctx->file_open) return fail(ctx, FR_ERR_INVALID, "fr_begin_file: a file is already open");
     if (file_index < 0 || file_index + 1 >= (1 << 19)) return fail(ctx, FR_ERR_INVALID, "too many files in one scan");
     if ((u32)file_index + 1u <= ctx->file_tag)
@@ -1014,10 +1043,10 @@ int fr_end_file(fr_ctx* ctx, fr_file_stats* out) {
 
 int fr_finalize(fr_ctx* ctx, uint64_t* n_unique, uint64_t* n_presence, uint64_t* n_exotic) {
     if (ctx->file_open) return fail(ctx, FR_ERR_INVALID, "fr_finalize: a file is still open");
-    hipEvent_t e0, e1;
-    CK(hipEventCreate(&e0));
-    CK(hipEventCreate(&e1));
-    int rc = grow_table(ctx, false);
+    int rc = settle_finalize(ctx);
+    if (rc) return rc;
+    hipEvent_t e0 = ctx->fin_e0, e1 = ctx->fin_e1;
+    rc = grow_table(ctx, false);
     if (rc) return rc;
     rc = read_state(ctx);
     if (rc) return rc;
@@ -1139,19 +1168,14 @@ int fr_finalize(fr_ctx* ctx, uint64_t* n_unique, uint64_t* n_presence, uint64_t*
     }
     CK(launch_presence_map(ctx->tab.slots, ctx->tab.mask, ctx->tab.pres, np, ctx->d_pres_u, ctx->d_pres_f,
                            ctx->stream));
-    CK(hipEventRecord(e1, ctx->stream));
-    u64 got = 0;
+    *ctx->h_fin = 0;
     if (nbins)  // the scan's last entry: every live slot counted once
-        CK(hipMemcpyAsync(&got, ctx->d_binbase + nbins, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
+        CK(hipMemcpyAsync(ctx->h_fin, ctx->d_binbase + nbins, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
     else
-        CK(hipMemcpyAsync(&got, ctx->d_counter, sizeof(u64), hipMemcpyDeviceToHost, ctx->stream));
-    CK(hipStreamSynchronize(ctx->stream));
-    float ms = 0;
-    CK(hipEventElapsedTime(&ms, e0, e1));
-    ctx->finalize_ms = ms;
-    CK(hipEventDestroy(e0));
-    CK(hipEventDestroy(e1));
-    if (got != nk) return fail(ctx, FR_ERR_DEVICE, "compaction count mismatch");
+        CK(hipMemcpyAsync(ctx->h_fin, ctx->d_counter, sizeof(u64), hipMemcpyDeviceToHost, ctx->stream));
+    CK(hipEventRecord(e1, ctx->stream));
+    ctx->fin_pending = true;
+    ctx->fin_expect = nk;
     ctx->U = nk;
     ctx->n_pres = np;
     ctx->n_exo = ctx->exo_codes.size();
@@ -1162,6 +1186,7 @@ int fr_finalize(fr_ctx* ctx, uint64_t* n_unique, uint64_t* n_presence, uint64_t*
 }
 
 int fr_get_unique(fr_ctx* ctx, uint64_t* keys, uint64_t* counts, uint64_t* first_ordinal) {
+    if (int src = settle_finalize(ctx)) return src;
     const u64 n = ctx->U;
     if (!n) return FR_OK;
     if (keys) CK(hipMemcpy(keys, ctx->d_keys_s, n * 8, hipMemcpyDeviceToHost));
@@ -1171,6 +1196,7 @@ int fr_get_unique(fr_ctx* ctx, uint64_t* keys, uint64_t* counts, uint64_t* first
 }
 
 int fr_get_presence(fr_ctx* ctx, uint32_t* unique_idx, uint32_t* file_idx) {
+    if (int src = settle_finalize(ctx)) return src;
     const u64 n = ctx->n_pres;
     if (!n) return FR_OK;
     CK(hipMemcpy(unique_idx, ctx->d_pres_u, n * 4, hipMemcpyDeviceToHost));
@@ -1179,6 +1205,7 @@ int fr_get_presence(fr_ctx* ctx, uint32_t* unique_idx, uint32_t* file_idx) {
 }
 
 int fr_exotic_sizes(fr_ctx* ctx, uint64_t* n_codes, uint64_t* code_bytes, uint64_t* n_presence) {
+    if (int src = settle_finalize(ctx)) return src;
     u64 b = 0;
     for (const auto& c : ctx->exo_str) b += c.size();
     if (n_codes) *n_codes = ctx->exo_str.size();
@@ -1189,6 +1216,7 @@ int fr_exotic_sizes(fr_ctx* ctx, uint64_t* n_codes, uint64_t* code_bytes, uint64
 
 int fr_get_exotic_table(fr_ctx* ctx, uint64_t* counts, uint64_t* first, uint64_t* offsets, uint8_t* bytes,
                         uint32_t* pres_code, uint32_t* pres_file) {
+    if (int src = settle_finalize(ctx)) return src;
     const u64 n = ctx->exo_str.size();
     u64 b = 0;
     for (u64 i = 0; i < n; ++i) {
@@ -1250,6 +1278,7 @@ int fr_classify(fr_ctx* ctx, int num_subs, int rc_mode, int16_t* m1, int16_t* m2
     u64 ef = ~0ull;
     CK(hipMemcpyAsync(&ef, ctx->d_errf, 8, hipMemcpyDeviceToHost, ctx->stream));
     CK(hipStreamSynchronize(ctx->stream));
+    if (int src = settle_finalize(ctx)) return src;  // landed with the classify: no extra round trip
     float ms = 0;
     CK(hipEventElapsedTime(&ms, e0, e1));
     ctx->classify_ms = ms;
@@ -1275,6 +1304,7 @@ int fr_classify(fr_ctx* ctx, int num_subs, int rc_mode, int16_t* m1, int16_t* m2
 }
 
 int fr_rc_counts(fr_ctx* ctx, uint64_t* reads_f, uint64_t* reads_rc) {
+    if (int src = settle_finalize(ctx)) return src;
     if (!ctx->d_rcf) return fail(ctx, FR_ERR_INVALID, "fr_rc_counts: no rc classify yet");
     const int names = std::max(ctx->n_names, 1);
     std::vector<u64> f(names), r(names);
@@ -1291,6 +1321,7 @@ int fr_classify_cp(fr_ctx* ctx, int n, const uint32_t* q1, const int32_t* q1len,
                    const int32_t* q2len, int cp_stride, int num_subs, int rc_mode, int16_t* m1, int16_t* m2,
                    uint8_t* cls, int16_t* row, int16_t* rc_m2, uint8_t* rc_cls, int16_t* rc_row,
                    int32_t* err_which) {
+    if (int src = settle_finalize(ctx)) return src;
     if (n <= 0) return FR_OK;
     if (ctx->S > 0 && (!ctx->d_cp1 || cp_stride != ctx->cp_stride))
         return fail(ctx, FR_ERR_INVALID, "fr_classify_cp: sheet code points missing or stride mismatch");
@@ -1337,6 +1368,7 @@ int fr_classify_cp(fr_ctx* ctx, int n, const uint32_t* q1, const int32_t* q1len,
 }
 
 int fr_export_unique_device(fr_ctx* ctx, void* dev_keys, void* dev_counts, void* dev_first, uint64_t cap) {
+    if (int src = settle_finalize(ctx)) return src;
     if (ctx->U > cap) return fail(ctx, FR_ERR_CAPACITY, "export buffer too small");
     if (ctx->U) {
         CK(hipMemcpyAsync(dev_keys, ctx->d_keys_s, ctx->U * 8, hipMemcpyDeviceToDevice, ctx->stream));
@@ -1349,6 +1381,7 @@ int fr_export_unique_device(fr_ctx* ctx, void* dev_keys, void* dev_counts, void*
 
 int fr_merge_unique_device(fr_ctx* ctx, const void* dev_keys, const void* dev_counts, const void* dev_first,
                            uint64_t n) {
+    if (int src = settle_finalize(ctx)) return src;
     if (ctx->file_open) return fail(ctx, FR_ERR_INVALID, "fr_merge_unique_device: a file is open");
     ctx->merged = true;
     int rc = read_state(ctx);

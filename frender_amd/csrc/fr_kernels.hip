@@ -1926,19 +1926,38 @@ __device__ __forceinline__ void log_slice(u64 n, u32 s, u64& lo, u64& hi) {
     hi = min(n, lo + per);
 }
 
-// aggregation scratch (fr_api allocates (AGG_SLICES + 3) * AGG_NB u32, zeroed once):
-//   sh[s][b]  per-slice bucket counts        total[b]  entries per bucket (zeroed again by log_base_kernel)
+// aggregation scratch (fr_api allocates (AGG_SLICES + 3) * AGG_NB + 64 u32, zeroed once):
+//   sh[s][b]  per-slice bucket counts        total[b]  entries per bucket (zeroed again by the count pass's last block)
 //   base[b]   first entry of bucket b         cur[b]    scatter cursor (starts at base[b])
 struct AggScratch {
     u32* sh;
     u32* total;
     u32* base;
     u32* cur;
+    u32* ctl;  // [0] count-pass blocks done, [1] reduce-pass blocks done (each back to 0 by its last block)
     __host__ __device__ static AggScratch at(u32* p) {
         return AggScratch{p, p + (size_t)AGG_SLICES * AGG_NB, p + (size_t)(AGG_SLICES + 1) * AGG_NB,
-                          p + (size_t)(AGG_SLICES + 2) * AGG_NB};
+                          p + (size_t)(AGG_SLICES + 2) * AGG_NB, p + (size_t)(AGG_SLICES + 3) * AGG_NB};
     }
 };
+
+// this block is the last of the grid to pass here (counter ctr, reset for the next launch); every
+// block's earlier global writes are visible to the last one
+__device__ __forceinline__ bool last_block(u32* ctr) {
+    __shared__ u32 last;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        const u32 prev = atomicAdd(ctr, 1u);
+        last = prev == gridDim.x - 1u;
+        if (last) {
+            *ctr = 0;
+            __threadfence();
+        }
+    }
+    __syncthreads();
+    return last != 0;
+}
 
 // pass 1: bucket counts per slice of the log, summed per bucket with one atomic per (slice, bucket)
 __global__ __launch_bounds__(256) void log_count_kernel(const LogEntry* log, const DevState* st, u64 cap, AggScratch g) {
@@ -1967,21 +1986,18 @@ __global__ __launch_bounds__(256) void log_count_kernel(const LogEntry* log, con
         row[b] = c;
         if (c) atomicAdd(&g.total[b], c);
     }
-}
-
-// pass 2 (one workgroup): bucket bases = exclusive scan of the totals; cursors start there
-__global__ __launch_bounds__(1024) void log_base_kernel(const DevState* st, AggScratch g) {
-    if (st->log_n == 0) return;
-    constexpr int PER = AGG_NB / 1024;
-    __shared__ u32 ws[16];
+    if (!last_block(&g.ctl[0])) return;
+    // the last block: bucket bases = exclusive scan of the totals; cursors start there
+    constexpr int PER = AGG_NB / 256;
+    __shared__ u32 ws[4];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     u32 v[PER], sum = 0;
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
-        v[j] = g.total[tid * PER + j];
+        v[j] = __hip_atomic_load(&g.total[tid * PER + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         sum += v[j];
     }
-    u32 x = sum;  // inclusive wave scan, then across the 16 waves
+    u32 x = sum;  // inclusive wave scan, then across the 4 waves
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
         const u32 y = __shfl_up(x, d, 64);
@@ -1989,9 +2005,8 @@ __global__ __launch_bounds__(1024) void log_base_kernel(const DevState* st, AggS
     }
     if (lane == 63) ws[wid] = x;
     __syncthreads();
-    u32 before = 0;
-    for (int w = 0; w < wid; ++w) before += ws[w];
-    u32 run = before + x - sum;
+    u32 run = x - sum;
+    for (int w = 0; w < wid; ++w) run += ws[w];
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
         const int b = tid * PER + j;
@@ -2217,6 +2232,9 @@ __global__ __launch_bounds__(256) void log_reduce_kernel(Table t, DevState* st, 
         __syncthreads();
     }
     add_created(st, made);
+    // every block has read log_n: the last one empties the log for the next launch
+    if (last_block(&g.ctl[1]) && threadIdx.x == 0)
+        __hip_atomic_store(&st->log_n, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 size_t log_aggregate_temp_bytes() { return 0; }
@@ -2226,15 +2244,12 @@ hipError_t launch_log_aggregate(Table t, DevState* st, LogEntry* log, LogEntry* 
     const AggScratch g = AggScratch::at(hist);
     // every pass reads log_n on the device and returns at once when no commit logged (the usual case
     // for low-cardinality runs: only commits past ScanArgs::log_min pairs per 16 tiles log)
-    hipLaunchKernelGGL(log_count_kernel, dim3(AGG_SLICES), dim3(256), 0, s, log, st, cap, g);
-    hipLaunchKernelGGL(log_base_kernel, dim3(1), dim3(1024), 0, s, st, g);
+    hipLaunchKernelGGL(log_count_kernel, dim3(AGG_SLICES), dim3(256), 0, s, log, st, cap, g);  // + bucket bases
     hipLaunchKernelGGL(log_scatter_kernel, dim3(AGG_SLICES), dim3(256), 0, s, log, st, cap, g, sorted);
     const u64 ord0 = ((u64)file_tag << ORD_SHIFT) | file_offset;
     static const int rgrid = getenv("FR_AGG_GRID") ? atoi(getenv("FR_AGG_GRID")) : 1024;
     hipLaunchKernelGGL(log_reduce_kernel, dim3(rgrid), dim3(256), 0, s, t, st, sorted, g, file_tag, ord0, ablate);
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    return hipMemsetAsync(&st->log_n, 0, sizeof(u64), s);
+    return hipGetLastError();  // log_reduce_kernel's last block emptied the log
 }
 
 // Stream compaction of table slots with one atomic per workgroup (single-address atomics

@@ -711,3 +711,51 @@ def test_bgzf_scan_matches_oracle(tmp_path, corrupt):
     assert outs["gpu"] == outs["oracle"]
     if not corrupt:
         assert isinstance(outs["gpu"], dict) and outs["gpu"]
+
+
+# ---------------------------------------------------------------------------------------
+# first-occurrence order by binning (fr_finalize, fin_* kernels)
+# ---------------------------------------------------------------------------------------
+@pytest.mark.parametrize("mode", ["host", "device"])
+def test_first_occurrence_bins(lib, mode):
+    """Dense bins: ~22-B records whose codes are nearly all new, so every 8-KiB bin holds hundreds of
+    codes ranked inside the bin; files at non-consecutive indices and one at a large byte base (the
+    bins span every file's bytes); codes repeated across files keep their first file's ordinal.
+    Order, counts and records equal the oracle's."""
+    rng = np.random.default_rng(17)
+    alpha = np.array(list("ACGT"))
+    pool = ["".join(rng.choice(alpha, 8)) + "+" + "".join(rng.choice(alpha, 8)) for _ in range(60000)]
+    files = []
+    for n in (40000, 25000, 30000):
+        idx = rng.integers(0, len(pool), n)
+        files.append("".join(f"@r 1:N:0:{pool[i]}\nA\n+\nF\n" for i in idx).encode())
+    c = lib.Context(device=0, chunk_bytes=1 << 20, table_slots=1 << 16)
+    try:
+        c.reset()
+        recs = []
+        for fi, base, data in zip((0, 3, 7), (0, 0, 3 << 30), files):
+            c.begin_file(None, file_index=fi, byte_base=base)
+            if mode == "device":
+                p = c.device_alloc(len(data) + 16)
+                try:
+                    c.copy_to_device(p, data)
+                    c.feed_device(p, len(data))
+                    st = c.end_file()
+                finally:
+                    c.device_free(p)
+            else:
+                for pos in range(0, len(data), 1 << 18):
+                    c.feed(data[pos:pos + (1 << 18)])
+                st = c.end_file()
+            assert st.error == 0 and st.exotic == 0
+            recs.append(int(st.records))
+        U, _, _ = c.finalize()
+        keys, counts, first = c.unique()
+        assert U == len(keys)
+        assert np.all(np.diff(first.astype(np.float64)) > 0)
+        got = dict(zip(lib.decode_keys(keys), counts.tolist()))
+    finally:
+        c.close()
+    exp = oracle_tally(files)
+    assert recs == exp[1]
+    assert list(got.items()) == list(exp[0].items())

@@ -47,6 +47,7 @@ struct fr_ctx {
     // next call that synchronises (settle_finalize)
     u64* h_fin = nullptr;          // pinned: the finalize's live-slot count
     hipEvent_t fin_e0 = nullptr, fin_e1 = nullptr;
+    hipEvent_t cls_e0 = nullptr, cls_e1 = nullptr;  // fr_classify's timing (created once, not per call)
     bool fin_pending = false;
     u64 fin_expect = 0;
     bool st_fresh = false;         // h_st equals the device state (no device work on it since)
@@ -580,6 +581,8 @@ fr_ctx* fr_create(int device, uint64_t chunk_bytes, uint64_t table_slots) {
     if ((e = hipHostMalloc((void**)&ctx->h_fin, 64, hipHostMallocDefault)) != hipSuccess) return bad("pinned count", e);
     if ((e = hipEventCreate(&ctx->fin_e0)) != hipSuccess) return bad("event", e);
     if ((e = hipEventCreate(&ctx->fin_e1)) != hipSuccess) return bad("event", e);
+    if ((e = hipEventCreate(&ctx->cls_e0)) != hipSuccess) return bad("event", e);
+    if ((e = hipEventCreate(&ctx->cls_e1)) != hipSuccess) return bad("event", e);
     if ((e = hipHostMalloc((void**)&ctx->h_zero, sizeof(DevState), hipHostMallocDefault)) != hipSuccess)
         return bad("pinned reset state", e);
     std::memset(ctx->h_zero, 0, sizeof(DevState));
@@ -635,6 +638,8 @@ void fr_destroy(fr_ctx* ctx) {
     if (ctx->h_fin) (void)hipHostFree(ctx->h_fin);
     if (ctx->fin_e0) (void)hipEventDestroy(ctx->fin_e0);
     if (ctx->fin_e1) (void)hipEventDestroy(ctx->fin_e1);
+    if (ctx->cls_e0) (void)hipEventDestroy(ctx->cls_e0);
+    if (ctx->cls_e1) (void)hipEventDestroy(ctx->cls_e1);
     if (ctx->h_sheet) (void)hipHostFree(ctx->h_sheet);
     if (ctx->h_tab) (void)hipHostFree(ctx->h_tab);
     for (int i = 0; i < 2; ++i) {
@@ -1263,9 +1268,7 @@ int fr_classify(fr_ctx* ctx, int num_subs, int rc_mode, int16_t* m1, int16_t* m2
     const u64 n = ctx->U;
     int rc = ensure_class_scratch(ctx, n);
     if (rc) return rc;
-    hipEvent_t e0, e1;
-    CK(hipEventCreate(&e0));
-    CK(hipEventCreate(&e1));
+    hipEvent_t e0 = ctx->cls_e0, e1 = ctx->cls_e1;
     CK(hipMemsetAsync(ctx->d_errf, 0xFF, 8, ctx->stream));
     CK(hipMemsetAsync(ctx->d_rcf, 0, std::max(ctx->n_names, 1) * 8, ctx->stream));
     CK(hipMemsetAsync(ctx->d_rcr, 0, std::max(ctx->n_names, 1) * 8, ctx->stream));
@@ -1282,8 +1285,6 @@ int fr_classify(fr_ctx* ctx, int num_subs, int rc_mode, int16_t* m1, int16_t* m2
     float ms = 0;
     CK(hipEventElapsedTime(&ms, e0, e1));
     ctx->classify_ms = ms;
-    CK(hipEventDestroy(e0));
-    CK(hipEventDestroy(e1));
     if (err_unique) *err_unique = ef == ~0ull ? -1 : (int64_t)ef;
     if (err_which) {
         *err_which = 0;

@@ -72,6 +72,12 @@ struct fr_ctx {
     u64 chunk_bytes = 0;
     u64 ring_bytes = 0;
     u32 chunk_tiles = 80;  // tiles per full chunk of a ramped launch (FR_CHUNK_TILES; 64-96 measured within 2 %, 80 best)
+    // A context whose commits go to the launch log (many distinct codes per chunk: the config-3 shape)
+    // walks larger chunks from then on: fewer, bigger commits, all logged (FR_CHUNK_TILES_HEAVY; the
+    // config-3 shape's tally 1.61 -> 1.53 ms per launch at 112, config 2 never logs and keeps 80)
+    u32 chunk_tiles_heavy = 112;
+    bool heavy = false;
+    u64 chunks_since_reset = 0;  // chunks launched since the state's counters were zeroed
     bool ramp = true;      // FR_RAMP=0: one uniform chunk per workgroup
     u8* pin[2] = {nullptr, nullptr};
     u8* dbuf[2] = {nullptr, nullptr};
@@ -188,10 +194,18 @@ static u64 pow2_at_least(u64 x) {
     return p;
 }
 
+// a landed snapshot: at least a quarter of the chunks since the reset logged their commits -> heavy
+static void note_snapshot(fr_ctx* ctx) {
+    const u64 lc = ctx->h_st->log_commits;
+    if (lc && lc * 4 >= ctx->chunks_since_reset) ctx->heavy = true;
+}
+
 static int state_reset_counts(fr_ctx* ctx) {
     // the device copy comes from a pinned image that never changes, so nothing waits for it; the
     // host snapshot is overwritten only once no asynchronous snapshot can still land on it
     if (ctx->st_pending) CK(hipStreamSynchronize(ctx->stream));
+    note_snapshot(ctx);
+    ctx->chunks_since_reset = 0;
     *ctx->h_st = *ctx->h_zero;
     CK(hipMemcpyAsync(ctx->st, ctx->h_zero, sizeof(DevState), hipMemcpyHostToDevice, ctx->stream));
     ctx->st_pending = false;
@@ -205,6 +219,7 @@ static int read_state(fr_ctx* ctx) {  // exact snapshot (a host round trip only 
     CK(hipStreamSynchronize(ctx->stream));
     ctx->st_pending = false;
     ctx->st_fresh = true;
+    note_snapshot(ctx);
     return FR_OK;
 }
 
@@ -486,7 +501,7 @@ static int launch_range(fr_ctx* ctx, const u8* dptr, u64 len, u64 avail, int own
     CK(hipEventRecord(ctx->ev_a[ctx->ev_used], ctx->stream));
     // chunking (chunk_bounds in fr_kernels.hip): ramped when the range holds both ramps and a full
     // chunk, else one uniform chunk per workgroup
-    const u64 G = (u64)ctx->grid, C = ctx->chunk_tiles;
+    const u64 G = (u64)ctx->grid, C = ctx->heavy ? ctx->chunk_tiles_heavy : ctx->chunk_tiles;
     const u64 rg = G + ((C - 1) * G * (G + 1)) / (2 * G);  // R(G)
     if (ctx->ramp && (u64)a.num_tiles >= 2 * rg + C) {
         a.ramp_g = (u32)G;
@@ -520,6 +535,7 @@ static int launch_range(fr_ctx* ctx, const u8* dptr, u64 len, u64 avail, int own
     ctx->ev_used++;
     ctx->scan_launches++;
     ctx->scan_bytes += len;
+    ctx->chunks_since_reset += a.num_chunks;
     ctx->par ^= 1u;
     ctx->file_offset += len;
     ctx->max_file_bytes = std::max(ctx->max_file_bytes, ctx->file_offset);  // bounds every ordinal's offset
@@ -567,6 +583,7 @@ fr_ctx* fr_create(int device, uint64_t chunk_bytes, uint64_t table_slots) {
     }
     if (const char* f = getenv("FR_LOG_MIN")) ctx->log_min = (u32)std::max(0, atoi(f));
     if (const char* f = getenv("FR_CHUNK_TILES")) ctx->chunk_tiles = (u32)std::max(2, atoi(f));
+    if (const char* f = getenv("FR_CHUNK_TILES_HEAVY")) ctx->chunk_tiles_heavy = (u32)std::max(2, atoi(f));
     if (const char* f = getenv("FR_RAMP")) ctx->ramp = atoi(f) != 0;
     ctx->tiles_cap = RANGE_MAX / TSTEP + 2;
     ctx->nslots = pow2_at_least(std::max<u64>(table_slots, 1024));

@@ -106,6 +106,7 @@ struct DevState {
     u32 spin_max;        // diagnostics: longest look-back wait (polls)
     u64 spin_total;      // diagnostics: total look-back polls that found a window not ready
     u64 log_n;           // entries appended to the launch log (may exceed its capacity: the rest went to HBM)
+    u64 log_commits;     // commits that went to the launch log since the last reset (never emptied by the aggregation)
     u64 stamp[8];        // diagnostics (FR_STAMPS builds only): per-phase shader cycles, summed over workgroups
 };
 

@@ -971,6 +971,7 @@ __device__ __attribute__((noinline)) void commit_buffers(ScanShared& sh, const S
         // launch_log_aggregate); a block past the log's end is blanked and the pairs inserted below
         if (tid == 0) {
             const u64 base = atomicAdd((unsigned long long*)&a.st->log_n, (unsigned long long)(nl + nc));
+            atomicAdd((unsigned long long*)&a.st->log_commits, 1ull);
             sh.log_base = base + nl + nc <= a.log_cap ? base : ~0ull;
             sh.log_pos = 0;
             if (base + nl + nc > a.log_cap)

@@ -520,12 +520,13 @@ class Context:
         return t
 
     def diag(self) -> dict:
-        v = np.zeros(18, dtype=np.uint64)
-        self._ck(lib.fr_get_diag(self.h, _ptr(v), 18), "fr_get_diag")
+        v = np.zeros(19, dtype=np.uint64)
+        self._ck(lib.fr_get_diag(self.h, _ptr(v), 19), "fr_get_diag")
         d = dict(zip(("spin_max", "spin_total", "keys", "overflow", "presence", "exotic", "grid", "slots"),
                      v[:8].tolist()))
         d["spec_replays"] = int(v[16])
         d["exo_replays"] = int(v[17])
+        d["chunk_tiles"] = int(v[18])  # full-chunk size of ramped launches now (larger once commits log)
         if v[8:16].any():  # FR_TIMING build / FR_ABLATE=64: per-phase cycles or commit counts
             names = (("lookback", "barrier", "headers", "parse", "stage", "count", "flush", "prologue")
                      if os.environ.get("FR_KERNEL") == "0" else

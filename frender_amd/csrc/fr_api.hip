@@ -682,7 +682,8 @@ int fr_get_diag(fr_ctx* ctx, uint64_t* out, int n) {
     const DevState& s = *ctx->h_st;
     const uint64_t v[] = {s.spin_max,   s.spin_total, s.n_keys,   s.n_overflow, s.n_presence, s.n_exotic,
                           (uint64_t)ctx->grid, ctx->nslots, s.stamp[0], s.stamp[1], s.stamp[2], s.stamp[3],
-                          s.stamp[4],  s.stamp[5],  s.stamp[6], s.stamp[7], ctx->spec_replays, ctx->exo_replays};
+                          s.stamp[4],  s.stamp[5],  s.stamp[6], s.stamp[7], ctx->spec_replays, ctx->exo_replays,
+                          ctx->heavy ? ctx->chunk_tiles_heavy : ctx->chunk_tiles};
     for (int i = 0; i < n && i < (int)(sizeof(v) / sizeof(v[0])); ++i) out[i] = v[i];
     return FR_OK;
 }

@@ -188,6 +188,41 @@ def test_launch_log_commits(lib, monkeypatch, log_min):
             c.close()
 
 
+@pytest.mark.skip(reason="written when no GPU box was available; run on hardware, then unskip")
+def test_heavy_chunk_switch(lib, monkeypatch):
+    """A context whose commits all go to the launch log switches its ramped launches to the heavy
+    chunk size after the first landed snapshot (fr_api.hip note_snapshot).  A 6-workgroup grid makes
+    1 MiB launches ramped; the tally over both chunk sizes must equal the oracle's."""
+    from frender_amd import synth
+    from oracle.frender_oracle import tally_text
+    monkeypatch.setenv("FR_GRID", "6")
+    monkeypatch.setenv("FR_LOG_MIN", "0")
+    monkeypatch.setenv("FR_CHUNK_TILES", "5")
+    monkeypatch.setenv("FR_CHUNK_TILES_HEAVY", "7")
+    c = lib.Context(device=0, chunk_bytes=1 << 20, table_slots=1 << 16)
+    try:
+        assert c.diag()["chunk_tiles"] == 5
+        sheet = synth.make_sheet(384, 10, 10)
+        n = 300_000
+        host = synth.generate_bytes(sheet, 0, n, R=8, seed=4)
+        p = c.device_alloc(len(host))
+        c.synth_device(p, 0, n, 8, 4, sheet.idx1, sheet.idx2)
+        for _ in range(2):  # the second pass starts heavy
+            c.reset()
+            c.begin_file(None)
+            c.feed_device(p, len(host))
+            st = c.end_file()
+            assert st.records == n and st.error == 0
+            c.finalize()
+            keys, counts, first = c.unique()
+            exp, _ = tally_text(host.decode())
+            assert list(zip(lib.decode_keys(keys), counts.tolist())) == list(exp.items())
+        c.device_free(p)
+        assert c.diag()["chunk_tiles"] == 7
+    finally:
+        c.close()
+
+
 def test_table_growth_and_overflow(lib):
     """Start from a 1024-slot table with ~60k distinct codes: the table must grow
     between launches (overflow list absorbs in-flight inserts) and stay exact."""

@@ -40,6 +40,8 @@ def main(argv=None):
                    default=f"./frender-demux-output_{datetime.strftime(datetime.now(timezone.utc), '%Y-%M-%d_%H%M_%Z')}/",
                    help="output directory (default: ./frender-demux-output_{date_time}/)")
     d.add_argument("-r", metavar="result_file", required=True, help="REQUIRED: frender scan result file")
+    d.add_argument("--strict-header", action="store_true",
+                   help="reject a results file in scan's own column order, as frender.py does (default: accept it)")
     d.add_argument("--gz-level", type=int, default=9,
                    help="gzip level of the outputs (the reference writes gzip.open's default, 9)")
     d.add_argument("files", nargs="+", help="Fastq file, list of fastq files, or directory path")
@@ -108,9 +110,12 @@ def run_rank(args) -> int:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         dist.init_process_group(backend)
+    from .dist import PeerFailed
     try:
         from .scan import frender_scan
         frender_scan(args)
+    except PeerFailed:  # rank 0 raises the reference's exception; this rank just fails
+        return 1
     finally:
         dist.destroy_process_group()
     return 0

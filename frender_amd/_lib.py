@@ -85,6 +85,9 @@ _SIGS = {
     # native inflate (row f-2)
     "fr_gz_open": (P, [C.POINTER(C.c_char_p), C.c_int, C.c_int]),
     "fr_gz_feed": (C.c_int, [P, C.c_int, P]),
+    "fr_gz_feed_part": (C.c_int, [P, C.c_int, P, C.c_int64, C.c_int, C.c_int, C.c_uint64, C.POINTER(C.c_uint64)]),
+    "fr_gz_size_hint": (C.c_uint64, [C.c_char_p]),
+    "fr_gz_part_bounds": (C.c_int, [C.c_char_p, C.c_int, C.c_uint64, C.POINTER(C.c_uint64)]),
     "fr_gz_error": (C.c_char_p, [P]),
     "fr_gz_close": (None, [P]),
     # demux (row f-1)
@@ -233,6 +236,32 @@ class GzPool:
             raise FrenderError(f"fr_gz_feed failed ({rc}): {lib.fr_gz_error(self.h).decode(errors='replace')}")
         return rc == FR_SAMPLE_DONE
 
+    def _feed_part(self, i: int, ctx_handle, file_index: int, part: int, nparts: int, hint: int) -> int:
+        base = C.c_uint64(0)
+        rc = lib.fr_gz_feed_part(self.h, i, ctx_handle, int(file_index), int(part), int(nparts), int(hint),
+                                 C.byref(base))
+        if rc == FR_ERR_IO:
+            raise GzError(lib.fr_gz_error(self.h).decode(errors="replace"))
+        if rc != FR_OK:
+            raise FrenderError(f"fr_gz_feed_part failed ({rc}): {lib.fr_gz_error(self.h).decode(errors='replace')}")
+        return int(base.value)
+
+    @staticmethod
+    def part_bounds(path, nparts: int, hint: int) -> list:
+        """fr_gz_part_bounds: the record-aligned cuts [b_0 = 0, ..., b_nparts = size] of the file."""
+        out = (C.c_uint64 * (nparts + 1))()
+        rc = lib.fr_gz_part_bounds(os.fsencode(str(path)), int(nparts), int(hint), out)
+        if rc == FR_ERR_IO:
+            raise GzError(f"{path}: not a valid gzip stream")
+        if rc != FR_OK:
+            raise FrenderError(f"fr_gz_part_bounds failed ({rc})")
+        return [int(x) for x in out]
+
+    @staticmethod
+    def size_hint(path) -> int:
+        """fr_gz_size_hint: the decoded size the file's trailers promise (deterministic)."""
+        return int(lib.fr_gz_size_hint(os.fsencode(str(path))))
+
     def close(self):
         if self.h:
             lib.fr_gz_close(self.h)
@@ -315,6 +344,7 @@ class Context:
     """One GPU's scan state (fr_ctx)."""
 
     def __init__(self, device: int = 0, chunk_bytes: int = 256 << 20, table_slots: int = 1 << 20):
+        self.device = int(device)
         self.h = lib.fr_create(device, chunk_bytes, table_slots)
         if not self.h:
             raise FrenderError("fr_create returned NULL")
@@ -403,6 +433,11 @@ class Context:
     def feed_gz(self, pool: "GzPool", i: int) -> bool:
         """Feed file i of a native inflate pool (GzPool); True once the -s sample is complete."""
         return pool._feed(i, self.h)
+
+    def feed_gz_part(self, pool: "GzPool", i: int, file_index: int, part: int, nparts: int, hint: int) -> int:
+        """Begin file_index at part `part` of `nparts` of pool file i's records and feed that part
+        (fr_gz_feed_part; call fr_end_file after); returns the part's byte base."""
+        return pool._feed_part(i, self.h, file_index, part, nparts, hint)
 
     def feed_device(self, dev_ptr: int, nbytes: int):
         self._ck(lib.fr_feed_device(self.h, P(dev_ptr), nbytes), "fr_feed_device")
@@ -520,17 +555,18 @@ class Context:
         return t
 
     def diag(self) -> dict:
-        v = np.zeros(19, dtype=np.uint64)
-        self._ck(lib.fr_get_diag(self.h, _ptr(v), 19), "fr_get_diag")
+        v = np.zeros(20, dtype=np.uint64)
+        self._ck(lib.fr_get_diag(self.h, _ptr(v), 20), "fr_get_diag")
         d = dict(zip(("spin_max", "spin_total", "keys", "overflow", "presence", "exotic", "grid", "slots"),
                      v[:8].tolist()))
         d["spec_replays"] = int(v[16])
         d["exo_replays"] = int(v[17])
-        d["chunk_tiles"] = int(v[18])  # full-chunk size of ramped launches now (larger once commits log)
+        d["chunk_tiles"] = int(v[18])  # full-chunk size of the next ramped launch (larger once commits log)
+        d["heavy_launches"] = int(v[19])  # ramped launches since the reset that walked the heavy chunk size
         if v[8:16].any():  # FR_TIMING build / FR_ABLATE=64: per-phase cycles or commit counts
             names = (("lookback", "barrier", "headers", "parse", "stage", "count", "flush", "prologue")
                      if os.environ.get("FR_KERNEL") == "0" else
-                     ("classify", "barriers", "parse", "tiles", "walk", "kernel", "guess", "commit"))
+                     ("guess", "walk0", "wait0", "resolve", "walk1", "commit", "kernel", "chunks"))
             d["stamps"] = dict(zip(names, v[8:].tolist()))
         return d
 
@@ -544,3 +580,24 @@ class Context:
     def merge_unique_device(self, keys_ptr: int, counts_ptr: int, first_ptr: int, n: int):
         self._ck(lib.fr_merge_unique_device(self.h, P(keys_ptr), P(counts_ptr), P(first_ptr), n),
                  "fr_merge_unique_device")
+
+    # ---- tensor views for the multi-GPU merge (frender_amd/dist.py) ----------------------
+    def export_rows(self, device):
+        """The finalized table as an int64 tensor [U, 3] of (key, count, first) rows on `device`
+        (this GPU's HBM: fr_export_unique_device; "cpu" stages through it for gloo rehearsals)."""
+        U = int(self.U)
+        cols = torch.empty((3, max(U, 1)), dtype=torch.int64, device=torch.device("cuda", self.device))
+        if U:
+            self.export_unique_device(cols[0].data_ptr(), cols[1].data_ptr(), cols[2].data_ptr(), U)
+        return cols[:, :U].t().to(device)
+
+    def merge_rows(self, rows):
+        """Merge (key, count, first) rows [n, 3] into this context's table (count = sum, first = min:
+        fr_merge_unique_device); the rows may live on any device."""
+        n = int(rows.shape[0])
+        if not n:
+            return
+        cols = rows.t().contiguous().to(torch.device("cuda", self.device))
+        torch.cuda.current_stream(cols.device).synchronize()  # a transfer on torch's stream has landed
+        self.merge_unique_device(cols[0].data_ptr(), cols[1].data_ptr(), cols[2].data_ptr(), n)
+        self.sync()  # cols goes back to torch's allocator after this

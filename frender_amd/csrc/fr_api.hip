@@ -71,13 +71,14 @@ struct fr_ctx {
     // go through a pinned ring of ring_bytes slots (<= HOST_CHUNK_MAX)
     u64 chunk_bytes = 0;
     u64 ring_bytes = 0;
-    u32 chunk_tiles = 80;  // tiles per full chunk of a ramped launch (FR_CHUNK_TILES; 64-96 measured within 2 %, 80 best)
-    // A context whose commits go to the launch log (many distinct codes per chunk: the config-3 shape)
-    // walks larger chunks from then on: fewer, bigger commits, all logged (FR_CHUNK_TILES_HEAVY; the
-    // config-3 shape's tally 1.61 -> 1.53 ms per launch at 112, config 2 never logs and keeps 80)
-    u32 chunk_tiles_heavy = 112;
-    bool heavy = false;
-    u64 chunks_since_reset = 0;  // chunks launched since the state's counters were zeroed
+    u32 chunk_tiles = 320;  // wave-tiles (4 KiB) per full chunk of a ramped launch (FR_CHUNK_TILES; round 2's
+                            // 80 workgroup tiles of 16 KiB: 64-96 measured within 2 %, 80 best)
+    // Ramped launches after one in which at least a quarter of the chunks since the reset logged their
+    // commits (many distinct codes per chunk: the config-3 shape) walk larger chunks: fewer, bigger
+    // commits, all logged (FR_CHUNK_TILES_HEAVY; the config-3 shape's tally 1.61 -> 1.53 ms per launch at
+    // 112, config 2 never logs and keeps 80).  The device decides (DevState::heavy, note_commit in
+    // fr_kernels.hip); fr_reset clears it.
+    u32 chunk_tiles_heavy = 448;
     bool ramp = true;      // FR_RAMP=0: one uniform chunk per workgroup
     u8* pin[2] = {nullptr, nullptr};
     u8* dbuf[2] = {nullptr, nullptr};
@@ -194,18 +195,10 @@ static u64 pow2_at_least(u64 x) {
     return p;
 }
 
-// a landed snapshot: at least a quarter of the chunks since the reset logged their commits -> heavy
-static void note_snapshot(fr_ctx* ctx) {
-    const u64 lc = ctx->h_st->log_commits;
-    if (lc && lc * 4 >= ctx->chunks_since_reset) ctx->heavy = true;
-}
-
 static int state_reset_counts(fr_ctx* ctx) {
     // the device copy comes from a pinned image that never changes, so nothing waits for it; the
     // host snapshot is overwritten only once no asynchronous snapshot can still land on it
     if (ctx->st_pending) CK(hipStreamSynchronize(ctx->stream));
-    note_snapshot(ctx);
-    ctx->chunks_since_reset = 0;
     *ctx->h_st = *ctx->h_zero;
     CK(hipMemcpyAsync(ctx->st, ctx->h_zero, sizeof(DevState), hipMemcpyHostToDevice, ctx->stream));
     ctx->st_pending = false;
@@ -219,7 +212,6 @@ static int read_state(fr_ctx* ctx) {  // exact snapshot (a host round trip only 
     CK(hipStreamSynchronize(ctx->stream));
     ctx->st_pending = false;
     ctx->st_fresh = true;
-    note_snapshot(ctx);
     return FR_OK;
 }
 
@@ -417,6 +409,7 @@ static int replay_exotic(fr_ctx* ctx) {
     a.log = nullptr;
     a.epoch = ++ctx->epoch;
     a.tab = ctx->d_tab;
+    a.tabv = ctx->tab;
     CK(hipMemsetAsync(&ctx->st->ticket, 0, 2 * sizeof(u32), ctx->stream));  // ticket, chunks_done
     rc = launch_args(ctx, a, ctx->last_grid);
     if (rc) return rc;
@@ -482,6 +475,7 @@ static int launch_range(fr_ctx* ctx, const u8* dptr, u64 len, u64 avail, int own
     rc = upload_table(ctx);
     if (rc) return rc;
     a.tab = ctx->d_tab;
+    a.tabv = ctx->tab;
     if (ctx->epoch >= 0x7FFFFFFFu) {  // tag wrap: restart epochs on a cleared descriptor array
         CK(hipMemsetAsync(ctx->tiles, 0, ctx->tiles_cap * sizeof(u64), ctx->stream));
         ctx->epoch = 1;
@@ -500,14 +494,21 @@ static int launch_range(fr_ctx* ctx, const u8* dptr, u64 len, u64 avail, int own
     }
     CK(hipEventRecord(ctx->ev_a[ctx->ev_used], ctx->stream));
     // chunking (chunk_bounds in fr_kernels.hip): ramped when the range holds both ramps and a full
-    // chunk, else one uniform chunk per workgroup
-    const u64 G = (u64)ctx->grid, C = ctx->heavy ? ctx->chunk_tiles_heavy : ctx->chunk_tiles;
-    const u64 rg = G + ((C - 1) * G * (G + 1)) / (2 * G);  // R(G)
+    // chunk, else one uniform chunk per workgroup.  A ramped launch also carries the heavy geometry
+    // when the range fits it; the kernel picks one (DevState::heavy)
+    const u64 G = (u64)ctx->grid, C = ctx->chunk_tiles, Ch = ctx->chunk_tiles_heavy;
+    auto ramp_tiles = [&](u64 c) { return G + ((c - 1) * G * (G + 1)) / (2 * G); };  // R(G) at chunk size c
+    const u64 rg = ramp_tiles(C), rgh = ramp_tiles(Ch);
     if (ctx->ramp && (u64)a.num_tiles >= 2 * rg + C) {
         a.ramp_g = (u32)G;
         a.chunk_tiles = (u32)C;
         a.mid_chunks = (u32)(((u64)a.num_tiles - 2 * rg + C - 1) / C);
         a.num_chunks = (u32)(2 * G) + a.mid_chunks;
+        if (Ch != C && (u64)a.num_tiles >= 2 * rgh + Ch) {
+            a.chunk_tiles_h = (u32)Ch;
+            a.mid_chunks_h = (u32)(((u64)a.num_tiles - 2 * rgh + Ch - 1) / Ch);
+            a.num_chunks_h = (u32)(2 * G) + a.mid_chunks_h;
+        }
     } else {
         a.ramp_g = 0;
         a.mid_chunks = 0;
@@ -535,7 +536,6 @@ static int launch_range(fr_ctx* ctx, const u8* dptr, u64 len, u64 avail, int own
     ctx->ev_used++;
     ctx->scan_launches++;
     ctx->scan_bytes += len;
-    ctx->chunks_since_reset += a.num_chunks;
     ctx->par ^= 1u;
     ctx->file_offset += len;
     ctx->max_file_bytes = std::max(ctx->max_file_bytes, ctx->file_offset);  // bounds every ordinal's offset
@@ -683,7 +683,8 @@ int fr_get_diag(fr_ctx* ctx, uint64_t* out, int n) {
     const uint64_t v[] = {s.spin_max,   s.spin_total, s.n_keys,   s.n_overflow, s.n_presence, s.n_exotic,
                           (uint64_t)ctx->grid, ctx->nslots, s.stamp[0], s.stamp[1], s.stamp[2], s.stamp[3],
                           s.stamp[4],  s.stamp[5],  s.stamp[6], s.stamp[7], ctx->spec_replays, ctx->exo_replays,
-                          ctx->heavy ? ctx->chunk_tiles_heavy : ctx->chunk_tiles};
+                          s.heavy[ctx->par] ? ctx->chunk_tiles_heavy : ctx->chunk_tiles,  // the next ramped launch's
+                          s.heavy_launches};
     for (int i = 0; i < n && i < (int)(sizeof(v) / sizeof(v[0])); ++i) out[i] = v[i];
     return FR_OK;
 }

@@ -13,10 +13,17 @@
 // then re-reads the file through Python's gzip to raise the reference's own exception.
 //
 // Fast path: when the image has libdeflate (whole-buffer DEFLATE, 2-3x zlib's inflate speed; loaded
-// with dlopen, so the library is optional), a file of up to 256 MiB compressed is decompressed
-// whole, member by member, and queued in one piece.  Anything unusual -- bytes after a member that
-// are neither NUL padding nor a new member, a member libdeflate rejects, more than 1 GiB of output --
-// falls back to the zlib stream, which owns the exact rules and errors above.
+// with dlopen, so the library is optional), a file of up to 256 MiB compressed whose last member's
+// ISIZE trailer promises at most 1 GiB is decompressed whole, member by member, and queued in one
+// piece; a BGZF file (every member carries its size) is decoded member-parallel in windows of
+// BGZF_WINDOW output bytes.  Anything unusual -- bytes after a member that are neither NUL padding
+// nor a new member, a member libdeflate rejects, more output than promised, a BGZF header field out
+// of the format's bounds -- falls back to the zlib stream, which owns the exact rules and errors above.
+//
+// Memory and threads are bounded per pool: whole-file buffers (input + output) draw on a shared
+// budget of WHOLE_BUDGET bytes (a file that does not fit streams through zlib instead), and the
+// helper threads of a BGZF decode come out of the pool's own thread count (the workers that are
+// idle), so at most `threads` threads inflate at once.
 #include <dlfcn.h>
 #include <sys/stat.h>
 #include <zlib.h>
@@ -29,6 +36,8 @@
 #include <cstring>
 #include <deque>
 #include <mutex>
+#include <new>
+#include <stdexcept>
 #include <string>
 #include <thread>
 #include <vector>
@@ -50,6 +59,8 @@ struct GzFile {
 struct fr_gz {
     std::vector<GzFile> files;
     int threads = 1;
+    int busy = 0;          // threads inflating now (workers + BGZF helpers), <= threads
+    size_t whole_used = 0; // bytes of whole-file buffers held now (<= WHOLE_BUDGET)
     size_t block = 16u << 20;
     size_t depth = 3;  // blocks queued per file (set by fr_gz_open)
     std::mutex m;
@@ -89,6 +100,9 @@ const Libdeflate* libdeflate() {
 constexpr size_t LD_MAX_IN = 256ull << 20;   // compressed bytes a file may have for the fast path
 constexpr size_t LD_MAX_OUT = 1ull << 30;    // decoded bytes it may produce
 constexpr size_t BGZF_MAX_IN = 1ull << 30;   // BGZF files: compressed bytes for the parallel path
+constexpr size_t BGZF_MAX_BLOCK = 65536;     // the format's bound on a member's size and ISIZE
+constexpr size_t BGZF_WINDOW = 64ull << 20;  // decoded bytes per parallel BGZF window
+constexpr size_t WHOLE_BUDGET = 3ull << 30;  // whole-file buffers (input + output) held at once per pool
 
 struct Member {
     size_t off, len, dst, isize;
@@ -116,13 +130,15 @@ bool bgzf_members(const std::vector<uint8_t>& in, std::vector<Member>& ms) {
         const size_t xlen = le16(&in[pos + 10]);
         if (n - pos < 12 + xlen) return false;
         size_t bsize = 0;
-        for (size_t q = pos + 12; q + 4 <= pos + 12 + xlen;) {
+        const size_t xend = pos + 12 + xlen;
+        for (size_t q = pos + 12; q + 4 <= xend;) {
             const size_t slen = le16(&in[q + 2]);
-            if (in[q] == 'B' && in[q + 1] == 'C' && slen == 2) bsize = le16(&in[q + 4]) + 1;
+            if (in[q] == 'B' && in[q + 1] == 'C' && slen == 2 && q + 6 <= xend) bsize = le16(&in[q + 4]) + 1;
             q += 4 + slen;
         }
-        if (bsize < 12 + xlen + 8 || n - pos < bsize) return false;
+        if (bsize < 12 + xlen + 8 || bsize > BGZF_MAX_BLOCK || n - pos < bsize) return false;
         const size_t isize = le32(&in[pos + bsize - 4]);
+        if (isize > BGZF_MAX_BLOCK) return false;
         ms.push_back(Member{pos, bsize, dst, isize});
         dst += isize;
         pos += bsize;
@@ -130,10 +146,24 @@ bool bgzf_members(const std::vector<uint8_t>& in, std::vector<Member>& ms) {
     return !ms.empty();
 }
 
-// decode BGZF members in parallel (`threads` helpers, each with its own decompressor) into out
-bool bgzf_decode(const Libdeflate* ld, const std::vector<uint8_t>& in, const std::vector<Member>& ms,
-                 std::vector<uint8_t>& out, int threads) {
-    std::atomic<size_t> next{0};
+// Take up to `want` idle thread slots of the pool (BGZF helpers); returns how many were taken.
+int take_threads(fr_gz* g, int want) {
+    std::lock_guard<std::mutex> lk(g->m);
+    const int k = std::max(0, std::min(want, g->threads - g->busy));
+    g->busy += k;
+    return k;
+}
+void give_threads(fr_gz* g, int k) {
+    std::lock_guard<std::mutex> lk(g->m);
+    g->busy -= k;
+    g->cv.notify_all();
+}
+
+// decode BGZF members [k0, k1) in parallel into out (member m lands at m.dst - base): this thread
+// plus the pool's idle threads, each with its own decompressor
+bool bgzf_decode(fr_gz* g, const Libdeflate* ld, const std::vector<uint8_t>& in, const std::vector<Member>& ms,
+                 size_t k0, size_t k1, size_t base, uint8_t* out) {
+    std::atomic<size_t> next{k0};
     std::atomic<bool> ok{true};
     auto run = [&]() {
         void* d = ld->alloc();
@@ -141,19 +171,33 @@ bool bgzf_decode(const Libdeflate* ld, const std::vector<uint8_t>& in, const std
             ok = false;
             return;
         }
-        for (size_t k; ok && (k = next.fetch_add(1)) < ms.size();) {
+        for (size_t k; ok && (k = next.fetch_add(1)) < k1;) {
             const Member& m = ms[k];
             size_t used = 0, produced = 0;
-            const int r = ld->gzip_ex(d, in.data() + m.off, m.len, out.data() + m.dst, m.isize, &used, &produced);
+            const int r = ld->gzip_ex(d, in.data() + m.off, m.len, out + (m.dst - base), m.isize, &used, &produced);
             if (r != 0 || used != m.len || produced != m.isize) ok = false;
         }
         ld->release(d);
     };
+    const int nh = take_threads(g, (int)std::min<size_t>(k1 - k0, 64) - 1);
     std::vector<std::thread> helpers;
-    for (int t = 1; t < threads; ++t) helpers.emplace_back(run);
+    for (int t = 0; t < nh; ++t) helpers.emplace_back(run);
     run();
     for (auto& h : helpers) h.join();
+    give_threads(g, nh);
     return ok;
+}
+
+// hold `bytes` of the pool's whole-file budget (false: it does not fit now; stream instead)
+bool take_budget(fr_gz* g, size_t bytes) {
+    std::lock_guard<std::mutex> lk(g->m);
+    if (g->whole_used + bytes > WHOLE_BUDGET) return false;
+    g->whole_used += bytes;
+    return true;
+}
+void give_budget(fr_gz* g, size_t bytes) {
+    std::lock_guard<std::mutex> lk(g->m);
+    g->whole_used -= bytes;
 }
 
 // the libdeflate fast path: true when the whole file was decoded and queued (or the scan cancelled
@@ -164,6 +208,12 @@ bool inflate_whole(fr_gz* g, GzFile& f) {
     struct stat sb;
     if (stat(f.path.c_str(), &sb) != 0 || (size_t)sb.st_size > std::max(LD_MAX_IN, BGZF_MAX_IN)) return false;
     const size_t n = (size_t)sb.st_size;
+    if (!take_budget(g, n)) return false;
+    struct Hold {  // the input's share of the budget, returned on every path
+        fr_gz* g;
+        size_t b;
+        ~Hold() { give_budget(g, b); }
+    } hold{g, n};
     std::vector<uint8_t> in(n);
     FILE* fp = fopen(f.path.c_str(), "rb");
     if (!fp) return false;
@@ -171,19 +221,48 @@ bool inflate_whole(fr_gz* g, GzFile& f) {
     fclose(fp);
     if (got != n) return false;
     std::vector<Member> ms;
-    if (bgzf_members(in, ms)) {  // members split across the pool's thread count
-        std::vector<uint8_t> out(ms.back().dst + ms.back().isize);
-        if (!bgzf_decode(ld, in, ms, out, g->threads)) return false;
-        std::unique_lock<std::mutex> lk(g->m);
-        if (f.cancel || g->stop) return true;
-        if (!out.empty()) f.q.push_back(std::move(out));
-        g->cv.notify_all();
+    if (bgzf_members(in, ms)) {  // member-parallel, one window of about BGZF_WINDOW output bytes at a time
+        size_t k0 = 0;
+        while (k0 < ms.size()) {
+            size_t k1 = k0;
+            while (k1 < ms.size() && ms[k1].dst + ms[k1].isize - ms[k0].dst <= BGZF_WINDOW) ++k1;
+            if (k1 == k0) ++k1;
+            const size_t base = ms[k0].dst, len = ms[k1 - 1].dst + ms[k1 - 1].isize - base;
+            std::vector<uint8_t> out;
+            {  // wait for room in the file's queue (bounded memory), then decode the window
+                std::unique_lock<std::mutex> lk(g->m);
+                g->cv.wait(lk, [&] { return f.q.size() < g->depth || f.cancel || g->stop; });
+                if (f.cancel || g->stop) return true;
+                if (!g->spare.empty()) {
+                    out = std::move(g->spare.back());
+                    g->spare.pop_back();
+                }
+            }
+            out.resize(len);
+            if (!bgzf_decode(g, ld, in, ms, k0, k1, base, out.data())) {
+                if (k0 == 0) return false;  // nothing queued yet: the zlib stream redoes the file
+                std::lock_guard<std::mutex> lk(g->m);  // windows already queued: the file is bad
+                f.err = "bgzf member failed to decode";
+                g->cv.notify_all();
+                return true;
+            }
+            std::lock_guard<std::mutex> lk(g->m);
+            if (f.cancel || g->stop) return true;
+            if (len) f.q.push_back(std::move(out));
+            g->cv.notify_all();
+            k0 = k1;
+        }
         return true;
     }
-    if (n > LD_MAX_IN) return false;
+    if (n > LD_MAX_IN || n < 18) return false;
+    // the last member's ISIZE (decoded length mod 2^32): a file that will not fit LD_MAX_OUT streams
+    const size_t hint = le32(&in[n - 4]);
+    const size_t cap = std::min(LD_MAX_OUT, std::max<size_t>({hint + 4096, 4 * n, 1u << 20}));
+    if (hint > LD_MAX_OUT || !take_budget(g, cap)) return false;
+    Hold hold_out{g, cap};
     void* d = ld->alloc();
     if (!d) return false;
-    std::vector<uint8_t> out(std::min(LD_MAX_OUT, std::max<size_t>(4 * n, 1u << 20)));
+    std::vector<uint8_t> out(cap);
     size_t len = 0, pos = 0;
     bool ok = true;
     while (ok) {
@@ -195,18 +274,22 @@ bool inflate_whole(fr_gz* g, GzFile& f) {
         }
         for (;;) {
             size_t used = 0, produced = 0;
-            const int r = ld->gzip_ex(d, in.data() + pos, n - pos, out.data() + len, out.size() - len, &used, &produced);
+            const int r =
+                ld->gzip_ex(d, in.data() + pos, n - pos, out.data() + len, out.size() - len, &used, &produced);
             if (r == 0) {  // LIBDEFLATE_SUCCESS
                 len += produced;
                 pos += used;
                 break;
             }
-            if (r == 3 && out.size() < LD_MAX_OUT) {  // LIBDEFLATE_INSUFFICIENT_SPACE: a bigger buffer, again
-                out.resize(std::min(LD_MAX_OUT, 2 * out.size()));
-                continue;
+            // LIBDEFLATE_INSUFFICIENT_SPACE (a multi-member file: ISIZE covered only its last member):
+            // a bigger buffer within LD_MAX_OUT and the pool's budget, else the zlib stream
+            const size_t more = std::min(LD_MAX_OUT, 2 * out.size()) - out.size();
+            if (r != 3 || more == 0 || !take_budget(g, more)) {
+                ok = false;
+                break;
             }
-            ok = false;
-            break;
+            hold_out.b += more;
+            out.resize(out.size() + more);
         }
     }
     ld->release(d);
@@ -220,9 +303,12 @@ bool inflate_whole(fr_gz* g, GzFile& f) {
 }
 
 // inflate one file into g->files[i].q (blocks of g->block bytes); returns "" or an error text
-std::string inflate_file(fr_gz* g, int i) {
+std::string inflate_stream(fr_gz* g, int i) {
     GzFile& f = g->files[i];
-    if (inflate_whole(g, f)) return "";
+    if (inflate_whole(g, f)) {
+        std::lock_guard<std::mutex> lk(g->m);
+        return f.err;
+    }
     FILE* fp = fopen(f.path.c_str(), "rb");
     if (!fp) return "cannot open " + f.path;
     std::vector<uint8_t> in(4u << 20);
@@ -319,19 +405,34 @@ std::string inflate_file(fr_gz* g, int i) {
     return err;
 }
 
+// a failed allocation (a huge or corrupt file) ends that file with an error, which the host replays
+// through Python's gzip for the reference's exception, instead of terminating the process
+std::string inflate_file(fr_gz* g, int i) {
+    try {
+        return inflate_stream(g, i);
+    } catch (const std::bad_alloc&) {
+        return "out of memory while inflating";
+    } catch (const std::exception& e) {
+        return std::string("inflate: ") + e.what();
+    }
+}
+
 void worker(fr_gz* g) {
     for (;;) {
         int i;
         {
             std::unique_lock<std::mutex> lk(g->m);
             g->cv.wait(lk, [&] {
-                return g->stop || (g->next < (int)g->files.size() && g->next < g->consume + g->threads);
+                return g->stop || (g->next < (int)g->files.size() && g->next < g->consume + g->threads &&
+                                   g->busy < g->threads);
             });
             if (g->stop) return;
             i = g->next++;
+            g->busy++;
         }
         std::string err = inflate_file(g, i);
         std::lock_guard<std::mutex> lk(g->m);
+        g->busy--;
         g->files[i].err = err;
         g->files[i].done = true;
         g->cv.notify_all();
@@ -399,6 +500,258 @@ int fr_gz_feed(fr_gz* g, int i, fr_ctx* ctx) {
         }
     }
 }
+
+// ---- record-aligned parts of one file (multi-GPU scans of fewer files than GPUs) ----------------
+// Part j of k of a decoded stream covers [b_j, b_{j+1}): b_0 = 0, b_k = the end and, for 0 < j < k,
+// b_j is the first record start at or after j * hint / k, a record start being a line start whose
+// line index from the file start is 0 mod 4 under the reference's universal newlines (frender.py:159:
+// '\n', '\r\n' and a lone '\r' each end a line).  `hint` (fr_gz_size_hint) depends on the file alone,
+// so every rank that owns a part of the file cuts it the same way.
+
+}  // extern "C"
+
+namespace {
+
+struct Cutter {
+    uint64_t target[2];  // the part's two cut targets (b_part, b_part+1)
+    uint64_t cut[2];
+    int found = 0;       // cuts found so far (in order)
+    uint64_t pos = 0;    // bytes consumed
+    uint64_t lines = 0;  // terminators in [0, pos), except a '\r' at pos - 1 still pending
+    bool pend_cr = false;
+
+    // a line start at p with line index L
+    void line_start(uint64_t p, uint64_t L) {
+        while (found < 2 && p >= target[found] && (L & 3u) == 0) cut[found++] = p;
+    }
+    // consume [pos, pos + n) of the stream; returns when both cuts are found or the block is used up
+    void consume(const uint8_t* b, size_t n) {
+        size_t i = 0;
+        while (i < n && found < 2) {
+            if (!pend_cr) {  // fast part: '\n' only, no cut due before the block's byte t - 1
+                const uint64_t t = target[found];
+                const size_t fast_end = t > pos + 1 ? (size_t)std::min<uint64_t>(n, t - 1 - pos + i) : i;
+                if (fast_end > i && !std::memchr(b + i, '\r', fast_end - i)) {
+                    lines += (uint64_t)std::count(b + i, b + fast_end, (uint8_t)'\n');
+                    pos += fast_end - i;
+                    i = fast_end;
+                    continue;
+                }
+            }
+            const uint8_t c = b[i];
+            if (pend_cr) {  // byte pos - 1 was '\r': a terminator unless this byte is '\n'
+                pend_cr = false;
+                if (c != '\n') {
+                    ++lines;
+                    line_start(pos, lines);
+                }
+            }
+            if (c == '\n') {
+                ++lines;
+                line_start(pos + 1, lines);
+            } else if (c == '\r') {
+                pend_cr = true;
+            }
+            ++pos;
+            ++i;
+        }
+    }
+    void finish() {  // the end of the stream: a pending '\r' ends a line; cuts not found are the end
+        if (pend_cr) {
+            pend_cr = false;
+            ++lines;
+            line_start(pos, lines);
+        }
+        while (found < 2) cut[found++] = pos;
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
+uint64_t fr_gz_size_hint(const char* path) {
+    FILE* fp = fopen(path, "rb");
+    if (!fp) return 0;
+    struct stat sb;
+    if (fstat(fileno(fp), &sb) != 0 || sb.st_size < 18) {
+        fclose(fp);
+        return 0;
+    }
+    const uint64_t csize = (uint64_t)sb.st_size;
+    // BGZF: the members' ISIZE trailers sum to the decoded size exactly (headers only are read)
+    uint64_t pos = 0, sum = 0;
+    bool bgzf = true;
+    uint8_t h[18];
+    while (bgzf && pos < csize) {
+        if (fseek(fp, (long)pos, SEEK_SET) != 0 || fread(h, 1, 18, fp) != 18) {
+            bgzf = false;
+            break;
+        }
+        if (h[0] != 0x1f || h[1] != 0x8b || h[2] != 8 || !(h[3] & 4) || le16(h + 10) != 6 || h[12] != 'B' ||
+            h[13] != 'C' || le16(h + 14) != 2) {
+            bgzf = false;
+            break;
+        }
+        const uint64_t bsize = le16(h + 16) + 1u;
+        uint8_t t[4];
+        if (bsize < 26 || pos + bsize > csize || fseek(fp, (long)(pos + bsize - 4), SEEK_SET) != 0 ||
+            fread(t, 1, 4, fp) != 4) {
+            bgzf = false;
+            break;
+        }
+        sum += le32(t);
+        pos += bsize;
+    }
+    if (bgzf && pos == csize) {
+        fclose(fp);
+        return sum;
+    }
+    // otherwise the last member's ISIZE (decoded length mod 2^32), lifted by whole 2^32 steps toward
+    // 4x the compressed size (exact for a single-member file of up to 4 GiB decoded)
+    uint8_t t[4];
+    const bool ok = fseek(fp, -4, SEEK_END) == 0 && fread(t, 1, 4, fp) == 4;
+    fclose(fp);
+    if (!ok) return 4 * csize;
+    const uint64_t isize = le32(t), want = 4 * csize;
+    const uint64_t m = want > isize ? (want - isize + (1ull << 31)) >> 32 : 0;
+    return isize + (m << 32);
+}
+
+int fr_gz_part_bounds(const char* path, int nparts, uint64_t hint, uint64_t* bounds) {
+    if (nparts < 1 || !bounds) return FR_ERR_INVALID;
+    const char* paths[1] = {path};
+    fr_gz* g = fr_gz_open(paths, 1, 1);
+    bounds[0] = 0;
+    int rc = FR_OK;
+    // one pass per cut pair keeps the cutter identical to fr_gz_feed_part's (targets j and j + 1)
+    std::vector<Cutter> cs(nparts);
+    for (int j = 0; j < nparts; ++j) {
+        Cutter& cu = cs[j];
+        cu.target[0] = j == 0 ? 0 : (uint64_t)((unsigned __int128)hint * (unsigned)j / (unsigned)nparts);
+        cu.target[1] = j + 1 == nparts ? ~0ull : (uint64_t)((unsigned __int128)hint * (unsigned)(j + 1) / (unsigned)nparts);
+        if (cu.target[1] < cu.target[0]) cu.target[1] = cu.target[0];
+        if (j == 0) cu.cut[cu.found++] = 0;
+    }
+    GzFile& f = g->files[0];
+    {
+        std::lock_guard<std::mutex> lk(g->m);
+        g->consume = 0;
+        g->cv.notify_all();
+    }
+    for (;;) {
+        std::vector<uint8_t> b;
+        {
+            std::unique_lock<std::mutex> lk(g->m);
+            g->cv.wait(lk, [&] { return !f.q.empty() || f.done; });
+            if (f.q.empty()) {
+                if (!f.err.empty()) rc = FR_ERR_IO;
+                break;
+            }
+            b = std::move(f.q.front());
+            f.q.pop_front();
+            g->cv.notify_all();
+        }
+        for (Cutter& cu : cs) cu.consume(b.data(), b.size());
+    }
+    for (int j = 0; j < nparts; ++j) {
+        cs[j].finish();
+        bounds[j] = cs[j].cut[0];
+        if (j + 1 == nparts) bounds[nparts] = cs[j].cut[1];
+    }
+    fr_gz_close(g);
+    return rc;
+}
+
+int fr_gz_feed_part(fr_gz* g, int i, fr_ctx* ctx, int64_t file_index, int part, int nparts, uint64_t hint,
+                    uint64_t* byte_base) {
+    if (i < 0 || i >= (int)g->files.size() || nparts < 1 || part < 0 || part >= nparts) {
+        g->err = "fr_gz_feed_part: bad arguments";
+        return FR_ERR_INVALID;
+    }
+    GzFile& f = g->files[i];
+    {
+        std::lock_guard<std::mutex> lk(g->m);
+        g->consume = i;
+        g->cv.notify_all();
+    }
+    Cutter cu;
+    cu.target[0] = part == 0 ? 0 : (uint64_t)((unsigned __int128)hint * (unsigned)part / (unsigned)nparts);
+    cu.target[1] = part + 1 == nparts ? ~0ull : (uint64_t)((unsigned __int128)hint * (unsigned)(part + 1) / (unsigned)nparts);
+    if (cu.target[1] < cu.target[0]) cu.target[1] = cu.target[0];
+    if (part == 0) cu.cut[cu.found++] = 0;  // b_0 = 0 (the file's first byte is a record start)
+    bool begun = false;
+    int rc = FR_OK;
+    auto begin = [&]() -> int {
+        begun = true;
+        if (byte_base) *byte_base = cu.cut[0];
+        const int r = fr_begin_file_at(ctx, file_index, cu.cut[0], 0);
+        if (r != FR_OK) g->err = fr_last_error(ctx);
+        return r;
+    };
+    auto finish_file = [&](bool cancel) {
+        std::lock_guard<std::mutex> lk(g->m);
+        if (cancel) {
+            f.cancel = true;
+            f.q.clear();
+        }
+        g->cv.notify_all();
+    };
+    for (;;) {
+        std::vector<uint8_t> b;
+        bool end = false;
+        {
+            std::unique_lock<std::mutex> lk(g->m);
+            g->cv.wait(lk, [&] { return !f.q.empty() || f.done; });
+            if (f.q.empty()) {
+                if (!f.err.empty()) {
+                    g->err = f.path + ": " + f.err;
+                    return FR_ERR_IO;
+                }
+                end = true;
+            } else {
+                b = std::move(f.q.front());
+                f.q.pop_front();
+                g->cv.notify_all();
+            }
+        }
+        if (end) {
+            cu.finish();
+            if (!begun && (rc = begin()) != FR_OK) return rc;
+            return FR_OK;
+        }
+        const uint64_t b0 = cu.pos;
+        cu.consume(b.data(), b.size());
+        const uint64_t e0 = cu.pos;  // bytes [b0, e0) of the block were scanned
+        if (!begun && cu.found >= 1 && (rc = begin()) != FR_OK) {
+            finish_file(true);
+            return rc;
+        }
+        if (begun) {  // the part's bytes of this block: [max(b_part, b0), min(b_part+1, block end))
+            const uint64_t lo = std::max(cu.cut[0], b0);
+            const uint64_t hi = std::min(cu.found >= 2 ? cu.cut[1] : b0 + b.size(), b0 + b.size());
+            if (hi > lo) rc = fr_feed(ctx, b.data() + (lo - b0), hi - lo);
+            if (rc != FR_OK) {
+                g->err = fr_last_error(ctx);
+                finish_file(true);
+                return rc;
+            }
+        }
+        (void)e0;
+        {
+            std::lock_guard<std::mutex> lk(g->m);
+            if (g->spare.size() < (size_t)g->threads * g->depth) g->spare.push_back(std::move(b));
+        }
+        if (cu.found >= 2) {  // the part is complete: the rest of the file is another rank's
+            finish_file(true);
+            return FR_OK;
+        }
+    }
+}
+
+}  // extern "C"
+
+extern "C" {
 
 void fr_gz_close(fr_gz* g) {
     if (!g) return;

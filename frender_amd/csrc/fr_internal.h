@@ -14,11 +14,10 @@ typedef int64_t i64;
 
 // ---- tally kernel geometry --------------------------------------------------------
 constexpr int WG = 256;              // 4 waves of 64
-constexpr int TILE = 16384;          // bytes per tile (one look-back unit)
-constexpr int SEG = TILE / WG;       // 64 contiguous bytes per thread
+constexpr int SEG = 64;              // contiguous bytes per lane
+constexpr int TILE = 64 * SEG;       // bytes per wave-tile (one wave's step; chunks count these)
 constexpr int TSTEP = TILE - SEG;    // tile stride: tiles overlap by one segment, so the bitmaps
                                      // of a tile's last own segment always have a successor
-constexpr int HALO = 0;              // bytes staged past the tile (lines past it are read from HBM)
 #ifndef FR_LOG_NS
 #define FR_LOG_NS 10
 #endif
@@ -49,8 +48,8 @@ constexpr int EXO_BUF = 32;          // chunk kernel: exotic records buffered wh
 #define FR_PHASE_LINES 24
 #endif
 constexpr int PHASE_LINES = FR_PHASE_LINES;  // lines the chunk phase guess looks at (>= 8)
-constexpr u32 RARE_RING = 8192;      // chunk kernel: rare events queued per workgroup between drains
-                                     // (<= TILE/4 + 1 headers and WG UTF-8 checks per tile)
+constexpr u32 RARE_RING = 8192;      // chunk kernel: rare events queued per workgroup (a quarter per wave)
+                                     // between drains (<= TILE/4 + 1 headers and 64 UTF-8 checks per wave-tile)
 
 // ---- HBM structures ---------------------------------------------------------------
 struct alignas(32) GSlot {           // open-addressing slot, one 32-B sector
@@ -108,6 +107,14 @@ struct DevState {
     u64 log_n;           // entries appended to the launch log (may exceed its capacity: the rest went to HBM)
     u64 log_commits;     // commits that went to the launch log since the last reset (never emptied by the aggregation)
     u64 stamp[8];        // diagnostics (FR_STAMPS builds only): per-phase shader cycles, summed over workgroups
+    // Heavy chunk geometry, decided on the device: the last workgroup to commit in a
+    // launch sets heavy[par ^ 1] = (at least a quarter of the chunks since the reset logged their
+    // commits); the next launch (parity par ^ 1) reads it at its start and never writes it, so every
+    // workgroup of a launch walks the same geometry.  fr_reset zeroes all of it.
+    u32 heavy[2];
+    u32 commits_done;    // chunks of the current launch that finished their commit (back to 0 by the last)
+    u32 heavy_launches;  // ramped launches since the reset that walked the heavy geometry (diagnostics)
+    u64 chunks_total;    // chunks committed since the reset
 };
 
 struct Table {
@@ -146,6 +153,9 @@ struct ScanArgs {
                          // last ramp_g shrink linearly (chunk_bounds), so workgroups finish their chunks
                          // (look-back, HBM commit) at staggered times and all run out of work together
     u32 mid_chunks;      // full chunks between the two ramps
+    u32 chunk_tiles_h;   // the heavy geometry of the same ramped launch (num_chunks_h = 0: none; the
+    u32 mid_chunks_h;    // kernel picks it when DevState::heavy[par] is set)
+    u32 num_chunks_h;
     u32 cold_cap;        // chunk kernel: entries of each workgroup's cold list
     u64* cold;           // chunk kernel: cold lists, [grid][cold_cap] x {key, ordinal}
     uint4* rare;         // chunk kernel: rare-event rings, [grid][RARE_RING] (fr_kernels.hip)
@@ -159,8 +169,9 @@ struct ScanArgs {
                          // launch end by verify_launch; a wrong guess sets spec_fail)
     DevState* st;
     u64* tiles;          // look-back descriptors
-    const Table* tab;    // device copy: read where used (rare paths), so the tile loop holds no
-                         // table fields in scalar registers
+    const Table* tab;    // device copy (the exotic-only replay's table after the exotic list grew)
+    Table tabv;          // the table by value: read from the kernarg segment where used (scalar loads,
+                         // no dependent global load before a commit's first slot load)
 };
 
 struct SheetArgs {

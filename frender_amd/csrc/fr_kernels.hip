@@ -6,13 +6,14 @@
 //  table / order        : the first-occurrence-ordered merged table of :199-203
 //  synth                : SYN-v1 records (frender_amd/synth.py), device side
 //
-// Design notes: the tally is HBM-bound byte work.  A workgroup owns a
-// 16 KiB tile at a time (dynamic ticket), stages it in LDS with 16-B loads, computes
-// the line-terminator bitmap with SWAR compares, gets the tile's line prefix by a
-// decoupled look-back over 8-B {tag,value} granules (agent-scope relaxed atomics, no
-// fences: MI355X guide Guideline 16 R2), finds every 4th line, parses each header from
-// LDS (lane per header), packs the code 3 bits/char and counts it in an LDS-private
-// open-addressing table that is flushed to the HBM table with 64-bit atomics.
+// Design notes: the tally is HBM-bound byte work.  A workgroup takes a chunk of
+// 4-KiB wave-tiles by ticket and each of its four waves walks a quarter of it without workgroup
+// barriers: lanes classify their 64-B segments in registers (line-end / ' ' / ':' bitmaps by v_perm
+// lookups and dot4 gathers), find every 4th line from the wave's line count, parse each header
+// lane-owned from the bitmaps and the wave's LDS copy of the tile, pack the code 3 bits/char and
+// count it in an LDS open-addressing table shared by the workgroup; each chunk's table is
+// committed to the HBM table (or to the launch log) once.  Line phases are guessed per wave and
+// verified per chunk and per launch (decoupled look-back over 8-B {tag, value} granules).
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
@@ -23,24 +24,28 @@
 
 namespace fr {
 
-#ifndef FR_TIMING
-#define FR_TIMING 0  // diagnostic builds: per-phase s_memtime cycles of the tile loop into DevState::stamp
+#if defined(FR_STAMPS) && FR_STAMPS == 1  // diagnostic builds only: per-wave shader cycles of the chunk loop's phases (DevState::stamp)
+#define FR_STAMP_DECL u64 st_[8] = {0, 0, 0, 0, 0, 0, 0, 0}; u64 tq_ = __builtin_amdgcn_s_memtime();
+#define FR_STAMP(i) do { const u64 n_ = __builtin_amdgcn_s_memtime(); st_[i] += n_ - tq_; tq_ = n_; } while (0)
+#define FR_STAMP_FLUSH(k0) do { st_[6] = __builtin_amdgcn_s_memtime() - (k0); \
+    if ((threadIdx.x & 63) == 0) for (int i_ = 0; i_ < 8; ++i_) atomicAdd((unsigned long long*)&a.st->stamp[i_], \
+        (unsigned long long)st_[i_]); } while (0)
+#else
+#define FR_STAMP_DECL
+#define FR_STAMP(i) do { } while (0)
+#define FR_STAMP_FLUSH(k0) do { } while (0)
 #endif
-#ifndef FR_PREFETCH
-#define FR_PREFETCH 0  // load tile t+1's segment before tile t's header parse
+
+#if defined(FR_STAMPS) && FR_STAMPS == 2  // diagnostic builds only: the commit's phases instead
+#define FR_CSTAMP(i) do { const u64 n_ = __builtin_amdgcn_s_memtime(); cst_[i] += n_ - cq_; cq_ = n_; } while (0)
+#else
+#define FR_CSTAMP(i) do { } while (0)
 #endif
-#ifndef FR_LDS_RAW
-#define FR_LDS_RAW 1  // keep each tile's raw bytes in LDS for the parse (code bytes read from LDS, not L2);
-                      // the next tile's segment loads are issued right after this tile's bytes are stored
-#endif
-#ifndef FR_PF_DEPTH
-#define FR_PF_DEPTH 1  // FR_LDS_RAW: tiles of segment loads each wave keeps in flight (1 or 2 register sets)
-#endif
-#ifndef FR_PARSE2
-#define FR_PARSE2 1  // FR_LDS_RAW: header parse v2 (two 64-bit bitmap windows, wave-uniform code length encode)
-#endif
-#ifndef FR_SEG_AUX
-#define FR_SEG_AUX 0  // cache policy bits of the segment stream loads (2 = nt)
+
+#ifdef FR_DEBUG_PRINT  // diagnostic builds only: trace the tally kernel's chunk loop (workgroup 0, lane 0 of each wave)
+#define FR_TRACE(...) do { if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) printf(__VA_ARGS__); } while (0)
+#else
+#define FR_TRACE(...) do { } while (0)
 #endif
 
 // FR_OUTLINE_COLD=1 keeps the rare paths out of line (measured slower: the calls make the
@@ -178,7 +183,25 @@ __device__ __forceinline__ void add_created(DevState* st, u32 mine) {
 }
 
 // ------------------------------------------------------------------------------------
-// the tally kernel
+// the tally kernel (v8): per-wave walkers
+//
+// A workgroup takes a chunk (a contiguous run of wave-tiles) by ticket and splits it into four
+// contiguous parts, one per wave.  Each wave walks its part alone: no workgroup barrier inside the
+// tile loop, so a wave that waits for its next tile's loads does not hold the other three (round 2
+// had two barriers per 16-KiB workgroup tile; MI355X measurements in profiles/r03a_ubench_tile.txt:
+// the barrier-free walk is 8-12 % faster at equal loads and parse work).  A wave-tile is 4 KiB: lane
+// L holds the 64-B segment [64 L, 64 L + 64) in registers, loaded one wave-tile ahead, classifies it
+// there, and stores its ' ' / ':' / line-end bitmaps and its bytes to the wave's own LDS area, where
+// the lane-owned header parse reads them.  Tiles overlap by one segment (stride TSTEP), so a
+// header's bitmap window always has a successor segment.
+//
+// Line phase per wave: the first wave of chunk 0 starts at the range's exact line count; every
+// other wave guesses its starting phase from its first wave-tile (FASTQ structure, infer_phase).
+// After the walk the chunk's four counts give each wave's phase relative to the chunk start; a wave
+// whose guess disagrees makes the chunk redo with the derived phases, a wave that could not guess
+// walks again with its derived phase.  The chunk start itself is exact (chunk 0, or a decoupled
+// look-back) or, for device feeds, the first wave's guess, committed at once and checked for the
+// whole launch by verify_launch.  Correctness never depends on a guess.
 // ------------------------------------------------------------------------------------
 struct alignas(16) LSlot {  // one ds_read_b128 reads key, count and first offset together
     u64 key;                 // 0 = empty
@@ -186,58 +209,67 @@ struct alignas(16) LSlot {  // one ds_read_b128 reads key, count and first offse
     u32 mino;                // min range offset of the code's records, ~0 = none
 };
 
+constexpr int NW = WG / 64;                  // waves per workgroup
+constexpr int SEGS = TILE / SEG;             // segments per wave-tile (= lanes)
+constexpr u32 RARE_WAVE = RARE_RING / NW;    // rare-event ring entries per wave
+
 struct ScanShared {
-#if FR_LDS_RAW
-    u32 raw[TILE / 4];  // the current tile's bytes (stored after B1, read by the parse after B2)
-#endif
-    LSlot ls[NS];     // LDS hash table of this workgroup's chunk
-    alignas(16) u32 wsum[WG / 64];
+    u32 raw[NW][TILE / 4];   // each wave's current wave-tile (the parse reads code bytes here)
+    LSlot ls[NS];            // LDS hash table of this workgroup's chunk
+    u64 bsp[NW][SEGS + 1];   // per wave, per 64-B segment of its staged tile: ' ' | line-end bitmap
+    u64 bcol[NW][SEGS + 1];  //                                              ':' bitmap
+    u64 beol[NW][SEGS + 1];  //                                              '\r' | '\n' bitmap
+                             // entry SEGS of each stays zero: the window's second segment past the tile
+    u64 wcount[NW];          // pass 0: line terminators of each wave's part of the chunk
+    int wphase[NW];          // pass 0: the phase each wave parsed with (mod 4), -1 count only
+    u32 rq_tail[NW];         // rare-event ring: events pushed by each wave (monotonic)
     u64 tile_excl;
-    u32 tile;
-    u32 next;
-    u32 nkeys;        // occupied LDS slots
-    u32 created;      // HBM slots this workgroup created (added to n_keys once, at exit)
-    u32 flags;
-    u32 rq_tail;      // rare-event ring: events pushed by this workgroup (monotonic)
-    u32 last;         // this workgroup published the launch's last chunk count (runs verify_launch)
-    u32 log_pos;      // commit: next free entry of this commit's launch-log block
-    u64 log_base;     // commit: the block's first entry (~0: the block did not fit, insert directly)
-    // ---- chunk kernel state ----
-    u32 buffered;     // LDS-table misses go to this workgroup's cold list (committed later)
-    u32 spec;         // speculating on the line phase: exotic records / errors are buffered
-    u32 spec_bad;     // a speculation buffer overflowed: redo this chunk exactly
-    u32 ncold;        // cold list fill
-    u32 nexo;         // buffered exotic records
-    u32 err_off;      // min range offset of a header without ' ' (buffered), ~0 none
     u32 chunk;
-    int phase;        // guessed line phase (lines before the chunk, mod 4), -1 unsure
+    u32 nkeys;               // occupied LDS slots
+    u32 created;             // HBM slots this workgroup created (added to n_keys once, at exit)
+    u32 flags;
+    u32 last;                // this workgroup published the launch's last chunk count (runs verify_launch)
+    u32 log_pos;             // commit: next free entry of this commit's launch-log block
+    u64 log_base;            // commit: the block's first entry (~0: the block did not fit, insert directly)
+    u32 spec;                // side effects are buffered (a phase in use is a guess); the chunk may be redone
+    u32 spec_bad;            // a speculation buffer overflowed: redo this chunk exactly
+    u32 ncold;               // cold list fill
+    u32 nexo;                // buffered exotic records
+    u32 err_off;             // min range offset of a header without ' ' (buffered), ~0 none
     u32 exo_p[EXO_BUF], exo_start[EXO_BUF], exo_len[EXO_BUF];
-    u64 bsp[WG + 1];  // per 64-B segment of the staged tile: ' ' | line-end bitmap (phase inference: the
-                      // line-terminator bitmap of a chunk's first tile)
-    u64 bcol[WG + 1]; //                                      ':' bitmap
-    u64 beol[WG + 1]; //                                      '\r' | '\n' bitmap
-                      // entry WG of each stays zero: the window's second segment past the tile
 };
+
+typedef u32 u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) u32 lds_u32;
+typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
 
 __device__ __forceinline__ u64 make_ord(const ScanArgs& a, u64 off_in_range) {
     return ((u64)a.file_tag << ORD_SHIFT) | (a.file_offset + off_in_range);
 }
 
-__device__ FR_COLD void direct_insert(ScanShared& sh, const ScanArgs& a, u64 key, u32 off) {
-    if (global_insert(*a.tab, a.st, key, 1, make_ord(a, off), a.file_tag)) atomicAdd(&sh.created, 1u);
+__device__ __forceinline__ u32 wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
+// this wave's LDS stores are complete: later reads by other lanes of the wave see them (a wave's LDS
+// operations execute in order; the wait also keeps the compiler from moving reads above the stores).
+// LDS only: outstanding global loads (the next tile) stay in flight.
+__device__ __forceinline__ void lds_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-__device__ __forceinline__ void rare_push(ScanShared& sh, const ScanArgs& a, u32 p, u32 kind, u32 x, u32 y);
-
-// Barrier of the tile loop: orders LDS only.  __syncthreads() would also drain every global store
-// of the wave (cold-list entries) before the barrier; those are read only at the chunk's commit,
-// behind a full __syncthreads().  Global data handed over inside the loop (the rare ring) is
-// released by its writer (rare_push).
+// workgroup barrier that orders LDS only: outstanding global loads, stores and atomics stay in flight
+// (__syncthreads() would wait for every one of them)
 __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
+
+__device__ FR_COLD void direct_insert(ScanShared& sh, const ScanArgs& a, u64 key, u32 off) {
+    if (global_insert(a.tabv, a.st, key, 1, make_ord(a, off), a.file_tag)) atomicAdd(&sh.created, 1u);
+}
+
+__device__ __forceinline__ void rare_push(ScanShared& sh, const ScanArgs& a, u32 p, u32 kind, u32 x, u32 y);
 
 template <bool DRAIN = false>
 __device__ __forceinline__ void lds_insert(ScanShared& sh, const ScanArgs& a, u64 key, u32 off) {
@@ -245,16 +277,15 @@ __device__ __forceinline__ void lds_insert(ScanShared& sh, const ScanArgs& a, u6
     u32 h = (((u32)key ^ (u32)(key >> 27)) * 0x9E3779B1u) >> (32 - LOG_NS);
 #pragma unroll 2
     for (int pr = 0; pr < LPROBE; ++pr) {
-        typedef u32 u32x4 __attribute__((ext_vector_type(4)));
         // volatile through an explicit LDS pointer: a volatile access through a generic pointer
         // keeps its flat form (flat loads wait on vmcnt(0), i.e. on every outstanding HBM op)
-        const u32x4 sl = *(const volatile __attribute__((address_space(3))) u32x4*)&sh.ls[h];
+        const u32x4 sl = *(const volatile lds_u32x4*)&sh.ls[h];
         u64 k = ((u64)sl.y << 32) | sl.x;
         u32 mino = sl.w;
         if (k == 0) {
-            // a full LDS table stops claiming slots: the code goes to HBM directly; the
-            // codes already resident (the hot ones arrive first) keep aggregating here
-            if (*(const volatile __attribute__((address_space(3))) u32*)&sh.nkeys >= a.flush_at) break;
+            // a full LDS table stops claiming slots: the code goes to the cold list; the codes
+            // already resident (the hot ones arrive first) keep aggregating here
+            if (*(const volatile lds_u32*)&sh.nkeys >= a.flush_at) break;
             const u64 old = atomicCAS((unsigned long long*)&sh.ls[h].key, 0ull, (unsigned long long)key);
             if (old == 0) {
                 atomicAdd(&sh.nkeys, 1u);
@@ -272,40 +303,39 @@ __device__ __forceinline__ void lds_insert(ScanShared& sh, const ScanArgs& a, u6
         }
         h = (h + 1) & (NS - 1);
     }
-    if (sh.buffered) {  // chunk kernel: park the miss in this workgroup's cold list
-        const u32 i = atomicAdd(&sh.ncold, 1u);
-        if (i < a.cold_cap) {
-            u64* c = a.cold + 2ull * ((u64)blockIdx.x * a.cold_cap + i);
-            c[0] = key;
-            c[1] = make_ord(a, off);
-            return;
-        }
-        if (sh.spec) {  // cannot buffer while speculating: this chunk will be redone exactly
-            atomicOr(&sh.spec_bad, 1u);
-            return;
-        }
-        // exact phase and a full cold list: insert directly (queued out of the hot loop)
+    // an LDS-table miss: park it in this workgroup's cold list (committed with the chunk)
+    const u32 i = atomicAdd(&sh.ncold, 1u);
+    if (i < a.cold_cap) {
+        u64* c = a.cold + 2ull * ((u64)blockIdx.x * a.cold_cap + i);
+        c[0] = key;
+        c[1] = make_ord(a, off);
+        return;
     }
+    if (sh.spec) {  // cannot insert while speculating: this chunk will be redone exactly
+        atomicOr(&sh.spec_bad, 1u);
+        return;
+    }
+    // exact phase and a full cold list: insert directly (queued out of the hot loop)
     if (DRAIN) direct_insert(sh, a, key, off);
     else rare_push(sh, a, off, 3u, (u32)key, (u32)(key >> 32));
 }
 
 // Rare events (exotic codes, headers without ' ', headers whose code leaves the bitmap window,
-// direct HBM inserts, UTF-8 checks) go to the workgroup's ring in HBM and are handled by
-// drain_rare between tiles, so their code adds no registers to the tile loop.  Entry: {range
-// offset, kind, x, y}.
+// direct HBM inserts, UTF-8 checks) go to the wave's ring in HBM and are handled by drain_rare at
+// the wave's next tile, so their code adds no registers to the tile loop.  Entry: {range offset,
+// kind, x, y}.  No fence here (a release would wait for the next tile's loads): drain_rare fences.
 __device__ __forceinline__ void rare_push(ScanShared& sh, const ScanArgs& a, u32 p, u32 kind, u32 x, u32 y) {
-    const u32 i = atomicAdd(&sh.rq_tail, 1u);
-    a.rare[(u64)blockIdx.x * RARE_RING + (i & (RARE_RING - 1u))] = make_uint4(p, kind, x, y);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // visible to the drain after the next barrier
+    const u32 wid = wave_id();
+    const u32 i = atomicAdd(&sh.rq_tail[wid], 1u);
+    a.rare[(u64)blockIdx.x * RARE_RING + wid * RARE_WAVE + (i & (RARE_WAVE - 1u))] = make_uint4(p, kind, x, y);
 }
 
-// Decoupled look-back over the launch's tile descriptors {tag = 2*epoch + inclusive, value}.
-// The tile's own aggregate was published when it was staged (count_tile); this resolves its
-// exclusive prefix, reading 256 predecessors per poll (4 per lane), and publishes the
-// inclusive prefix.  Returns the number of line terminators in tiles [0, t) of the range.
+// Decoupled look-back over the launch's chunk descriptors {tag = 2*epoch + inclusive, value}.
+// The chunk's own aggregate was published before (chunk_kernel); this resolves its exclusive
+// prefix, reading 256 predecessors per poll (4 per lane), and publishes the inclusive prefix.
+// Returns the number of line terminators in chunks [0, t) of the range.
 __device__ __forceinline__ u64 lookback(const ScanArgs& a, u32 t, u32 agg, int lane) {
-    if (t == 0) return 0;  // tile 0 published its inclusive value directly
+    if (t == 0) return 0;  // chunk 0 published its inclusive value directly
     const u64 tagI = (u64)(2u * a.epoch + 1u) << 32;
     u64 excl = 0;
     i64 j = (i64)t - 1;
@@ -363,16 +393,15 @@ __device__ __forceinline__ u64 lookback(const ScanArgs& a, u32 t, u32 agg, int l
     return excl;
 }
 
-// validate UTF-8 for the bytes [s0, s0+n) of the tile (only called when a byte >= 0x80
-// is present); bytes are read from HBM (the range, and before it when readable), -1 past them.
-__device__ FR_COLD bool utf8_segment_ok(const ScanArgs& a, u64 tile0, int s0, int n) {
-    auto byte_at = [&](int q) -> int {
-        const i64 g = (i64)tile0 + q;
-        if (q < 0 && g < 0 && !a.pre_valid) return -1;
-        if (g >= (i64)a.avail) return -1;
-        return (int)a.buf[g];
+// validate UTF-8 for the range bytes [s0, s0+n) (only called when a byte >= 0x80 is present);
+// bytes are read from HBM (the range, and before it when readable), -1 past them.
+__device__ FR_COLD bool utf8_segment_ok(const ScanArgs& a, int s0, int n) {
+    auto byte_at = [&](i64 q) -> int {
+        if (q < 0 && !a.pre_valid) return -1;
+        if (q >= (i64)a.avail) return -1;
+        return (int)a.buf[q];
     };
-    for (int q = s0; q < s0 + n; ++q) {
+    for (i64 q = s0; q < (i64)s0 + n; ++q) {
         const int b = byte_at(q);
         if (b < 0x80) continue;
         if (b >= 0x80 && b <= 0xBF) {  // continuation: must be claimed by a lead
@@ -408,12 +437,12 @@ __device__ FR_COLD bool utf8_segment_ok(const ScanArgs& a, u64 tile0, int s0, in
 }
 
 template <bool DRAIN = false>
-__device__ __forceinline__ void count_code(ScanShared& sh, const ScanArgs& a, u64 tile0, u32 p, u64 key) {
+__device__ __forceinline__ void count_code(ScanShared& sh, const ScanArgs& a, u32 p, u64 key) {
     if ((a.ablate & 4u) || a.exo_only) {  // ablation / exotic-only replay: skip the hash insert
         asm volatile("" ::"v"(key));
         return;
     }
-    lds_insert<DRAIN>(sh, a, key, (u32)(tile0 + p));
+    lds_insert<DRAIN>(sh, a, key, p);
 }
 
 // code bytes [q, q+n) of the range (exact byte reads) -> wide key (fr_internal.h), false when the
@@ -446,27 +475,28 @@ __device__ bool wide_encode(const ScanArgs& a, u64 q, u64 n, u64& key) {
     return true;
 }
 
-// a code the fast encoder did not take: exact fast form (defensive), wide key, or an exotic record
-// captured verbatim (speculating: its position is buffered and the bytes stay resident in HBM)
-__device__ void exotic_record(const ScanArgs& a, u64 tile0, u32 p, u64 start, u64 n, ScanShared& sh) {
+// a code the fast encoder did not take (range offsets: header p, code [start, start + n)): exact
+// fast form (defensive), wide key, or an exotic record captured verbatim (speculating: its position
+// is buffered and the bytes stay resident in HBM)
+__device__ void exotic_record(const ScanArgs& a, u32 p, u64 start, u64 n, ScanShared& sh) {
     {
         bool fast = n >= 1 && n <= (u64)MAXSYM;
         u64 key = 0;
         for (u64 i = 0; fast && i < n; ++i) {
-            const u32 sy = sym_of(a.buf[tile0 + start + i]);
+            const u32 sy = sym_of(a.buf[start + i]);
             fast = sy != 0;
             key |= (u64)sy << (3 * i);
         }
-        if (fast || wide_encode(a, tile0 + start, n, key)) {
-            count_code<true>(sh, a, tile0, p, key);
+        if (fast || wide_encode(a, start, n, key)) {
+            count_code<true>(sh, a, p, key);
             return;
         }
     }
     if (sh.spec) {  // speculating: remember where it is; the bytes stay resident in HBM
         const u32 k = atomicAdd(&sh.nexo, 1u);
         if (k < (u32)EXO_BUF) {
-            sh.exo_p[k] = (u32)(tile0 + p);
-            sh.exo_start[k] = (u32)(tile0 + start);
+            sh.exo_p[k] = p;
+            sh.exo_start[k] = (u32)start;
             sh.exo_len[k] = (u32)n;
         } else {
             atomicOr(&sh.spec_bad, 1u);
@@ -475,36 +505,33 @@ __device__ void exotic_record(const ScanArgs& a, u64 tile0, u32 p, u64 start, u6
     }
     const u64 i = atomicAdd((unsigned long long*)&a.st->n_exotic, 1ull);
     const u64 po = atomicAdd((unsigned long long*)&a.st->exo_pool_used, (unsigned long long)n);
-    if (i < a.tab->exo_cap && po + n <= a.tab->exo_pool_cap) {
-        a.tab->exo_ord[i] = make_ord(a, tile0 + p);
-        a.tab->exo_off[i] = po;
-        a.tab->exo_len[i] = (u32)n;
-        for (u64 k = 0; k < n; ++k) {
-            const u64 q = start + k;
-            a.tab->exo_pool[po + k] = a.buf[tile0 + q];
-        }
+    if (i < a.tabv.exo_cap && po + n <= a.tabv.exo_pool_cap) {
+        a.tabv.exo_ord[i] = make_ord(a, p);
+        a.tabv.exo_off[i] = po;
+        a.tabv.exo_len[i] = (u32)n;
+        for (u64 k = 0; k < n; ++k) a.tabv.exo_pool[po + k] = a.buf[start + k];
     } else {
         atomicOr(&a.st->cap_flags, 4u);
     }
 }
 
-__device__ __forceinline__ void nospace(const ScanArgs& a, u64 tile0, u32 p, ScanShared& sh) {  // IndexError (:169)
-    if (sh.spec) atomicMin(&sh.err_off, (u32)(tile0 + p));
-    else atomicMin((unsigned long long*)&a.st->err_nospace, (unsigned long long)(a.file_offset + tile0 + p));
+__device__ __forceinline__ void nospace(const ScanArgs& a, u32 p, ScanShared& sh) {  // IndexError (:169)
+    if (sh.spec) atomicMin(&sh.err_off, p);
+    else atomicMin((unsigned long long*)&a.st->err_nospace, (unsigned long long)(a.file_offset + p));
 }
 
-// slow path (rare): a header whose code does not end inside its 128-bit bitmap window, parsed
-// byte by byte from HBM.  R2 (frender.py:169): the token after the first ' ' up to the next ' '
-// or line end, then its suffix after the last ':'.
-__device__ FR_COLD void process_header_global(ScanShared& sh, const ScanArgs& a, u64 tile0, u32 p) {
-    const u64 eof = a.avail - tile0;
-    auto rd = [&](u64 q) -> u32 { return (u32)a.buf[tile0 + q]; };
+// slow path (rare): a header whose code does not end inside its bitmap windows, parsed byte by
+// byte from HBM.  R2 (frender.py:169): the token after the first ' ' up to the next ' ' or line
+// end, then its suffix after the last ':'.  p = the header's range offset.
+__device__ FR_COLD void process_header_global(ScanShared& sh, const ScanArgs& a, u32 p) {
+    const u64 eof = a.avail;
+    auto rd = [&](u64 q) -> u32 { return (u32)a.buf[q]; };
     u64 q = p;
     for (;;) {
-        if (q >= eof) return nospace(a, tile0, p, sh);
+        if (q >= eof) return nospace(a, p, sh);
         const u32 c = rd(q);
         if (c == ' ') break;
-        if (c == '\n' || c == '\r') return nospace(a, tile0, p, sh);
+        if (c == '\n' || c == '\r') return nospace(a, p, sh);
         ++q;
     }
     const u64 sp1 = q++;
@@ -525,35 +552,23 @@ __device__ FR_COLD void process_header_global(ScanShared& sh, const ScanArgs& a,
         fast = sy != 0;
         key |= (u64)sy << (3 * i);
     }
-    if (fast) count_code<true>(sh, a, tile0, p, key);
-    else exotic_record(a, tile0, p, start, n, sh);
+    if (fast) count_code<true>(sh, a, p, key);
+    else exotic_record(a, p, start, n, sh);
 }
 
-struct TileCount {
-    u64 tmask;  // line-terminator bitmap of this thread's 64 bytes
-    u32 c;      // popcount(tmask)
-    u32 x;      // inclusive wave scan of c
-    u32 wexcl;  // terminators in earlier waves of this tile
-    u32 tot;    // terminators in the tile
-};
-
-// ---- tile staging: lane-contiguous segments classified straight from registers ---------
-// Lane tid loads its own 64-byte segment [tid*64, tid*64+64) of the tile (four 16-B loads) plus
-// the first dword of the next segment (a '\r' ending the segment needs the byte after it) and
-// classifies it in registers.  Only the ' ' / ':' / line-end bitmaps go to LDS; the raw bytes
-// never do (code bytes are re-read from L2 by the parse), which keeps a workgroup's LDS at
-// ~22 KB so that 7 workgroups share a CU.  Two barriers per tile: B1 (the previous tile's
-// parse is done with the bitmaps) and B2 (this tile's bitmaps and wave sums are in LDS).
+// ---- wave-tile staging: lane-contiguous segments classified straight from registers ---------
+// Lane L loads its own 64-byte segment [64 L, 64 L + 64) of the wave-tile (four 16-B loads through
+// a wave-uniform buffer descriptor) one tile ahead, classifies it in registers and stores it and
+// its bitmaps to the wave's LDS area.  (Coalesced 1-KiB-per-instruction loads with an LDS
+// transpose, and LDS-DMA rings, measured slower: profiles/r03a_ubench_tile.txt.)
 struct SegRegs {
     uint4 v[SEG / 16];
     u32 nx;  // first dword of the next segment (zero past the staged bytes)
 };
 
-__device__ __forceinline__ void seg_fetch(const ScanArgs& a, u32 t, SegRegs& r, int tid, bool want = true,
-                                          bool with_nx = false) {
-    const bool live = want && t < a.num_tiles;
-    const u64 tile0 = live ? (u64)t * TSTEP : 0ull;
-    const u32 nb = live ? (u32)min((u64)(TILE + HALO), a.avail - tile0) : 0u;
+__device__ __forceinline__ void seg_fetch(const ScanArgs& a, u32 t, SegRegs& r, int lane, bool with_nx = false) {
+    const u64 tile0 = (u64)t * TSTEP;
+    const u32 nb = (u32)min((u64)TILE, a.avail - tile0);
     const u64 base = (u64)(a.buf + tile0);
     const u32 lo = __builtin_amdgcn_readfirstlane((u32)base), hi = __builtin_amdgcn_readfirstlane((u32)(base >> 32));
     const u8* ub = (const u8*)(((u64)hi << 32) | lo);
@@ -561,18 +576,18 @@ __device__ __forceinline__ void seg_fetch(const ScanArgs& a, u32 t, SegRegs& r, 
                                                         0x00020000);
 #pragma unroll
     for (int k = 0; k < SEG / 16; ++k) {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, tid * SEG, k * 16, FR_SEG_AUX);
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, lane * SEG, k * 16, 0);
         r.v[k] = make_uint4(v[0], v[1], v[2], v[3]);
     }
-    r.nx = with_nx ? __builtin_amdgcn_raw_buffer_load_b32(rsrc, tid * SEG + SEG, 0, 0) : 0u;  // '\r' path only
+    r.nx = with_nx ? __builtin_amdgcn_raw_buffer_load_b32(rsrc, lane * SEG + SEG, 0, 0) : 0u;  // '\r' path only
 }
 
 // the data end (a segment, or the dword after it, reaches past avail): bytewise loads, zeros past
 // the staged bytes (the buffer range check is trusted only for whole vectors)
-__device__ __attribute__((noinline)) SegRegs seg_load_tail(const ScanArgs& a, u32 t, int tid) {
+__device__ __attribute__((noinline)) SegRegs seg_load_tail(const ScanArgs& a, u32 t, int lane) {
     const u64 tile0 = (u64)t * TSTEP;
-    const u32 nb = (u32)min((u64)(TILE + HALO), a.avail - tile0);
-    const u32 s0 = tid * SEG;
+    const u32 nb = (u32)min((u64)TILE, a.avail - tile0);
+    const u32 s0 = lane * SEG;
     u32 w[SEG / 4 + 1];
     for (int k = 0; k <= SEG / 4; ++k) {
         u32 v = 0;
@@ -588,30 +603,28 @@ __device__ __attribute__((noinline)) SegRegs seg_load_tail(const ScanArgs& a, u3
     return r;
 }
 
-// every lane's segment loads of tile t lie inside the data (else seg_load_tail)
+// every lane's segment loads of wave-tile t (and the dword after them) lie inside the data
 __device__ __forceinline__ bool seg_in_range(const ScanArgs& a, u32 t) {
-    return (u64)t * TSTEP + (TILE + HALO + SEG + 4) <= a.avail;
+    return (u64)t * TSTEP + (TILE + SEG + 4) <= a.avail;
 }
 
-// tile t's segment into r (the data end: bytewise loads, zeros past it)
-__device__ __forceinline__ void seg_prefetch_next(const ScanArgs& a, u32 t, SegRegs& r, int tid) {
-    if (seg_in_range(a, t)) seg_fetch(a, t, r, tid);
-    else r = seg_load_tail(a, t, tid);
+__device__ __forceinline__ void seg_load(const ScanArgs& a, u32 t, SegRegs& r, int lane) {
+    if (seg_in_range(a, t)) seg_fetch(a, t, r, lane);
+    else r = seg_load_tail(a, t, lane);
 }
 
 struct SegClass {
     u64 tmask, sp, col, eol;  // terminators (own bytes), and the parse bitmaps (staged bytes)
     u32 c, x;                 // popcount(tmask), its inclusive wave scan
-    u32 wtot;                 // the wave's terminators
-    bool hi;                  // a byte >= 0x80 among the own bytes (UTF-8 check after B2)
+    u32 wtot;                 // the wave's terminators (own bytes of the wave-tile)
+    bool hi;                  // a byte >= 0x80 among the own bytes (UTF-8 check, kind 4)
 };
 
-__device__ __forceinline__ SegClass seg_classify(const ScanArgs& a, u32 t, const SegRegs& r, int tid) {
+__device__ __forceinline__ SegClass seg_classify(const ScanArgs& a, u32 t, const SegRegs& r, int lane) {
     const u64 tile0 = (u64)t * TSTEP;
     const u32 tlen = (u32)min((u64)TSTEP, a.len - tile0);
-    const u32 nb = (u32)min((u64)(TILE + HALO), a.avail - tile0);
-    const u32 bl = min((u32)TILE, nb);
-    const u32 s0 = tid * SEG;
+    const u32 bl = (u32)min((u64)TILE, a.avail - tile0);
+    const u32 s0 = lane * SEG;
     SegClass sc;
     sc.tmask = 0;
     sc.sp = sc.col = sc.eol = 0;
@@ -638,8 +651,8 @@ __device__ __forceinline__ SegClass seg_classify(const ScanArgs& a, u32 t, const
             // The segment (and the byte after it) is re-read from L2 here, so no class word has to
             // stay live through the common path.
             SegRegs q;
-            if (seg_in_range(a, t)) seg_fetch(a, t, q, tid, true, true);
-            else q = seg_load_tail(a, t, tid);
+            if (seg_in_range(a, t)) seg_fetch(a, t, q, lane, true);
+            else q = seg_load_tail(a, t, lane);
             u32 cr16[4];
 #pragma unroll
             for (int qv = 0; qv < SEG / 16; ++qv)
@@ -675,45 +688,20 @@ __device__ __forceinline__ SegClass seg_classify(const ScanArgs& a, u32 t, const
     x += __builtin_amdgcn_update_dpp(0u, x, 0x118, 0xF, 0xF, true);  // row_shr:8
     x += __builtin_amdgcn_update_dpp(0u, x, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
     x += __builtin_amdgcn_update_dpp(0u, x, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
-    const u32 wtot = __builtin_amdgcn_readlane(x, 63);
     sc.x = x;
-    sc.wtot = wtot;
+    sc.wtot = __builtin_amdgcn_readlane(x, 63);
     return sc;
 }
 
-// after B1: the segment's bitmaps into LDS, the wave's terminator count
-__device__ __forceinline__ void seg_store(ScanShared& sh, const SegClass& sc, int tid, int lane, int wid) {
-    sh.bsp[tid] = sc.sp | sc.eol;  // token ends: ' ' or line end
-    sh.bcol[tid] = sc.col;
-    sh.beol[tid] = sc.eol;
-    if (lane == 0) sh.wsum[wid] = sc.wtot;
-}
+__device__ FR_COLD void slow_header(ScanShared& sh, const ScanArgs& a, u32 p, int r, u32 start, u32 n);
 
-// after B2: the tile's line prefix for this lane (TileCount, as parse_own_headers takes it)
-__device__ __forceinline__ TileCount seg_count(const ScanShared& sh, const SegClass& sc, int wid) {
-    TileCount tc;
-    tc.tmask = sc.tmask;
-    tc.c = sc.c;
-    tc.x = sc.x;
-    u32 wexcl = 0, tot = 0;
-#pragma unroll
-    for (int w = 0; w < WG / 64; ++w) {
-        const u32 v = sh.wsum[w];
-        wexcl += w < wid ? v : 0u;
-        tot += v;
-    }
-    tc.wexcl = wexcl;
-    tc.tot = tot;
-    return tc;
-}
-
-__device__ FR_COLD void slow_header(ScanShared& sh, const ScanArgs& a, u64 tile0, u32 p, int r, u32 start, u32 n);
-
-// handle the ring entries [from, to) (all threads; between B1 and B2 nothing is pushed)
-__device__ __attribute__((noinline)) void drain_rare(ScanShared& sh, const ScanArgs& a, u32 from, u32 to, int tid) {
-    const uint4* q = a.rare + (u64)blockIdx.x * RARE_RING;
-    for (u32 i = from + tid; i - from < to - from; i += WG) {
-        const uint4 e = q[i & (RARE_RING - 1u)];
+// handle this wave's ring entries [from, to) (its lanes; the wave pushes nothing meanwhile)
+__device__ __attribute__((noinline)) void drain_rare(ScanShared& sh, const ScanArgs& a, u32 wid, u32 from, u32 to,
+                                                     int lane) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");  // the wave's ring stores are visible to its loads
+    const uint4* q = a.rare + (u64)blockIdx.x * RARE_RING + wid * RARE_WAVE;
+    for (u32 i = from + lane; i - from < to - from; i += 64) {
+        const uint4 e = q[i & (RARE_WAVE - 1u)];
         if (e.y == 3u) {
             direct_insert(sh, a, ((u64)e.w << 32) | e.z, e.x);
         } else if (e.y == 4u) {  // UTF-8: the segment's own bytes [e.x, e.x + e.z)
@@ -721,16 +709,16 @@ __device__ __attribute__((noinline)) void drain_rare(ScanShared& sh, const ScanA
             for (u32 k = 0; k < e.z; ++k) hi |= a.buf[e.x + k] >= 0x80;
             if (hi) {
                 atomicOr(&sh.flags, 1u);
-                if (!utf8_segment_ok(a, 0, (int)e.x, (int)e.z)) atomicOr(&sh.flags, 2u);
+                if (!utf8_segment_ok(a, (int)e.x, (int)e.z)) atomicOr(&sh.flags, 2u);
             }
         } else {
-            slow_header(sh, a, 0, e.x, (int)e.y, e.z, e.w);
+            slow_header(sh, a, e.x, (int)e.y, e.z, e.w);
         }
     }
 }
 
-// phase inference bitmaps of a chunk's first tile: '@' and '+' (first bytes of header / separator
-// lines); exact per-byte equality, once per chunk
+// phase inference bitmaps of a wave's first tile: '@' and '+' (first bytes of header / separator
+// lines); exact per-byte equality, once per wave and chunk
 __device__ __forceinline__ void seg_marks(const SegRegs& r, u64& at, u64& plus) {
     at = 0;
     plus = 0;
@@ -745,36 +733,26 @@ __device__ __forceinline__ void seg_marks(const SegRegs& r, u64& at, u64& plus) 
     }
 }
 
-
-// =====================================================================================
-// chunk kernel (v3): a workgroup owns a contiguous chunk of tiles and walks it in order, so
-// the line count is local; the chunk's starting line phase is guessed from the FASTQ record
-// structure, results are buffered (LDS table + the workgroup's cold list + buffered exotic
-// records / errors) and committed once the chunk's exact prefix (one chunk-level look-back)
-// confirms the guess.  A wrong/unsure guess, a buffer overflow or -s re-runs the chunk with
-// the exact prefix.  Correctness never depends on the guess.
-// =====================================================================================
-
-// Guess P = (lines before the chunk) mod 4 from the first PHASE_LINES complete lines of the
-// staged first tile: with lines indexed P+k+1 after the k-th terminator, a FASTQ record has a
-// header ('@') at phase 0, '+' at phase 2 and equal seq/qual lengths at phases 1/3.  Exactly
-// one consistent P -> the guess; otherwise -1 (unsure).  One lane, once per chunk.
-// Bitmaps (staged by the caller): bsp = line terminators, bcol = '@', beol = '+'.  Line lengths
-// include a '\r' of "\r\n" (equal on both lines of a consistently terminated record).
-__device__ __forceinline__ int infer_phase(const ScanShared& sh) {
+// Guess P = (lines before the wave-tile) mod 4 from its first PHASE_LINES complete lines: with lines
+// indexed P+k+1 after the k-th terminator, a FASTQ record has a header ('@') at phase 0, '+' at
+// phase 2 and equal seq/qual lengths at phases 1/3.  Exactly one consistent P -> the guess;
+// otherwise -1 (unsure).  One lane.  Bitmaps (staged by the caller, the wave's area): bsp = line
+// terminators, bcol = '@', beol = '+'.  Line lengths include a '\r' of "\r\n" (equal on both
+// lines of a consistently terminated record).
+__device__ __forceinline__ int infer_phase(const ScanShared& sh, u32 wid) {
     bool ok[4] = {true, true, true, true};
     int seqlen[4] = {-1, -1, -1, -1};
     int prev = -1, k = 0;
-    for (int w = 0; w < WG && k < PHASE_LINES; ++w) {
-        u64 m = sh.bsp[w];
+    for (int w = 0; w < SEGS && k < PHASE_LINES; ++w) {
+        u64 m = sh.bsp[wid][w];
         while (m && k < PHASE_LINES) {
             const int e = w * SEG + (__ffsll((long long)m) - 1);
             m &= m - 1;
             if (prev >= 0) {  // the line [prev+1, e)
                 const int st = prev + 1;
                 const int len = e - st;
-                const bool is_at = len > 0 && ((sh.bcol[st >> 6] >> (st & 63)) & 1ull);
-                const bool is_plus = len > 0 && ((sh.beol[st >> 6] >> (st & 63)) & 1ull);
+                const bool is_at = len > 0 && ((sh.bcol[wid][st >> 6] >> (st & 63)) & 1ull);
+                const bool is_plus = len > 0 && ((sh.beol[wid][st >> 6] >> (st & 63)) & 1ull);
 #pragma unroll
                 for (int P = 0; P < 4; ++P) {
                     const int ph = (P + k + 1) & 3;
@@ -802,155 +780,154 @@ __device__ __forceinline__ int infer_phase(const ScanShared& sh) {
     return nfound == 1 ? found : -1;
 }
 
-// insert up to B entries with their first slot loads issued together (latency overlap)
-template <int B>
-__device__ __forceinline__ u32 insert_many(const ScanArgs& a, const u64 (&key)[B], const u64 (&cnt)[B],
-                                           const u64 (&ord)[B], const bool (&valid)[B]) {
-    const Table T = *a.tab;
-    uint4 w0[B], w1[B];
-    u64 h[B];
-#pragma unroll
-    for (int b = 0; b < B; ++b) {
-        h[b] = table_home(key[b], T.mask);
-        if (valid[b]) {
-            const GSlot* sl = &T.slots[h[b]];
-            w0[b] = *(const uint4*)sl;
-            w1[b] = *((const uint4*)sl + 1);
-        }
-    }
-    u32 made = 0;
-#pragma unroll
-    for (int b = 0; b < B; ++b) {
-        if (!valid[b]) continue;
-        const u64 k = ((u64)w0[b].y << 32) | w0[b].x;
-        if (k == key[b]) {  // the common case: the code is already in the table
-            GSlot* sl = &T.slots[h[b]];
-            if (a.ablate & 128u) {  // timing ablation: plain stores instead of atomics (wrong counts)
-                sl->count = cnt[b];
-                continue;
-            }
-            atomicAdd((unsigned long long*)&sl->count, (unsigned long long)cnt[b]);
-            const u64 first = ((u64)w1[b].y << 32) | w1[b].x;
-            if (ord[b] < first) atomicMin((unsigned long long*)&sl->first, (unsigned long long)ord[b]);
-            if (w1[b].z < a.file_tag) atomicMax(&sl->last_tag, a.file_tag);
-        } else {
-            made += global_insert(T, a.st, key[b], cnt[b], ord[b], a.file_tag) ? 1u : 0u;
-        }
-    }
-    return made;
+// the line phase at wave-tile t, guessed from its content (infer_phase); -1 unsure.  Whole wave.
+__device__ __attribute__((noinline)) int guess_phase(ScanShared& sh, const ScanArgs& a, u32 t, int lane, u32 wid) {
+    SegRegs r;
+    seg_load(a, t, r, lane);
+    const SegClass sc = seg_classify(a, t, r, lane);
+    u64 at, plus;
+    seg_marks(r, at, plus);
+    sh.bsp[wid][lane] = sc.tmask;  // infer_phase: terminators, '@', '+'
+    sh.bcol[wid][lane] = at;
+    sh.beol[wid][lane] = plus;
+    lds_fence();
+    int P = 0;
+    if (lane == 0) P = infer_phase(sh, wid);
+    return __shfl(P, 0, 64);
 }
 
-// Insert B (key, count, min ordinal) entries into the HBM table in rounds: each round loads the
-// current probe slot of every pending entry together, then settles hits with fire-and-forget atomics
-// and claims empty slots with CASes issued together, so a lane waits for max-probe-depth round trips,
-// not for the sum over its entries (insert_many + global_insert walk each miss serially).
-#ifndef FR_COMMIT2
-#define FR_COMMIT2 0
-#endif
-#ifndef FR_CB2
-#define FR_CB2 4
-#endif
-constexpr int CB2 = FR_CB2;
-template <int B>
-__device__ __forceinline__ u32 insert_rounds(const ScanArgs& a, const u64 (&key)[B], const u32 (&cnt)[B],
-                                             const u64 (&ord)[B], const bool (&valid)[B]) {
-    const Table& T = *a.tab;
-    const u64 mask = T.mask;
-    GSlot* const slots = T.slots;
-    u32 h[B];  // slot index (tables stay below 2^32 slots)
-    bool pend[B];
+// Commit: resolve first, update last.  A wait for a load or CAS return also waits for every
+// vector-memory op issued before it (vmcnt counts in order), and under the streaming load of the
+// other workgroups each round trip is long; so every entry's table slot is found before any count
+// is added.  resolve_batch walks CE entries per lane in rounds: the probe loads of all pending
+// entries together, then the CASes that claim empty slots together; it adds nothing.  The count /
+// first / tag atomics follow in apply_entry, fire-and-forget: an LDS-only barrier ends the commit.
+struct Resolved {
+    u32 slot;      // the key's slot; ~0: probe bound exceeded (the overflow list takes the entry)
+    u32 tag;       // the slot's last_tag as loaded (0: claimed now, or unknown)
+    u64 first;     // the slot's first as loaded (~0: claimed now, or unknown)
+};
+
+template <int CE>
+__device__ __forceinline__ u32 resolve_batch(const ScanArgs& a, const u64 (&key)[CE], const bool (&valid)[CE],
+                                             Resolved (&rs)[CE]) {
+    const Table& T = a.tabv;
+    bool pend[CE];
 #pragma unroll
-    for (int b = 0; b < B; ++b) {
-        h[b] = (u32)table_home(key[b], mask);
+    for (int b = 0; b < CE; ++b) {
+        rs[b].slot = (u32)table_home(key[b], T.mask);
+        rs[b].first = ~0ull;
+        rs[b].tag = 0;
         pend[b] = valid[b];
     }
     u32 made = 0;
     for (int round = 0; round < GPROBE; ++round) {
         bool any = false;
 #pragma unroll
-        for (int b = 0; b < B; ++b) any |= pend[b];
-        if (!any) break;
-        u64 k[B], first[B];
-        u32 tag[B];
+        for (int b = 0; b < CE; ++b) any |= pend[b];
+        if (!any) return made;
+        u64 k[CE];
 #pragma unroll
-        for (int b = 0; b < B; ++b) {
+        for (int b = 0; b < CE; ++b)
             if (pend[b]) {
-                const GSlot* sl = &slots[h[b]];
-                k[b] = *(const u64*)&sl->key;
-                first[b] = *(const u64*)&sl->first;
-                tag[b] = *(const u32*)&sl->last_tag;
+                const GSlot* sl = &T.slots[rs[b].slot];
+                const uint2 w0 = *(const uint2*)sl;
+                const uint4 w1 = *((const uint4*)sl + 1);
+                k[b] = ((u64)w0.y << 32) | w0.x;
+                rs[b].first = ((u64)w1.y << 32) | w1.x;
+                rs[b].tag = w1.z;
             }
-        }
-        bool cas[B];
+        bool cas[CE];
 #pragma unroll
-        for (int b = 0; b < B; ++b) {
+        for (int b = 0; b < CE; ++b) {
             cas[b] = false;
             if (!pend[b]) continue;
-            GSlot* sl = &slots[h[b]];
-            if (k[b] == key[b]) {
-                atomicAdd((unsigned long long*)&sl->count, (unsigned long long)cnt[b]);
-                if (ord[b] < first[b]) atomicMin((unsigned long long*)&sl->first, (unsigned long long)ord[b]);
-                if (tag[b] < a.file_tag) atomicMax(&sl->last_tag, a.file_tag);
-                pend[b] = false;
-            } else if (k[b] == 0) {
-                cas[b] = true;
-            } else {
-                h[b] = (u32)((h[b] + 1ull) & mask);
-            }
+            if (k[b] == key[b]) pend[b] = false;
+            else if (k[b] == 0) cas[b] = true;
+            else rs[b].slot = (rs[b].slot + 1u) & (u32)T.mask;
         }
-        u64 old[B];
+        u64 old[CE];
 #pragma unroll
-        for (int b = 0; b < B; ++b)
-            if (cas[b]) old[b] = atomicCAS((unsigned long long*)&slots[h[b]].key, 0ull, (unsigned long long)key[b]);
+        for (int b = 0; b < CE; ++b)
+            if (cas[b]) old[b] = atomicCAS((unsigned long long*)&T.slots[rs[b].slot].key, 0ull, (unsigned long long)key[b]);
 #pragma unroll
-        for (int b = 0; b < B; ++b) {
+        for (int b = 0; b < CE; ++b) {
             if (!cas[b]) continue;
-            if (old[b] == 0 || old[b] == key[b]) {
-                GSlot* sl = &slots[h[b]];
+            if (old[b] == 0 || old[b] == key[b]) {  // claimed now, or by another workgroup meanwhile
                 made += old[b] == 0 ? 1u : 0u;
-                atomicAdd((unsigned long long*)&sl->count, (unsigned long long)cnt[b]);
-                atomicMin((unsigned long long*)&sl->first, (unsigned long long)ord[b]);
-                atomicMax(&sl->last_tag, a.file_tag);
+                rs[b].first = ~0ull;
+                rs[b].tag = 0;
                 pend[b] = false;
             } else {
-                h[b] = (u32)((h[b] + 1ull) & mask);
+                rs[b].slot = (rs[b].slot + 1u) & (u32)T.mask;
             }
         }
     }
 #pragma unroll
-    for (int b = 0; b < B; ++b) {
-        if (!pend[b]) continue;  // probe bound exceeded: the overflow list (reinserted after a rehash)
+    for (int b = 0; b < CE; ++b)
+        if (pend[b]) rs[b].slot = ~0u;
+    return made;
+}
+
+// the fire-and-forget update of one resolved entry (or its overflow-list entry)
+__device__ __forceinline__ void apply_entry(const ScanArgs& a, const Resolved& r, u64 key, u32 cnt, u64 ord) {
+    const Table& T = a.tabv;
+    if (r.slot == ~0u) {  // probe bound exceeded: the overflow list (reinserted after a rehash)
         const u64 i = atomicAdd((unsigned long long*)&a.st->n_overflow, 1ull);
         if (i < T.ovf_cap) {
             Overflow o;
-            o.key = key[b];
-            o.count = cnt[b];
-            o.first = ord[b];
+            o.key = key;
+            o.count = cnt;
+            o.first = ord;
             o.tag = a.file_tag;
             o.pad = 0;
             T.ovf[i] = o;
         } else {
             atomicOr(&a.st->cap_flags, 2u);
         }
+        return;
     }
-    return made;
+    GSlot* sl = &T.slots[r.slot];
+    if (a.ablate & 128u) {  // timing ablation: plain stores instead of atomics (wrong counts)
+        sl->count = cnt;
+        return;
+    }
+    atomicAdd((unsigned long long*)&sl->count, (unsigned long long)cnt);
+    if (ord < r.first) atomicMin((unsigned long long*)&sl->first, (unsigned long long)ord);
+    if (r.tag < a.file_tag) atomicMax(&sl->last_tag, a.file_tag);
 }
 
-// publish the LDS table and/or the cold list / buffered side effects into HBM (all threads).
-// CB entries per thread have their slot loads in flight together.
-#ifndef FR_CB
-#define FR_CB 4
-#endif
-constexpr int CB = FR_CB;
-__device__ __attribute__((noinline)) void commit_buffers(ScanShared& sh, const ScanArgs& a, bool table, int tid,
-                                                        u32 ntiles) {
-#if FR_TIMING == 2
-    const u64 q0 = __builtin_amdgcn_s_memtime();
+struct Geom {  // the launch's chunk geometry (ScanArgs' normal or heavy set, chosen at the kernel start)
+    u32 chunk_tiles, mid_chunks, num_chunks;
+};
+// After a chunk's commit (one lane): the launch's last commit decides the next launch's geometry
+// from the device's own counters (no host snapshot): heavy when at least a quarter of the chunks
+// since the reset sent their commits to the launch log.  Exotic-only replays leave it alone.
+__device__ __forceinline__ void note_commit(const ScanArgs& a, const Geom& g, bool hv) {
+    if (a.exo_only) return;
+    // relaxed: the decision is a performance heuristic (a stale log_commits only delays a switch), and
+    // a release here would write back the XCD's L2 once per chunk (MI355X_MICROARCH.md fence table)
+    const u32 prev = __hip_atomic_fetch_add(&a.st->commits_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev != g.num_chunks - 1u) return;
+    const u64 tot = __hip_atomic_load(&a.st->chunks_total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + g.num_chunks;
+    const u64 lc = __hip_atomic_load(&a.st->log_commits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&a.st->chunks_total, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&a.st->heavy[a.par ^ 1u], (lc && lc * 4 >= tot) ? 1u : 0u, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    if (hv) __hip_atomic_fetch_add(&a.st->heavy_launches, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&a.st->commits_done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// publish the LDS table and the cold list / buffered side effects into HBM (all threads): resolve
+// every entry's slot, then add (resolve_batch / apply_entry), or append them to the launch log.
+__device__ __attribute__((noinline)) void commit_buffers(ScanShared& sh, const ScanArgs& a, int tid, const Geom& g,
+                                                        bool hv) {
+#if defined(FR_STAMPS) && FR_STAMPS == 2
+    u64 cst_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    u64 cq_ = __builtin_amdgcn_s_memtime();
 #endif
     __syncthreads();
-#if FR_TIMING == 2
-    const u64 q1 = __builtin_amdgcn_s_memtime();
-#endif
+    FR_CSTAMP(0);
     u32 made = 0;
     if (a.ablate & 64u) {  // diag: flushed LDS slots and cold entries per commit
         u32 live = 0;
@@ -959,13 +936,12 @@ __device__ __attribute__((noinline)) void commit_buffers(ScanShared& sh, const S
         if (tid == 0) atomicAdd((unsigned long long*)&a.st->stamp[5], (unsigned long long)min(sh.ncold, a.cold_cap));
         if (tid == 0) atomicAdd((unsigned long long*)&a.st->stamp[6], 1ull);
     }
-    const bool flush = table && !(a.ablate & 8u);  // ablation 8: no HBM flush of the LDS table / cold list
-    const u32 nc = (a.ablate & 8u) ? 0u : min(sh.ncold, a.cold_cap);
+    const bool flush = !(a.ablate & 8u);  // ablation 8: no HBM flush of the LDS table / cold list
+    const u32 nc = flush ? min(sh.ncold, a.cold_cap) : 0u;
     const u32 nl = flush ? sh.nkeys : 0u;  // claimed LDS slots = the live ones
     bool logged = false;
     // heavy commits (at least log_min pairs: many distinct codes per chunk) go to the launch log,
     // aggregated after the launch; lighter ones insert straight into the table
-    (void)ntiles;
     if (a.log && nl + nc && nl + nc >= a.log_min) {
         // one block of the launch log for this commit's pairs (aggregated after the launch:
         // launch_log_aggregate); a block past the log's end is blanked and the pairs inserted below
@@ -980,81 +956,69 @@ __device__ __attribute__((noinline)) void commit_buffers(ScanShared& sh, const S
         __syncthreads();
         logged = sh.log_base != ~0ull;
     }
+    const u64* cl = a.cold + 2ull * (u64)blockIdx.x * a.cold_cap;
     if (logged) {
         LogEntry* out = a.log + sh.log_base;
-        if (flush)
-            for (int i = tid; i < NS; i += WG) {
-                const LSlot e = sh.ls[i];
-                if (e.key) out[atomicAdd(&sh.log_pos, 1u)] = LogEntry{e.key, e.mino, e.cnt};
-            }
-        const u64* cl = a.cold + 2ull * (u64)blockIdx.x * a.cold_cap;
+        for (int i = tid; i < NS; i += WG) {
+            const LSlot e = sh.ls[i];
+            if (e.key) out[atomicAdd(&sh.log_pos, 1u)] = LogEntry{e.key, e.mino, e.cnt};
+        }
         for (u32 i = tid; i < nc; i += WG) out[nl + i] = LogEntry{cl[2 * i], (u32)(cl[2 * i + 1] - make_ord(a, 0)), 1u};
-    } else if (FR_COMMIT2) {
-        // LDS slots and cold entries together: CB2 per lane per round of round-based inserts
-        const u64* cl = a.cold + 2ull * (u64)blockIdx.x * a.cold_cap;
-        const u32 nlds = flush ? (u32)NS : 0u;
-        for (u32 i0 = tid; i0 < nlds + nc; i0 += CB2 * WG) {
-            u64 key[CB2], ord[CB2];
-            u32 cnt[CB2];
-            bool v[CB2];
+    } else if (flush) {
+        constexpr int CL = NS / WG;  // LDS slots per lane; also cold entries per lane per batch
+        Resolved* park = (Resolved*)&sh.raw[0][0];  // the walks are done: the tile area holds NS resolutions
+        static_assert(sizeof(Resolved) * NS <= sizeof(sh.raw), "resolution parking");
+        // the first cold batch's HBM reads lead: they land while the LDS slots resolve
+        u64 ck[CL], co[CL];
+        bool cv[CL];
 #pragma unroll
-            for (int b = 0; b < CB2; ++b) {
-                const u32 i = i0 + b * WG;
-                v[b] = false;
-                key[b] = 0;
-                ord[b] = 0;
-                cnt[b] = 1;
-                if (i < nlds) {
-                    const LSlot e = sh.ls[i];
-                    v[b] = e.key != 0;
-                    key[b] = e.key;
-                    cnt[b] = e.cnt;
-                    ord[b] = make_ord(a, e.mino);
-                } else if (i < nlds + nc) {
-                    v[b] = true;
-                    key[b] = cl[2 * (i - nlds)];
-                    ord[b] = cl[2 * (i - nlds) + 1];
-                }
+        for (int b = 0; b < CL; ++b) {
+            const u32 i = tid + b * WG;
+            cv[b] = i < nc;
+            ck[b] = cv[b] ? cl[2 * i] : 0;
+            co[b] = cv[b] ? cl[2 * i + 1] : 0;
+        }
+        {
+            u64 lk[CL];
+            bool lv[CL];
+            Resolved rs[CL];
+#pragma unroll
+            for (int b = 0; b < CL; ++b) {
+                lk[b] = sh.ls[tid + b * WG].key;
+                lv[b] = lk[b] != 0;
             }
-            made += insert_rounds<CB2>(a, key, cnt, ord, v);
-        }
-    }
-    if (!FR_COMMIT2 && !logged && flush) {
-        for (int i0 = tid; i0 < NS; i0 += CB * WG) {
-            u64 key[CB], cnt[CB], ord[CB];
-            bool v[CB];
+            made += resolve_batch<CL>(a, lk, lv, rs);
 #pragma unroll
-            for (int b = 0; b < CB; ++b) {
-                const int i = i0 + b * WG;
-                const LSlot e = i < NS ? sh.ls[i] : LSlot{0, 0, 0};
-                v[b] = e.key != 0;
-                key[b] = e.key;
-                cnt[b] = e.cnt;
-                ord[b] = v[b] ? make_ord(a, e.mino) : 0;
+            for (int b = 0; b < CL; ++b) park[tid + b * WG] = rs[b];
+        }
+        FR_CSTAMP(1);
+        Resolved rc[CL];
+        made += resolve_batch<CL>(a, ck, cv, rc);
+        FR_CSTAMP(2);
+        // every slot is known: the updates, none waited for
+#pragma unroll
+        for (int b = 0; b < CL; ++b) {
+            const LSlot e = sh.ls[tid + b * WG];
+            if (e.key) apply_entry(a, park[tid + b * WG], e.key, e.cnt, make_ord(a, e.mino));
+        }
+#pragma unroll
+        for (int b = 0; b < CL; ++b)
+            if (cv[b]) apply_entry(a, rc[b], ck[b], 1u, co[b]);
+        // a cold list of more than NS entries: further batches, each resolved, then applied
+        for (u32 c0 = CL * WG; c0 < nc; c0 += CL * WG) {
+#pragma unroll
+            for (int b = 0; b < CL; ++b) {
+                const u32 i = c0 + tid + b * WG;
+                cv[b] = i < nc;
+                ck[b] = cv[b] ? cl[2 * i] : 0;
+                co[b] = cv[b] ? cl[2 * i + 1] : 0;
             }
-            made += insert_many<CB>(a, key, cnt, ord, v);
-        }
-    }
-#if FR_TIMING == 2
-    const u64 q15 = __builtin_amdgcn_s_memtime();
-#endif
-    const u64* cl = a.cold + 2ull * (u64)blockIdx.x * a.cold_cap;
-    for (u32 i0 = tid; i0 < ((logged || FR_COMMIT2) ? 0u : nc); i0 += CB * WG) {
-        u64 key[CB], cnt[CB], ord[CB];
-        bool v[CB];
+            made += resolve_batch<CL>(a, ck, cv, rc);
 #pragma unroll
-        for (int b = 0; b < CB; ++b) {
-            const u32 i = i0 + b * WG;
-            v[b] = i < nc;
-            key[b] = v[b] ? cl[2 * i] : 0;
-            ord[b] = v[b] ? cl[2 * i + 1] : 0;
-            cnt[b] = 1;
+            for (int b = 0; b < CL; ++b)
+                if (cv[b]) apply_entry(a, rc[b], ck[b], 1u, co[b]);
         }
-        made += insert_many<CB>(a, key, cnt, ord, v);
     }
-#if FR_TIMING == 2
-    const u64 q2 = __builtin_amdgcn_s_memtime();
-#endif
     if (made) atomicAdd(&sh.created, made);
     // buffered exotic records and the first "no space" error
     const u32 ne = min(sh.nexo, (u32)EXO_BUF);
@@ -1062,46 +1026,47 @@ __device__ __attribute__((noinline)) void commit_buffers(ScanShared& sh, const S
         const u64 n = sh.exo_len[k];
         const u64 i = atomicAdd((unsigned long long*)&a.st->n_exotic, 1ull);
         const u64 po = atomicAdd((unsigned long long*)&a.st->exo_pool_used, (unsigned long long)n);
-        if (i < a.tab->exo_cap && po + n <= a.tab->exo_pool_cap) {
-            a.tab->exo_ord[i] = make_ord(a, sh.exo_p[k]);
-            a.tab->exo_off[i] = po;
-            a.tab->exo_len[i] = (u32)n;
-            for (u64 q = 0; q < n; ++q) a.tab->exo_pool[po + q] = a.buf[sh.exo_start[k] + q];
+        if (i < a.tabv.exo_cap && po + n <= a.tabv.exo_pool_cap) {
+            a.tabv.exo_ord[i] = make_ord(a, sh.exo_p[k]);
+            a.tabv.exo_off[i] = po;
+            a.tabv.exo_len[i] = (u32)n;
+            for (u64 q = 0; q < n; ++q) a.tabv.exo_pool[po + q] = a.buf[sh.exo_start[k] + q];
         } else {
             atomicOr(&a.st->cap_flags, 4u);
         }
     }
     if (tid == 0 && sh.err_off != 0xFFFFFFFFu)
         atomicMin((unsigned long long*)&a.st->err_nospace, (unsigned long long)(a.file_offset + sh.err_off));
-    __syncthreads();
-#if FR_TIMING == 2
-    const u64 q3 = __builtin_amdgcn_s_memtime();
-    if ((tid & 63) == 0) {  // diagnostic build only: commit phases (entry barrier, inserts, exit barrier)
-        atomicAdd((unsigned long long*)&a.st->stamp[0], (unsigned long long)(q1 - q0));
-        atomicAdd((unsigned long long*)&a.st->stamp[1], (unsigned long long)(q2 - q1));
-        atomicAdd((unsigned long long*)&a.st->stamp[2], (unsigned long long)(q3 - q2));
-        atomicAdd((unsigned long long*)&a.st->stamp[3], (unsigned long long)(q15 - q1));  // of which the LDS-table part
-    }
-#endif
-    if (table)
-        for (int i = tid; i < NS; i += WG) {
-            sh.ls[i] = LSlot{0, 0, 0xFFFFFFFFu};
-        }
+    // (in here, not in the chunk loop: lane-divergent code at the loop's end made the structurizer move
+    // it out of the loop, past the ticket barrier, for one lane)
+    if (tid == 0) note_commit(a, g, hv);
+    FR_CSTAMP(3);
+    // LDS-only barriers from here: the commit's count atomics, log entries and exotic bytes stay in
+    // flight (no later read in this launch needs them), while the LDS table is reset for the next chunk
+    lds_barrier();
+    FR_CSTAMP(4);
+    for (int i = tid; i < NS; i += WG) sh.ls[i] = LSlot{0, 0, 0xFFFFFFFFu};
     if (tid == 0) {
-        if (table) sh.nkeys = 0;
+        sh.nkeys = 0;
         sh.ncold = 0;
         sh.nexo = 0;
         sh.err_off = 0xFFFFFFFFu;
+        sh.spec_bad = 0;
     }
-    __syncthreads();
+    lds_barrier();
+#if defined(FR_STAMPS) && FR_STAMPS == 2
+    FR_CSTAMP(5);
+    cst_[6] = nl;
+    cst_[7] = nc;
+    if ((tid & 63) == 0)
+        for (int i_ = 0; i_ < 8; ++i_) atomicAdd((unsigned long long*)&a.st->stamp[i_], (unsigned long long)cst_[i_]);
+#endif
 }
 
-// drop everything buffered (a failed speculation)
+// drop everything buffered (a redone chunk)
 __device__ __forceinline__ void discard_buffers(ScanShared& sh, int tid) {
     __syncthreads();
-    for (int i = tid; i < NS; i += WG) {
-        sh.ls[i] = LSlot{0, 0, 0xFFFFFFFFu};
-    }
+    for (int i = tid; i < NS; i += WG) sh.ls[i] = LSlot{0, 0, 0xFFFFFFFFu};
     if (tid == 0) {
         sh.nkeys = 0;
         sh.ncold = 0;
@@ -1114,23 +1079,14 @@ __device__ __forceinline__ void discard_buffers(ScanShared& sh, int tid) {
 
 __device__ __forceinline__ bool uniform_flag(u32 v) { return __builtin_amdgcn_readfirstlane(v) != 0; }
 
-// code bytes [start, start+n) of the tile -> fast key with v_perm SWAR, 4 bytes per step (false
-// if outside the fast alphabet).  The bytes come from HBM/L2 through a range-checked buffer
-// descriptor over [tile0, avail) (zeros past the data: such codes fail here and take the exotic
-// path, which reads them exactly).  Byte index i = (c >> 1) & 7 selects the expected byte
-// (A C T G - + - N) and its symbol (A1 C2 G3 T4 N5 +6); a byte is valid iff it equals the
-// expected one.
-__device__ __forceinline__ void encode_load(const ScanArgs& a, u64 tile0, u32 start, u32 (&w)[8]) {
-    const u64 base = (u64)(a.buf + tile0);
-    const u32 lo = __builtin_amdgcn_readfirstlane((u32)base), hi = __builtin_amdgcn_readfirstlane((u32)(base >> 32));
-    const u32 nrec = (u32)min(a.avail - tile0, (u64)0xFFFFFFF0u);
-    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(((u64)hi << 32) | lo), (short)0,
-                                                        (int)__builtin_amdgcn_readfirstlane(nrec), 0x00020000);
-    const u32 b4 = start & ~3u;
-    const auto v0 = __builtin_amdgcn_raw_buffer_load_b128(rsrc, b4, 0, 0);
-    const auto v1 = __builtin_amdgcn_raw_buffer_load_b128(rsrc, b4, 16, 0);
-    w[0] = v0[0]; w[1] = v0[1]; w[2] = v0[2]; w[3] = v0[3];
-    w[4] = v1[0]; w[5] = v1[1]; w[6] = v1[2]; w[7] = v1[3];
+// code bytes at [start, start + n) of the wave's LDS copy -> fast key with v_perm SWAR, 4 bytes per
+// step (false if outside the fast alphabet).  Byte index i = (c >> 1) & 7 selects the expected
+// byte (A C T G - + - N) and its symbol (A1 C2 G3 T4 N5 +6); a byte is valid iff it equals the
+// expected one.  Eight dwords from start & ~3 (bytes past the tile read the next area; masked off).
+__device__ __forceinline__ void encode_load_lds(const ScanShared& sh, u32 wid, u32 start, u32 (&w)[8]) {
+    const lds_u32* p = (const lds_u32*)(&sh.raw[wid][0]) + (start >> 2);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) w[k] = p[k];
 }
 
 __device__ __forceinline__ bool encode_pack(const u32 (&w)[8], u32 start, u32 n, u64& key) {
@@ -1155,174 +1111,14 @@ __device__ __forceinline__ bool encode_pack(const u32 (&w)[8], u32 start, u32 n,
     return bad == 0;
 }
 
-// the code window from the tile's LDS copy: eight dwords from start & ~3 (bytes past the tile read the
-// struct's next fields; encode_pack masks them off)
-__device__ __forceinline__ void encode_load_lds(const ScanShared& sh, u32 start, u32 (&w)[8]) {
-#if FR_LDS_RAW
-    const __attribute__((address_space(3))) u32* p =
-        (const __attribute__((address_space(3))) u32*)(&sh.raw[0]) + (start >> 2);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) w[k] = p[k];
-#else
-    (void)sh; (void)start;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) w[k] = 0;
-#endif
+// the rare header outcomes (range offsets): word-scan fallback, no ' ' (IndexError), or an exotic code
+__device__ FR_COLD void slow_header(ScanShared& sh, const ScanArgs& a, u32 p, int r, u32 start, u32 n) {
+    if (r == 2) process_header_global(sh, a, p);
+    else if (r == 1) nospace(a, p, sh);
+    else exotic_record(a, p, start, n, sh);
 }
 
-__device__ __forceinline__ bool encode_glob(const ScanShared& sh, const ScanArgs& a, u64 tile0, u32 start, u32 n,
-                                            u64& key) {
-    if (n < 1 || n > (u32)MAXSYM) return false;
-    u32 w[8];
-    if (FR_LDS_RAW) encode_load_lds(sh, start, w);
-    else encode_load(a, tile0, start, w);
-    return encode_pack(w, start, n, key);
-}
-
-// the rare header outcomes: word-scan fallback, no ' ' (IndexError), or an exotic code
-__device__ FR_COLD void slow_header(ScanShared& sh, const ScanArgs& a, u64 tile0, u32 p, int r, u32 start, u32 n) {
-    if (r == 2) process_header_global(sh, a, tile0, p);
-    else if (r == 1) nospace(a, tile0, p, sh);
-    else exotic_record(a, tile0, p, start, n, sh);
-}
-
-// lowest set bit of a 128-bit window, >= 128 when empty (v_ffbl gives ~0 for a zero word, and
-// OR-ing the word's base keeps ~0, so a min over the four words needs no select)
-__device__ __forceinline__ u32 ctz128(u64 lo, u64 hi) {
-    const u32 a = (u32)__builtin_ctzg((u32)lo, -1), b = (u32)__builtin_ctzg((u32)(lo >> 32), -1) | 32u;
-    const u32 c = (u32)__builtin_ctzg((u32)hi, -1) | 64u, d = (u32)__builtin_ctzg((u32)(hi >> 32), -1) | 96u;
-    return min(min(a, b), min(c, d));
-}
-
-// leading zeros of a 128-bit window counted from bit 127, ~0 when empty
-__device__ __forceinline__ u32 clz128(u64 lo, u64 hi) {
-    const u32 a = (u32)__builtin_clzg((u32)(hi >> 32), -1), b = (u32)__builtin_clzg((u32)hi, -1) | 32u;
-    const u32 c = (u32)__builtin_clzg((u32)(lo >> 32), -1) | 64u, d = (u32)__builtin_clzg((u32)lo, -1) | 96u;
-    return min(min(a, b), min(c, d));
-}
-
-// returns 0 parsed (code at [start, start+n)), 1 no ' ' on the line, 2 fall back to the word scan.
-// The line's bitmaps are read as one 128-bit window (segments w and w+1; past the tile the second
-// is the zero entry), branch-free: the first ' ' / line end f1, the token end f2 (the next one),
-// and the last ':' below f2 (one at or before f1 leaves the code right after f1).  Lines whose
-// code does not end inside the window take the word scan.
-__device__ __forceinline__ int locate_code_bm(const ScanShared& sh, u32 p, u32 bl, u32& start, u32& n) {
-    if (p >= bl) return 2;
-    const u32 w = p >> 6, b = p & 63u;
-    const u32 wn = (w + 1u) * 64u < bl ? w + 1u : (u32)WG;
-    const u64 s0 = sh.bsp[w], s1 = sh.bsp[wn], e0 = sh.beol[w], e1 = sh.beol[wn];
-    const u64 c0 = sh.bcol[w], c1 = sh.bcol[wn];
-    const u64 v0 = (s0 | e0) & (~0ull << b), v1 = s1 | e1;  // window positions relative to segment w
-    const u32 f1 = ctz128(v0, v1);
-    const u64 v0b = v0 & (v0 - 1ull), v1b = v0 ? v1 : (v1 & (v1 - 1ull));  // drop bit f1
-    const u32 f2 = ctz128(v0b, v1b);
-    const bool at_eol = (((f1 < 64u ? e0 : e1) >> (f1 & 63u)) & 1ull) != 0;
-    const u64 t = (1ull << (f2 & 63u)) - 1ull;              // colons below f2
-    const u64 k0 = f2 >= 64u ? ~0ull : t, k1 = f2 >= 64u ? t : 0ull;
-    const u32 hc = clz128(c0 & k0, c1 & k1) ^ 127u;         // highest such colon (negative if none)
-    const u32 lastc = (u32)max((int)f1, (int)hc);
-    start = w * 64u + lastc + 1u;
-    n = f2 - lastc - 1u;
-    return f1 >= 128u ? 2 : at_eol ? 1 : f2 >= 128u ? 2 : 0;
-}
-
-// R2 via the tile's ' ' / ':' / line-end bitmaps: first ' ', then the next ' ' or line end,
-// then the last ':' between them.  Lines that reach past the tile's bitmaps fall back to the
-// word-scan parser (process_header).
-__device__ __forceinline__ void process_header_bm(ScanShared& sh, const ScanArgs& a, u64 tile0, u32 p, u32 bl) {
-    u32 start = 0, n = 0;
-    int r = locate_code_bm(sh, p, bl, start, n);
-    u64 key = 0;
-    bool fast = false;
-    if (r == 0) {
-        if (a.ablate & 2u) {
-            asm volatile("" ::"v"(start), "v"(n));
-            return;
-        }
-        if (!FR_LDS_RAW && (u64)(start & ~3u) + 32u > a.avail - tile0) r = 2;  // the loads would straddle the data end
-        else fast = encode_glob(sh, a, tile0, start, n, key);
-    }
-    if (fast) count_code(sh, a, tile0, p, key);
-    else rare_push(sh, a, (u32)(tile0 + p), (u32)r, (u32)(tile0 + start), n);
-}
-
-// Every 4th line start whose terminator lies in this lane's 64-B segment is a header owned by
-// this lane (the range's first byte by lane 0 of its first tile): parse it where it lies.  No
-// header list, no block scan: the tile's line prefix (seg_count) gives each lane its index.
-__device__ __forceinline__ void parse_own_headers(ScanShared& sh, const ScanArgs& a, u32 t, const TileCount& tc,
-                                                  u64 L0, int tid, SegRegs& r, bool pf) {
-    const u64 tile0 = (u64)t * TSTEP;
-    const u32 nb = (u32)min((u64)(TILE + HALO), a.avail - tile0);
-    const u32 bl = min((u32)TILE, nb);
-    const u32 rem = (u32)min(a.len - tile0, (u64)0xFFFFFFFFu);  // line starts p < rem lie in the range
-    const u32 s0 = tid * SEG;
-    const bool own0 = t == 0 && tid == 0 && a.own_start && (L0 & 3ull) == 0 && a.avail > 0 &&
-                      (a.max_records <= 0 || (i64)(L0 >> 2) < a.max_records);
-    // the i-th terminator (from 0) of this segment starts line lb + i + 1: a header line when
-    // i = 3 - lb (mod 4); skip to the first such terminator, then step four at a time
-    const u32 lb32 = (u32)L0 + tc.wexcl + (tc.x - tc.c);  // the phase needs the low bits only
-    const u32 skip = (3u - lb32) & 3u;
-    u64 m = tc.tmask;
-#pragma unroll
-    for (u32 q = 0; q < 3; ++q) m = q < skip ? (m & (m - 1)) : m;
-    const bool limited = a.max_records > 0;  // -s: uniform
-    u64 rec = limited ? (L0 + tc.wexcl + (tc.x - tc.c) + skip + 1u) >> 2 : 0ull;  // next candidate's record
-    auto next = [&]() -> int {
-        if (!m) return -1;
-        const u32 p = s0 + (u32)__builtin_ctzll(m) + 1u;
-        if (__builtin_popcountll(m) > 4) {  // another header in this segment (short records)
-            m &= m - 1;
-            m &= m - 1;
-            m &= m - 1;
-            m &= m - 1;
-        } else {
-            m = 0;
-        }
-        const bool mine = p < rem || (a.own_end && tile0 + p == a.len && tile0 + p < a.avail);
-        if (!mine || (limited && (i64)rec >= a.max_records)) {  // so are all later ones
-            m = 0;
-            return -1;
-        }
-        rec += 1;
-        return (int)p;
-    };
-    // The first header in two stages around the next tile's segment loads: its code-byte loads
-    // are issued before them (vector loads complete in order, so the parse never waits on the
-    // prefetch), and the prefetch's HBM latency overlaps the encode and the LDS insert.
-    const int p1 = own0 ? 0 : next();
-    u32 start = 0, n = 0;
-    int rr = 0;
-    u32 w[8];
-    if (p1 >= 0) {
-        rr = locate_code_bm(sh, (u32)p1, bl, start, n);
-        if (!FR_LDS_RAW && rr == 0 && (u64)(start & ~3u) + 32u > a.avail - tile0) rr = 2;  // loads would straddle the data end
-        if (rr == 0 && !(a.ablate & 2u)) {
-            if (FR_LDS_RAW) encode_load_lds(sh, start, w);
-            else encode_load(a, tile0, start, w);
-        }
-    }
-    // always five loads (zeros when there is no next tile or it reaches the data end), so the
-    // compiler's wait counts for the code bytes stay exact on every path
-    if (FR_PREFETCH) seg_fetch(a, t + 1, r, tid, pf);
-    if (p1 >= 0) {
-        if (rr == 0 && (a.ablate & 2u)) {
-            asm volatile("" ::"v"(start), "v"(n));
-        } else {
-            u64 key = 0;
-            const bool fast = rr == 0 && encode_pack(w, start, n, key);
-            if (fast) count_code(sh, a, tile0, (u32)p1, key);
-            else rare_push(sh, a, (u32)(tile0 + (u32)p1), (u32)rr, (u32)(tile0 + start), n);
-        }
-    }
-    if (p1 < 0) return;
-    for (;;) {
-        const int p = next();
-        if (p < 0) break;
-        process_header_bm(sh, a, tile0, (u32)p, bl);
-    }
-}
-
-// ---- header parse v2 (FR_PARSE2): fewer VALU instructions per header ------------------------
+// ---- header parse: two 64-bit bitmap windows, wave-uniform code length encode ---------------
 // v_ffbl / v_ffbh return ~0 for 0, which the min tricks below rely on; the builtins add a
 // compare and select per word (or make the zero case undefined).
 __device__ __forceinline__ u32 ffbl32(u32 x) {
@@ -1342,23 +1138,24 @@ __device__ __forceinline__ int hsb64x(u64 x) { return (int)(min(ffbh32((u32)(x >
 // bits [b, b + 64) of the 128-bit (x0, x1), b in [0, 63]
 __device__ __forceinline__ u64 window64(u64 x0, u64 x1, u32 b) { return (x0 >> b) | ((x1 << 1) << (63u - b)); }
 
-// R2 on the tile's bitmaps in two 64-bit windows: from the line start p the first ' ' or line end
-// f1 (a line end first: no ' ', IndexError); from the token start q = f1 + 1 the token end f2 and
-// the last ':' before it.  0: code at [start, start + n); 1: no ' '; 2: word-scan fallback (the
-// first ' ' or the token end lies 64 or more bytes on, or the token starts past the tile).
-__device__ __forceinline__ int locate_code2(const ScanShared& sh, u32 p, u32 bl, u32& start, u32& n) {
+// R2 on the wave-tile's bitmaps in two 64-bit windows: from the line start p the first ' ' or line
+// end f1 (a line end first: no ' ', IndexError); from the token start q = f1 + 1 the token end f2
+// and the last ':' before it.  0: code at [start, start + n) (tile offsets); 1: no ' '; 2: word-scan
+// fallback (the first ' ' or the token end lies 64 or more bytes on, or the token starts past the
+// staged bytes).
+__device__ __forceinline__ int locate_code(const ScanShared& sh, u32 wid, u32 p, u32 bl, u32& start, u32& n) {
     if (p >= bl) return 2;
     const u32 w = p >> 6, b = p & 63u;
-    const u64 se = window64(sh.bsp[w], sh.bsp[w + 1], b);
-    const u64 eo = window64(sh.beol[w], sh.beol[w + 1], b);
+    const u64 se = window64(sh.bsp[wid][w], sh.bsp[wid][w + 1], b);
+    const u64 eo = window64(sh.beol[wid][w], sh.beol[wid][w + 1], b);
     const u32 f1 = ctz64x(se);
     const u32 q = p + f1 + 1u;
     if (f1 >= 64u) return 2;
     if (ctz64x(eo) == f1) return 1;
     if (q >= bl) return 2;
     const u32 w2 = q >> 6, b2 = q & 63u;
-    const u64 se2 = window64(sh.bsp[w2], sh.bsp[w2 + 1], b2);
-    const u64 co2 = window64(sh.bcol[w2], sh.bcol[w2 + 1], b2);
+    const u64 se2 = window64(sh.bsp[wid][w2], sh.bsp[wid][w2 + 1], b2);
+    const u64 co2 = window64(sh.bcol[wid][w2], sh.bcol[wid][w2 + 1], b2);
     const u32 f2 = ctz64x(se2);
     if (f2 >= 64u) return 2;
     const int hc = hsb64x(co2 & ((1ull << f2) - 1ull));  // the last ':' of the token, < 0 none
@@ -1368,11 +1165,11 @@ __device__ __forceinline__ int locate_code2(const ScanShared& sh, u32 p, u32 bl,
     return 0;
 }
 
-// code bytes [start, start + n) from the tile's LDS copy -> fast key, n wave-uniform (nu): the
+// code bytes [start, start + n) from the wave's LDS copy -> fast key, n wave-uniform (nu): the
 // per-word byte masks are scalars and only the words the code reaches are packed
-__device__ __forceinline__ bool encode_uniform(const ScanShared& sh, u32 start, u32 nu, u64& key) {
+__device__ __forceinline__ bool encode_uniform(const ScanShared& sh, u32 wid, u32 start, u32 nu, u64& key) {
     u32 w[8];
-    encode_load_lds(sh, start, w);
+    encode_load_lds(sh, wid, start, w);
     const u32 al = start & 3u;
     u32 bad = 0, lo = 0, hi = 0;
 #pragma unroll
@@ -1400,9 +1197,9 @@ __device__ __forceinline__ bool encode_uniform(const ScanShared& sh, u32 start, 
     return bad == 0;
 }
 
-__device__ __forceinline__ void parse_header2(ScanShared& sh, const ScanArgs& a, u64 tile0, u32 p, u32 bl) {
+__device__ __forceinline__ void parse_header(ScanShared& sh, const ScanArgs& a, u32 wid, u32 tile0, u32 p, u32 bl) {
     u32 start = 0, n = 0;
-    const int r = locate_code2(sh, p, bl, start, n);
+    const int r = locate_code(sh, wid, p, bl, start, n);
     if (a.ablate & 2u) {
         asm volatile("" ::"v"(start), "v"(n), "v"(r));
         return;
@@ -1411,32 +1208,31 @@ __device__ __forceinline__ void parse_header2(ScanShared& sh, const ScanArgs& a,
     bool fast = false;
     if (r == 0 && n >= 1u && n <= (u32)MAXSYM) {
         const u32 nu = __builtin_amdgcn_readfirstlane(n);
-        if (__ballot(n != nu) == 0) fast = encode_uniform(sh, start, nu, key);  // the common case
-        else fast = encode_glob(sh, a, tile0, start, n, key);
+        if (__ballot(n != nu) == 0) {
+            fast = encode_uniform(sh, wid, start, nu, key);  // the common case
+        } else {
+            u32 w[8];
+            encode_load_lds(sh, wid, start, w);
+            fast = encode_pack(w, start, n, key);
+        }
     }
-    if (fast) count_code(sh, a, tile0, p, key);
-    else rare_push(sh, a, (u32)(tile0 + p), (u32)r, (u32)(tile0 + start), n);
+    if (fast) count_code(sh, a, tile0 + p, key);
+    else rare_push(sh, a, tile0 + p, (u32)r, tile0 + start, n);
 }
 
-// the line starts after every 4th terminator (lines ≡ 0 mod 4) in this lane's segment, parsed
-// where they lie.  The first header needs the skip-th set bit of the terminator mask; a second
-// one in the same segment (records shorter than 64 B) takes the loop at the end.
-__device__ __forceinline__ void parse_own_headers2(ScanShared& sh, const ScanArgs& a, u32 t, const SegClass& sc,
-                                                   u64 L0, int tid, int wid) {
+// The line starts after every 4th terminator (lines == 0 mod 4) in this lane's segment, parsed
+// where they lie.  L0 = lines before the wave-tile (absolute with -s, else mod 4 suffices).  The
+// first header needs the skip-th set bit of the terminator mask; a second one in the same segment
+// (records shorter than 64 B) takes the loop at the end.
+__device__ __forceinline__ void parse_own_headers(ScanShared& sh, const ScanArgs& a, u32 t, const SegClass& sc,
+                                                  u64 L0, int lane, u32 wid) {
     const u64 tile0 = (u64)t * TSTEP;
-    const u32 nb = (u32)min((u64)(TILE + HALO), a.avail - tile0);
-    const u32 bl = min((u32)TILE, nb);
+    const u32 bl = (u32)min((u64)TILE, a.avail - tile0);
     const u64 rem64 = a.len - tile0;  // line starts p < pend are this launch's (uniform)
     const u32 pend = rem64 >= 0xFFFFFFFFull ? 0xFFFFFFFFu : (u32)rem64 + ((a.own_end && a.len < a.avail) ? 1u : 0u);
-    // terminators in earlier waves of the tile: wave sums from LDS, summed on the scalar unit
-    typedef u32 u32x4 __attribute__((ext_vector_type(4)));
-    const u32x4 ws = *(const __attribute__((address_space(3))) u32x4*)&sh.wsum[0];
-    const u32 w0 = __builtin_amdgcn_readfirstlane(ws.x), w1 = __builtin_amdgcn_readfirstlane(ws.y),
-              w2 = __builtin_amdgcn_readfirstlane(ws.z);
-    const u32 wexcl = (wid > 0 ? w0 : 0u) + (wid > 1 ? w1 : 0u) + (wid > 2 ? w2 : 0u);
-    const u32 lb = (u32)L0 + wexcl + (sc.x - sc.c);  // terminators before this segment (low bits)
+    const u32 lb = (u32)L0 + (sc.x - sc.c);  // terminators before this segment (low bits)
     const u32 skip = (3u - lb) & 3u;
-    const u32 s0 = tid * SEG;
+    const u32 s0 = lane * SEG;
     u64 m = sc.tmask;
 #pragma unroll
     for (u32 q = 0; q < 3; ++q) {
@@ -1445,13 +1241,13 @@ __device__ __forceinline__ void parse_own_headers2(ScanShared& sh, const ScanArg
     }
     const bool limited = a.max_records > 0;  // -s: uniform
     u64 rec = 0;
-    if (limited) rec = (L0 + wexcl + (sc.x - sc.c) + skip + 1u) >> 2;
-    const bool own0 = t == 0 && tid == 0 && a.own_start && (L0 & 3ull) == 0 && a.avail > 0 &&
+    if (limited) rec = (L0 + (sc.x - sc.c) + skip + 1u) >> 2;
+    const bool own0 = t == 0 && lane == 0 && a.own_start && (L0 & 3ull) == 0 && a.avail > 0 &&
                       (!limited || (i64)(L0 >> 2) < a.max_records);
     // m's lowest set bit: the first header terminator.  own0's header at position 0 comes first.
     const u32 p = own0 ? 0u : s0 + ctz64x(m) + 1u;
     const bool ok = own0 || (m != 0 && p < pend && (!limited || (i64)rec < a.max_records));
-    if (ok) parse_header2(sh, a, tile0, p, bl);
+    if (ok) parse_header(sh, a, wid, (u32)tile0, p, bl);
     // another header in this segment (records shorter than 64 B; never at R=8's 74 B): uniform check
     bool more = ok && (own0 ? m != 0 : __popcll(m) > 4);
     if (!__ballot(more)) return;
@@ -1466,7 +1262,7 @@ __device__ __forceinline__ void parse_own_headers2(ScanShared& sh, const ScanArg
         if (more) {
             const u32 pn = s0 + ctz64x(m) + 1u;
             more = pn < pend && (!limited || (i64)rec < a.max_records);
-            if (more) parse_header2(sh, a, tile0, pn, bl);
+            if (more) parse_header(sh, a, wid, (u32)tile0, pn, bl);
             ++rec;
             m &= m - 1ull;
             m &= m - 1ull;
@@ -1477,152 +1273,53 @@ __device__ __forceinline__ void parse_own_headers2(ScanShared& sh, const ScanArg
     }
 }
 
-// walk tiles [tb, te) of the range; L0 = line index (absolute, or mod-4 guess) at tile tb.
-// parse = false: count only.  (exact is kept for symmetry: with an exact phase a full cold
-// list falls back to direct HBM inserts inside lds_insert.)
-// Returns the line terminators in [tb, te).
-__device__ __forceinline__ u64 walk_chunk(ScanShared& sh, const ScanArgs& a, u32 tb, u32 te, u64 L0, bool parse, bool exact, int tid,
-                          int lane, int wid) {
+// One wave walks wave-tiles [tb, te) of the range; L0 = lines before tile tb (absolute, or only
+// mod 4 without -s).  parse = false: count only.  Returns the line terminators in [tb, te).  No
+// workgroup barrier: every LDS area the walk writes is this wave's.  Per step: the tile's bytes
+// (in registers since the previous step) go to the wave's LDS copy first, so the registers take the
+// next tile's loads at once and those stay in flight through this tile's classify AND its parse;
+// the classify reads the lane's segment back from LDS.
+__device__ __forceinline__ u64 walk_wave(ScanShared& sh, const ScanArgs& a, u32 tb, u32 te, u64 L0, bool parse,
+                                         int lane, u32 wid) {
     u64 lines = 0;
-    u32 done = sh.rq_tail;  // the caller synchronised: every thread reads the same value
-#if FR_TIMING == 1
-    u64 tm0 = 0, tm1 = 0, tm2 = 0, tm3 = 0;
-    const u64 w0 = __builtin_amdgcn_s_memtime();
-#endif
-#if FR_LDS_RAW
-    // Each lane's segment of tile t arrives in registers FR_PF_DEPTH tiles ahead: its loads are
-    // issued while tile t-FR_PF_DEPTH is parsed, so a wave keeps that many tiles of HBM reads in
-    // flight through its barriers and its parse.  After B1 the segment goes to the tile's LDS copy
-    // (the parse reads code bytes there) and the registers take the loads of tile t+FR_PF_DEPTH.
-    auto step = [&](u32 t, SegRegs& r) {
-#if FR_TIMING == 1
-        const u64 c0 = __builtin_amdgcn_s_memtime();
-#endif
-        const SegClass sc = seg_classify(a, t, r, tid);
-#if FR_TIMING == 1
-        __builtin_amdgcn_s_waitcnt(0);
-        const u64 c1 = __builtin_amdgcn_s_memtime();
-#endif
-        if (sc.hi) rare_push(sh, a, (u32)((u64)t * TSTEP) + tid * SEG, 4u,
-                             min((u32)min((u64)TSTEP, a.len - (u64)t * TSTEP) - tid * SEG, (u32)SEG), 0u);
-        lds_barrier();  // B1: the previous tile's parse is done with the bitmaps and the LDS copy
-        const u32 tail = sh.rq_tail;
-        if (tail != done) {  // uniform: nothing is pushed between B1 and B2
-            drain_rare(sh, a, done, tail, tid);
-            done = tail;
-        }
-        seg_store(sh, sc, tid, lane, wid);
-        {
-            typedef u32 u32x4 __attribute__((ext_vector_type(4)));
-            __attribute__((address_space(3))) u32x4* dst =
-                (__attribute__((address_space(3))) u32x4*)(&sh.raw[0]) + tid * (SEG / 16);
-#pragma unroll
-            for (int k = 0; k < SEG / 16; ++k) {
-                u32x4 v;
-                v.x = r.v[k].x; v.y = r.v[k].y; v.z = r.v[k].z; v.w = r.v[k].w;
-                dst[k] = v;
-            }
-            if (t + FR_PF_DEPTH < te) seg_prefetch_next(a, t + FR_PF_DEPTH, r, tid);
-        }
-        lds_barrier();  // B2
-#if FR_TIMING == 1
-        const u64 c2 = __builtin_amdgcn_s_memtime();
-#endif
-#if FR_PARSE2
-        if (parse && !uniform_flag(sh.spec_bad) && !(a.ablate & 1u))
-            parse_own_headers2(sh, a, t, sc, L0 + lines, tid, wid);
-        {
-            typedef u32 u32x4 __attribute__((ext_vector_type(4)));
-            const u32x4 ws = *(const __attribute__((address_space(3))) u32x4*)&sh.wsum[0];
-            lines += __builtin_amdgcn_readfirstlane(ws.x + ws.y + ws.z + ws.w);
-        }
-#else
-        const TileCount tc = seg_count(sh, sc, wid);
-        if (parse && !uniform_flag(sh.spec_bad) && !(a.ablate & 1u))
-            parse_own_headers(sh, a, t, tc, L0 + lines, tid, r, false);
-        lines += tc.tot;
-#endif
-#if FR_TIMING == 1
-        __builtin_amdgcn_s_waitcnt(0);
-        const u64 c3 = __builtin_amdgcn_s_memtime();
-        tm0 += c1 - c0;  // load + classify
-        tm1 += c2 - c1;  // B1 + drain + store + B2
-        tm2 += c3 - c2;  // parse
-        tm3 += 1;
-#endif
-    };
-    SegRegs rA, rB;
-    if (tb < te) seg_prefetch_next(a, tb, rA, tid);
-    if (FR_PF_DEPTH == 2 && tb + 1 < te) seg_prefetch_next(a, tb + 1, rB, tid);
-    for (u32 t = tb; t < te; t += FR_PF_DEPTH) {
-        step(t, rA);
-        if (FR_PF_DEPTH == 2 && t + 1 < te) step(t + 1, rB);
-    }
-#else
-#if FR_PREFETCH
-    // the next tile's segment is loaded during this tile's parse (parse_own_headers), so its HBM
-    // latency overlaps the parse; a tile reaching the data end is loaded bytewise instead
+    u32 done = *(const volatile lds_u32*)&sh.rq_tail[wid];
     SegRegs r;
-    seg_fetch(a, tb, r, tid, tb < te && seg_in_range(a, tb));
-#endif
+    if (tb < te) seg_load(a, tb, r, lane);
+    lds_u32x4* mine = (lds_u32x4*)(&sh.raw[wid][0]) + lane * (SEG / 16);
     for (u32 t = tb; t < te; ++t) {
-#if FR_TIMING == 1
-        const u64 c0 = __builtin_amdgcn_s_memtime();
-#endif
-#if FR_PREFETCH
-        if (!seg_in_range(a, t)) r = seg_load_tail(a, t, tid);
-#else
-        SegRegs r;
-        seg_prefetch_next(a, t, r, tid);
-#endif
-        const SegClass sc = seg_classify(a, t, r, tid);
-#if FR_TIMING == 1
-        __builtin_amdgcn_s_waitcnt(0);
-        const u64 c1 = __builtin_amdgcn_s_memtime();
-#endif
-        if (sc.hi) rare_push(sh, a, (u32)((u64)t * TSTEP) + tid * SEG, 4u,
-                             min((u32)min((u64)TSTEP, a.len - (u64)t * TSTEP) - tid * SEG, (u32)SEG), 0u);
-        lds_barrier();  // B1: the previous tile's parse is done with the bitmaps
-        const u32 tail = sh.rq_tail;
-        if (tail != done) {  // uniform: nothing is pushed between B1 and B2
-            drain_rare(sh, a, done, tail, tid);
+        // the previous tile's parse is done with the LDS copy (program order)
+#pragma unroll
+        for (int k = 0; k < SEG / 16; ++k) {
+            u32x4 v;
+            v.x = r.v[k].x; v.y = r.v[k].y; v.z = r.v[k].z; v.w = r.v[k].w;
+            mine[k] = v;
+        }
+        if (t + 1 < te) seg_load(a, t + 1, r, lane);
+        SegRegs q;
+#pragma unroll
+        for (int k = 0; k < SEG / 16; ++k) {
+            const u32x4 v = mine[k];
+            q.v[k] = make_uint4(v.x, v.y, v.z, v.w);
+        }
+        q.nx = 0;
+        const SegClass sc = seg_classify(a, t, q, lane);
+        if (sc.hi) rare_push(sh, a, (u32)((u64)t * TSTEP) + lane * SEG, 4u,
+                             min((u32)min((u64)TSTEP, a.len - (u64)t * TSTEP) - lane * SEG, (u32)SEG), 0u);
+        const u32 tail = *(const volatile lds_u32*)&sh.rq_tail[wid];
+        if (tail != done) {  // uniform: the previous tile's rare events (and this tile's UTF-8 checks)
+            drain_rare(sh, a, wid, done, tail, lane);
             done = tail;
         }
-        seg_store(sh, sc, tid, lane, wid);
-        lds_barrier();  // B2
-#if FR_TIMING == 1
-        const u64 c2 = __builtin_amdgcn_s_memtime();
-#endif
-        const TileCount tc = seg_count(sh, sc, wid);
-        const bool pf = t + 1 < te && seg_in_range(a, t + 1);
-        if (parse && !uniform_flag(sh.spec_bad) && !(a.ablate & 1u))
-            parse_own_headers(sh, a, t, tc, L0 + lines, tid, r, pf);
-        else if (FR_PREFETCH)
-            seg_fetch(a, t + 1, r, tid, pf);
-        lines += tc.tot;
-#if FR_TIMING == 1
-        __builtin_amdgcn_s_waitcnt(0);
-        const u64 c3 = __builtin_amdgcn_s_memtime();
-        tm0 += c1 - c0;  // load + classify
-        tm1 += c2 - c1;  // B1 + drain + store + B2
-        tm2 += c3 - c2;  // parse
-        tm3 += 1;
-#endif
+        sh.bsp[wid][lane] = sc.sp | sc.eol;  // token ends: ' ' or line end
+        sh.bcol[wid][lane] = sc.col;
+        sh.beol[wid][lane] = sc.eol;
+        lds_fence();
+        if (parse && !uniform_flag(sh.spec_bad) && !(a.ablate & 1u)) parse_own_headers(sh, a, t, sc, L0 + lines, lane, wid);
+        lines += sc.wtot;
     }
-#endif
-#if FR_TIMING == 1
-    if ((tid & 63) == 0) {  // diagnostic build only: per-phase shader cycles summed over waves
-        atomicAdd((unsigned long long*)&a.st->stamp[0], (unsigned long long)tm0);
-        atomicAdd((unsigned long long*)&a.st->stamp[1], (unsigned long long)tm1);
-        atomicAdd((unsigned long long*)&a.st->stamp[2], (unsigned long long)tm2);
-        atomicAdd((unsigned long long*)&a.st->stamp[3], (unsigned long long)tm3);
-        atomicAdd((unsigned long long*)&a.st->stamp[4], (unsigned long long)(__builtin_amdgcn_s_memtime() - w0));
-    }
-#endif
-    __syncthreads();  // the bitmaps are free for the caller; the last tile's events are queued
-    const u32 tail = sh.rq_tail;
-    if (tail != done) drain_rare(sh, a, done, tail, tid);
-    __syncthreads();
+    lds_fence();
+    const u32 tail = *(const volatile lds_u32*)&sh.rq_tail[wid];
+    if (tail != done) drain_rare(sh, a, wid, done, tail, lane);
     return lines;
 }
 
@@ -1631,20 +1328,20 @@ __device__ __forceinline__ u64 walk_chunk(ScanShared& sh, const ScanArgs& a, u32
 // 1 + ~(C-1)(j+1)/G tiles and the G first chunks, all taken at once, finish in ticket order;
 // mid_chunks full chunks follow; the last G chunks mirror the ramp-up, so every workgroup runs
 // out of work at about the same time.  fr_api only ramps ranges of >= 2 R(G) + C tiles.
-__device__ __forceinline__ u64 ramp_prefix(const ScanArgs& a, u64 j) {
-    return j + ((u64)(a.chunk_tiles - 1u) * j * (j + 1)) / (2ull * a.ramp_g);
+__device__ __forceinline__ u64 ramp_prefix(const ScanArgs& a, const Geom& g, u64 j) {
+    return j + ((u64)(g.chunk_tiles - 1u) * j * (j + 1)) / (2ull * a.ramp_g);
 }
 
 // Run by the workgroup that finishes the launch's last chunk: the exact line prefix of every chunk
 // (exclusive scan of the published counts), checked against the phase each committed speculative
 // chunk guessed; writes the range's line total for the next launch.
-__device__ __attribute__((noinline)) void verify_launch(ScanShared& sh, const ScanArgs& a, u64 base_lines, int tid) {
-    const u32 n = a.num_chunks;
+__device__ __attribute__((noinline)) void verify_launch(ScanShared& sh, const ScanArgs& a, u32 n, u64 base_lines,
+                                                       int tid) {
     const u32 per = (n + WG - 1) / WG;
     const u32 lo = min(tid * per, n), hi = min(lo + per, n);
     u64 sum = 0;
     for (u32 c = lo; c < hi; ++c) sum += (u32)agent_load(&a.chunk_info[c]);
-    // block exclusive scan of the per-thread sums (bitmap words are free scratch here)
+    // block exclusive scan of the per-thread sums (the wave counts are free scratch here)
     u64 x = sum;
     const int lane = tid & 63, wid = tid >> 6;
 #pragma unroll
@@ -1652,12 +1349,12 @@ __device__ __attribute__((noinline)) void verify_launch(ScanShared& sh, const Sc
         const u64 y = __shfl_up(x, d, 64);
         if (lane >= d) x += y;
     }
-    if (lane == 63) sh.bsp[wid] = x;
+    if (lane == 63) sh.wcount[wid] = x;
     __syncthreads();
     u64 before = 0, total = 0;
 #pragma unroll
-    for (int w = 0; w < WG / 64; ++w) {
-        const u64 v = sh.bsp[w];
+    for (int w = 0; w < NW; ++w) {
+        const u64 v = sh.wcount[w];
         before += w < wid ? v : 0ull;
         total += v;
     }
@@ -1674,52 +1371,30 @@ __device__ __attribute__((noinline)) void verify_launch(ScanShared& sh, const Sc
     __syncthreads();
 }
 
-// the line phase at a chunk's start, guessed from its first tile (infer_phase); -1 unsure
-__device__ __attribute__((noinline)) int guess_phase(ScanShared& sh, const ScanArgs& a, u32 tb, int tid, int lane,
-                                                     int wid) {
-    SegRegs r;
-    if ((u64)tb * TSTEP + (TILE + HALO + SEG + 4) <= a.avail) seg_fetch(a, tb, r, tid);
-    else r = seg_load_tail(a, tb, tid);
-    const SegClass sc = seg_classify(a, tb, r, tid);
-    u64 at, plus;
-    seg_marks(r, at, plus);
-    sh.bsp[tid] = sc.tmask;  // infer_phase: terminators, '@', '+'
-    sh.bcol[tid] = at;
-    sh.beol[tid] = plus;
-    __syncthreads();
-    if (tid == 0) sh.phase = infer_phase(sh);
-    __syncthreads();
-    const int P = sh.phase;
-    __syncthreads();  // the bitmaps are free again
-    return P;
-}
-
-__device__ __forceinline__ void chunk_bounds(const ScanArgs& a, u32 c, u32& tb, u32& te) {
+__device__ __forceinline__ void chunk_bounds(const ScanArgs& a, const Geom& g, u32 c, u32& tb, u32& te) {
     if (a.ramp_g == 0) {
-        tb = min(c * a.chunk_tiles, a.num_tiles);
-        te = min(tb + a.chunk_tiles, a.num_tiles);
+        tb = min(c * g.chunk_tiles, a.num_tiles);
+        te = min(tb + g.chunk_tiles, a.num_tiles);
         return;
     }
-    const u64 G = a.ramp_g, rg = ramp_prefix(a, G), mid_end = (u64)a.num_tiles - rg;
+    const u64 G = a.ramp_g, rg = ramp_prefix(a, g, G), mid_end = (u64)a.num_tiles - rg;
     if (c < G) {
-        tb = (u32)ramp_prefix(a, c);
-        te = (u32)ramp_prefix(a, c + 1);
-    } else if (c < G + a.mid_chunks) {
-        const u64 b = rg + (u64)(c - G) * a.chunk_tiles;
+        tb = (u32)ramp_prefix(a, g, c);
+        te = (u32)ramp_prefix(a, g, c + 1);
+    } else if (c < G + g.mid_chunks) {
+        const u64 b = rg + (u64)(c - G) * g.chunk_tiles;
         tb = (u32)b;
-        te = (u32)min(b + a.chunk_tiles, mid_end);
+        te = (u32)min(b + g.chunk_tiles, mid_end);
     } else {
-        const u64 j = c - G - a.mid_chunks;  // 0 .. G-1: shrinking
-        tb = (u32)((u64)a.num_tiles - ramp_prefix(a, G - j));
-        te = (u32)((u64)a.num_tiles - ramp_prefix(a, G - j - 1));
+        const u64 j = c - G - g.mid_chunks;  // 0 .. G-1: shrinking
+        tb = (u32)((u64)a.num_tiles - ramp_prefix(a, g, G - j));
+        te = (u32)((u64)a.num_tiles - ramp_prefix(a, g, G - j - 1));
     }
 }
 
 #ifndef FR_OCC
-#define FR_OCC 4  // workgroups (= waves per SIMD) per CU: the tile's LDS copy (FR_LDS_RAW) makes a workgroup
-                  // 39 KB, so 4 share a CU's 160 KB; 128 VGPRs hold the next tile's loads through the parse
-                  // (without the LDS copy 5 per CU at 96 VGPRs measured best); fr_api sizes the grid with
-                  // fr_chunk_occupancy()
+#define FR_OCC 4  // workgroups (= waves per SIMD) per CU: ~39 KB of LDS per workgroup (the wave-tile copies
+                  // and the LDS table) fit 4 in a CU's 160 KB; fr_api sizes the grid with chunk_occupancy()
 #endif
 __global__ __launch_bounds__(WG, FR_OCC) void chunk_kernel(ScanArgs args) {
     // every helper reads the arguments where they lie (the kernarg segment): the out-of-line
@@ -1729,105 +1404,160 @@ __global__ __launch_bounds__(WG, FR_OCC) void chunk_kernel(ScanArgs args) {
     __shared__ ScanShared sh;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: LDS addresses by wave stay scalar
-    for (int i = tid; i < NS; i += WG) {
-        sh.ls[i] = LSlot{0, 0, 0xFFFFFFFFu};
+    const u32 wid = wave_id();  // wave-uniform: LDS addresses by wave stay scalar
+    for (int i = tid; i < NS; i += WG) sh.ls[i] = LSlot{0, 0, 0xFFFFFFFFu};
+    if (lane == 0) {
+        sh.bsp[wid][SEGS] = 0;
+        sh.bcol[wid][SEGS] = 0;
+        sh.beol[wid][SEGS] = 0;
+        sh.rq_tail[wid] = 0;
     }
     if (tid == 0) {
-        sh.bsp[WG] = 0;
-        sh.bcol[WG] = 0;
-        sh.beol[WG] = 0;
         sh.nkeys = 0;
         sh.created = 0;
         sh.flags = 0;
-        sh.buffered = 1;
         sh.spec = 0;
         sh.spec_bad = 0;
         sh.ncold = 0;
         sh.nexo = 0;
         sh.err_off = 0xFFFFFFFFu;
-        sh.rq_tail = 0;
     }
     const u64 base_lines = a.st->lines[a.par];
-#if FR_TIMING
-    u64 tguess = 0, tcommit = 0;
-    const u64 k0 = __builtin_amdgcn_s_memtime();
+    // the geometry: heavy when the previous launch said so (ramped launches that have a heavy set)
+    const bool hv = a.num_chunks_h != 0 &&
+                    __builtin_amdgcn_readfirstlane(__hip_atomic_load(&a.st->heavy[a.par], __ATOMIC_RELAXED,
+                                                                     __HIP_MEMORY_SCOPE_AGENT)) != 0;
+    const Geom g = hv ? Geom{a.chunk_tiles_h, a.mid_chunks_h, a.num_chunks_h}
+                      : Geom{a.chunk_tiles, a.mid_chunks, a.num_chunks};
+    const bool limited = a.max_records > 0;
+#if defined(FR_STAMPS) && FR_STAMPS == 1
+    const u64 k0_ = __builtin_amdgcn_s_memtime();
 #endif
+    FR_STAMP_DECL
     for (;;) {
-        if (tid == 0) sh.chunk = atomicAdd(&a.st->ticket, 1u);
+        if (tid == 0) {
+            sh.chunk = atomicAdd(&a.st->ticket, 1u);
+            sh.spec = 1u;  // pass 0 runs on guessed phases: side effects are buffered
+        }
         __syncthreads();
         const u32 c = sh.chunk;
-        if (c >= a.num_chunks) break;
+        FR_TRACE("w%d ticket %u of %u\n", (int)wid, c, g.num_chunks);
+        if (c >= g.num_chunks) break;
         u32 tb, te;
-        chunk_bounds(a, c, tb, te);
-        // ---- the line phase at the chunk start: exact for chunk 0, else guessed ----------
-        const bool empty = tb >= te;  // defensive: no tile to stage (publishes 0 lines)
-        int P = -1;
-        if (c == 0) {
-            P = (int)(base_lines & 3ull);
-        } else if (a.max_records <= 0 && !empty && !a.exo_only) {
-#if FR_TIMING
-            const u64 g0 = __builtin_amdgcn_s_memtime();
-#endif
-            P = guess_phase(sh, a, tb, tid, lane, wid);
-#if FR_TIMING
-            tguess += __builtin_amdgcn_s_memtime() - g0;
-#endif
+        chunk_bounds(a, g, c, tb, te);
+        const u32 per = (te - tb + NW - 1) / NW;  // this wave's part of the chunk: [wb, we)
+        const u32 wb = min(tb + wid * per, te), we = min(wb + per, te);
+        // ---- pass 0: chunk 0's first wave starts at the range's exact line count; every other
+        // wave guesses its phase (count only when unsure, and with -s or an exotic-only replay) --
+        u64 L0 = 0;
+        bool parse = false;
+        FR_STAMP(3);
+        if (wb < we) {
+            if (c == 0 && wid == 0) {
+                L0 = base_lines;
+                parse = true;
+            } else if (!limited && !a.exo_only) {
+                const int P = guess_phase(sh, a, wb, lane, wid);
+                parse = P >= 0;
+                L0 = (u64)max(P, 0);
+            }
         }
-        // pass 0: exact (chunk 0) / speculative (guessed phase) / count-only (unsure, -s);
-        // pass 1 (only when pass 0 cannot be kept): exact, after the chunk-level look-back
-        const bool spec = c != 0 && P >= 0;
-        u64 L0 = c == 0 ? base_lines : (u64)(P >= 0 ? P : 0);
-        bool parse = c == 0 || spec;
-        bool exact = c == 0;
-        if (tid == 0) sh.spec = spec ? 1u : 0u;
-        __syncthreads();
+        FR_STAMP(0);
+#if defined(FR_STAMPS) && FR_STAMPS == 1
+        st_[7] += 1;
+#endif
+        // One walk site, several passes.  Pass 0 as above.  Then each wave's start follows from the
+        // chunk start and the earlier waves' pass-0 counts: a wave that parsed on another phase (or a
+        // buffer that overflowed) makes every wave redo; a wave that only counted walks again.  The
+        // chunk start is exact (chunk 0, or a decoupled look-back) or, for a device feed, the first
+        // wave's guess, committed at once (verify_launch checks it); a speculation buffer that
+        // overflows on a guessed start sends the chunk to the look-back and an exact redo.
+        bool run = wb < we, exact = true, force = false;
+        u64 base = base_lines;
         for (int pass = 0;; ++pass) {
-            const u64 cnt = empty ? 0ull : walk_chunk(sh, a, tb, te, L0, parse, exact, tid, lane, wid);
-            if (pass == 1) break;
-            // ---- publish the chunk's line count; a speculative chunk commits at once (checked
-            // by verify_launch), any other resolves its exact prefix first --------------------
-            const bool fast = spec && a.spec_commit && !uniform_flag(sh.spec_bad);
-            if (tid == 0) {
-                sh.spec = 0;
-                agent_store(&a.tiles[c], ((u64)(2u * a.epoch + (c == 0 ? 1u : 0u)) << 32) | (u32)cnt);
-                const u32 f = fast ? (1u | ((u32)P << 1)) : 0u;
-                agent_store(&a.chunk_info[c], ((u64)f << 32) | (u32)cnt);
-                const u32 prev = __hip_atomic_fetch_add(&a.st->chunks_done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-                sh.last = prev == a.num_chunks - 1u;
+            FR_TRACE("w%d pass %d run %d [%u,%u) parse %d\n", (int)wid, pass, (int)run, wb, we, (int)parse);
+            const u64 n = run ? walk_wave(sh, a, wb, we, L0, parse, lane, wid) : 0ull;
+            FR_TRACE("w%d walked %llu\n", (int)wid, (unsigned long long)n);
+            FR_STAMP(pass == 0 ? 1 : 4);
+            if (pass == 0) {
+                if (lane == 0) {
+                    sh.wcount[wid] = n;
+                    sh.wphase[wid] = run && parse ? (int)(L0 & 3ull) : -1;
+                }
+                __syncthreads();
+                FR_STAMP(2);
+                u64 total = 0;
+#pragma unroll
+                for (int w = 0; w < NW; ++w) total += sh.wcount[w];
+                const int p0 = sh.wphase[0];
+                const bool fast = a.spec_commit && c != 0 && p0 >= 0 && !uniform_flag(sh.spec_bad);
+                if (tid == 0) {  // publish the chunk's line count
+                    agent_store(&a.tiles[c], ((u64)(2u * a.epoch + (c == 0 ? 1u : 0u)) << 32) | (u32)total);
+                    const u32 f = fast ? (1u | ((u32)p0 << 1)) : 0u;
+                    agent_store(&a.chunk_info[c], ((u64)f << 32) | (u32)total);
+                    // the sc1 (agent) stores drain before the count that signals them; verify_launch reads
+                    // chunk_info with sc1 loads only (MI355X_MICROARCH.md, valid hand-off forms): no
+                    // release fence, which would write back the XCD's L2 once per chunk
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    const u32 prev = __hip_atomic_fetch_add(&a.st->chunks_done, 1u, __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_AGENT);
+                    sh.last = prev == g.num_chunks - 1u;
+                }
+                exact = !fast;
+                if (fast) {
+                    base = (u64)p0;
+                } else if (c != 0) {
+                    if (wid == 0) {
+                        const u64 ex = lookback(a, c, (u32)total, lane);
+                        if (lane == 0) sh.tile_excl = ex;
+                    }
+                    __syncthreads();
+                    base = base_lines + sh.tile_excl;
+                }
+            } else {
+                __syncthreads();
+                if (exact || !uniform_flag(sh.spec_bad)) break;
+                // a speculation buffer overflowed on the guessed chunk start: look back, redo exactly
+                u64 total = 0;
+#pragma unroll
+                for (int w = 0; w < NW; ++w) total += sh.wcount[w];
+                if (wid == 0) {
+                    const u64 ex = lookback(a, c, (u32)total, lane);
+                    if (lane == 0) sh.tile_excl = ex;
+                }
+                __syncthreads();
+                base = base_lines + sh.tile_excl;
+                exact = true;
+                force = true;
             }
-            if (fast) break;
-            if (wid == 0) {
-                const u64 ex = lookback(a, c, (u32)cnt, lane);
-                if (lane == 0) sh.tile_excl = ex;
+            // plan the next pass from the pass-0 counts and phases (LDS: nothing held across the walk)
+            u64 D = base;
+            bool bad = force || uniform_flag(sh.spec_bad);
+#pragma unroll
+            for (int w = 0; w < NW; ++w) {
+                const int pw = sh.wphase[w];
+                if (w == (int)wid) L0 = D;
+                if (pw >= 0 && (u64)pw != (D & 3ull)) bad = true;
+                D += sh.wcount[w];
             }
-            __syncthreads();
-            const u64 exact_L = base_lines + sh.tile_excl;
-            const bool keep = c == 0 || empty || (spec && (u32)P == (u32)(exact_L & 3ull) && !uniform_flag(sh.spec_bad));
-            if (keep) break;
-            discard_buffers(sh, tid);
-            L0 = exact_L;
+            run = wb < we && (bad || sh.wphase[wid] < 0);
             parse = true;
-            exact = true;
+            if (bad) discard_buffers(sh, tid);
+            if (tid == 0) sh.spec = exact ? 0u : 1u;
+            __syncthreads();
         }
-#if FR_TIMING
-        const u64 c0 = __builtin_amdgcn_s_memtime();
-#endif
-        commit_buffers(sh, a, true, tid, te - tb);  // starts and ends with a barrier: sh.last is visible
-#if FR_TIMING
-        tcommit += __builtin_amdgcn_s_memtime() - c0;
-#endif
-        if (sh.last) {
+        FR_TRACE("w%d commit\n", (int)wid);
+        FR_STAMP(3);
+        commit_buffers(sh, a, tid, g, hv);  // starts and ends with a barrier: sh.last is visible
+        FR_TRACE("w%d committed last %u\n", (int)wid, sh.last);
+        if (sh.last) {  // once per launch: the acquire is cheap here (chunk_info is read with sc1 loads anyway)
             __atomic_thread_fence(__ATOMIC_ACQUIRE);
-            verify_launch(sh, a, base_lines, tid);
+            verify_launch(sh, a, g.num_chunks, base_lines, tid);
         }
+        FR_STAMP(5);
     }
-#if FR_TIMING
-    if ((tid & 63) == 0) {  // diagnostic build only: guess / commit / whole-kernel wave cycles
-        atomicAdd((unsigned long long*)&a.st->stamp[6], (unsigned long long)tguess);
-        atomicAdd((unsigned long long*)&a.st->stamp[7], (unsigned long long)tcommit);
-        atomicAdd((unsigned long long*)&a.st->stamp[5], (unsigned long long)(__builtin_amdgcn_s_memtime() - k0));
-    }
+#if defined(FR_STAMPS) && FR_STAMPS == 1
+    FR_STAMP_FLUSH(k0_);
 #endif
     __syncthreads();
     if (tid == 0) {

@@ -27,19 +27,21 @@ RESULTS_HEADER = ["idx1", "idx2", "reads", "matched_idx1", "matched_idx2", "read
 SCAN_HEADER = ["idx1", "idx2", "matched_idx1", "matched_idx2", "read_type", "sample_name", "reads"]
 
 
-def parse_results_file(result_file) -> dict:
+def parse_results_file(result_file, strict: bool = False) -> dict:
     """frender.py:645-664: code -> (read_type, sample_id).
 
     The reference asserts the README's column order, which its own `scan` does not write, so its
-    demux rejects its own scan CSV.  Deliberate deviation: a
-    header in `scan`'s order is accepted too, its columns taken by name; any other header fails
-    with the reference's AssertionError, and README-order files behave exactly as in the
-    reference."""
+    demux rejects its own scan CSV.  Documented deviation, on by default so that
+    scan -> demux chains (BASELINE config 5) work: a header in `scan`'s order is
+    accepted too, its columns taken by name.  strict=True (`demux --strict-header`) is the
+    reference's behaviour exactly: that header raises its AssertionError (golden case
+    syn_scan_order_strict).  Any other header fails with the reference's AssertionError, and
+    README-order files behave exactly as in the reference, in both modes."""
     with open(result_file, newline="") as f:
         rd = csv.reader(f)
         header = next(rd)
         top = header[0:7]
-        if top == SCAN_HEADER:
+        if top == SCAN_HEADER and not strict:
             ti, si = top.index("read_type"), top.index("sample_name")
         else:
             assert top == RESULTS_HEADER, f"${result_file} does not appear to be a valid frender result file!"
@@ -297,7 +299,7 @@ def frender_demux(args, dev=None) -> None:
     result_file = Path(args.r)
     if not Path.is_file(result_file):
         raise SystemExit(f"File {result_file} not found")
-    results = parse_results_file(result_file)
+    results = parse_results_file(result_file, strict=getattr(args, "strict_header", False))
     ids = sorted({sid for _, sid in results.values()} - {""})
     if (not ids) & samples:
         print("Warning: no demuxable sample ids found in the supplied frender result file!")

@@ -56,7 +56,7 @@ def default_context() -> _lib.Context:
 class UniqueTable:
     """The merged tally: codes in (file, first occurrence) order (R4/R5)."""
 
-    def __init__(self, codes, counts, first, fast_idx, exo_idx, pres_u, pres_f, files, records):
+    def __init__(self, codes, counts, first, fast_idx, exo_idx, pres_u, pres_f, files, records, key_of=None):
         self.codes = codes            # list[str], merged order
         self.counts = counts          # uint64
         self.first = first            # uint64 ordinals (file_index+1) << 44 | byte offset
@@ -66,6 +66,9 @@ class UniqueTable:
         self.pres_f = pres_f
         self.files = files            # basenames in input order
         self.records = records        # records per file
+        self.key_of = key_of          # merged -> packed key (fast / wide codes), 0 for exotic codes
+        self.group = None             # multi-GPU scans: torch.distributed; this table is one key partition
+        self.wire = None              # and the device its exchange tensors live on
 
     def __len__(self):
         return len(self.codes)
@@ -215,14 +218,16 @@ def build_table(t: dict, names, records) -> UniqueTable:
     epc, epf = np.asarray(t["epc"], dtype=np.int64), np.asarray(t["epf"], dtype=np.int64)
     pres_u = np.concatenate([pos[pu], pos[nf + epc]])
     pres_f = np.concatenate([pf, epf])
+    key_of = np.concatenate([np.asarray(keys, dtype=np.uint64), np.zeros(len(exo_codes), np.uint64)])[order]
     return UniqueTable(codes, np.concatenate([counts, exo_counts])[order], all_first[order], fast_idx, exo_idx,
-                       pres_u, pres_f, list(names), list(records))
+                       pres_u, pres_f, list(names), list(records), key_of)
 
 
 def tally_barcodes(cores, files, sample=None, ctx=None) -> UniqueTable:
     """frender.py:183-207 (+ scan_file :154-181) on the GPU: files in order, one context.  With a
-    torch.distributed group of N > 1 ranks (one per GPU) the files are sharded over the GPUs
-    (frender_amd/dist.py: sharded_tally); rank 0 returns the merged table, other ranks None."""
+    torch.distributed group of N > 1 ranks (one per GPU) the record stream is sharded over the GPUs
+    and every rank returns its key partition of the merged table (frender_amd/dist.py:
+    sharded_tally); the functions below take such a partition and run their collectives."""
     from .dist import sharded_tally, world_group
     group = world_group()
     lead = group is None or group.get_rank() == 0  # the lines rank 0 prints for the whole job
@@ -278,14 +283,20 @@ def _length_error(q: str, entries) -> AssertionError:
     return AssertionError("length mismatch")  # pragma: no cover
 
 
+def _lead(table) -> bool:
+    return table.group is None or table.group.get_rank() == 0
+
+
 def process(cores, table: UniqueTable, indexes: dict, num_subs: int, rc_mode: bool, ctx=None) -> Results:
     """frender.py:391-426 on the GPU: classify every unique code (fast keys by packed
-    Hamming, exotic codes by the code-point classifier); raise the reference's first error."""
+    Hamming, exotic codes by the code-point classifier); raise the reference's first error.
+    On a key partition (multi-GPU): each rank classifies its partition; the -rc per-name sums are
+    all-reduced and the first error in first-occurrence order over all partitions is raised."""
     ctx = ctx or default_context()
     idx1, idx2, ids = list(indexes["idx1"]), list(indexes["idx2"]), list(indexes["id"])
     names, name_id = _sheet_names(ids)
     ctx.set_sheet(idx1, idx2, [reverse_complement(x) for x in idx2], name_id, len(names))
-    if cores > 1:
+    if cores > 1 and _lead(table):
         print(f"Multiprocessing with {cores} cores")
     n = len(table)
     res = Results(n, rc_mode)
@@ -328,18 +339,49 @@ def process(cores, table: UniqueTable, indexes: dict, num_subs: int, rc_mode: bo
             for k, j in enumerate(js):
                 if out["err"][k]:
                     errs.append((j, int(out["err"][k])))
+    if table.group is not None:
+        errs = _first_error_everywhere(table, errs)
     if errs:
         j, which = min(errs)
-        code = table.codes[j]
+        code = table.codes[j] if isinstance(j, int) else j[1]
         if which == 3:  # idx1, idx2 = barcode.split("+")[0:2]  (frender.py:306)
             raise ValueError("not enough values to unpack (expected 2, got 1)")
         parts = code.split("+")
         raise _length_error(parts[0], idx1) if which == 1 else _length_error(parts[1], idx2)
     if rc_mode:
-        f, r = ctx.rc_counts()
+        f, r = ctx.rc_counts() if fsel.size else (np.zeros(len(names), np.uint64), np.zeros(len(names), np.uint64))
         res.rc_f = f + f_add
         res.rc_r = r + r_add
+        if table.group is not None:  # the per-name sums of every partition (frender.py:367-373)
+            from .dist import reduce_sum
+            res.rc_f = reduce_sum(table.group, table.wire, res.rc_f.astype(np.int64)).astype(np.uint64)
+            res.rc_r = reduce_sum(table.group, table.wire, res.rc_r.astype(np.int64)).astype(np.uint64)
     return res
+
+
+def _first_error_everywhere(table, errs):
+    """Multi-GPU: the classification error the reference meets first (its Pool over the uniques in
+    first-occurrence order) among every partition's first error.  Rank 0 gets [((first, code), which)]
+    for it; the other ranks raise PeerFailed; no error anywhere -> []."""
+    from .dist import PeerFailed, gather_bytes, reduce_max
+
+    g = table.group
+    mine = b""
+    if errs:
+        j, which = min(errs, key=lambda e: int(table.first[e[0]]))
+        mine = f"{int(table.first[j])}\t{which}\t".encode() + table.codes[j].encode("utf-8", "surrogateescape")
+    any_err = int(reduce_max(g, table.wire, [1 if errs else 0])[0])
+    if not any_err:
+        return []
+    got = gather_bytes(g, table.wire, mine)
+    if g.get_rank() != 0:
+        raise PeerFailed("classification failed (rank 0 reports it)")
+    cands = []
+    for b in got:
+        if b:
+            f, w, c = b.split(b"\t", 2)
+            cands.append(((int(f), c.decode("utf-8", "surrogateescape")), int(w)))
+    return [min(cands)]
 
 
 def call_rc_mode_per_id(results: Results, ids) -> dict:
@@ -389,13 +431,28 @@ def call_barcodes_correctly_distributed(table: UniqueTable, results: Results, pr
     # one raises at the first demuxable barcode in order
     rows = results.row.astype(np.int64)
     demux = np.nonzero(results.cls == DEMUX)[0]
-    pat = {}
-    for j in demux.tolist():
-        nm = results.ids[rows[j]]
-        if nm not in pat:
-            pat[nm] = re.compile(nm.removeprefix(prefix), re.I)
     names = results.names
     name_of = {n: k for k, n in enumerate(names)}
+    order = [results.ids[rows[j]] for j in demux.tolist()]
+    if table.group is not None:  # every partition's demuxable names, by their first demuxable code
+        from .dist import reduce_min
+        big = (1 << 63) - 1
+        firsts = np.full(len(names), big, np.int64)
+        for j in demux.tolist():
+            k = name_of[results.ids[rows[j]]]
+            firsts[k] = min(firsts[k], int(table.first[j]))
+        firsts = reduce_min(table.group, table.wire, firsts)
+        order = [names[k] for k in np.argsort(firsts, kind="stable").tolist() if firsts[k] != big]
+    pat = {}
+    for nm in order:
+        if nm not in pat:
+            try:
+                pat[nm] = re.compile(nm.removeprefix(prefix), re.I)
+            except re.error:
+                if table.group is not None and table.group.get_rank() != 0:
+                    from .dist import PeerFailed
+                    raise PeerFailed("sample pattern failed to compile (rank 0 reports it)") from None
+                raise
     groups = [re.compile("undetermined", re.I), re.compile("undetermined|index-hop", re.I),
               re.compile("undetermined|ambiguous", re.I)] + [pat.get(n) for n in names]
     ok = np.ones((len(groups), len(basenames)), dtype=bool)
@@ -413,25 +470,67 @@ def call_barcodes_correctly_distributed(table: UniqueTable, results: Results, pr
     pair_ok = ok[grp[pu], file_b[pf]] if pu.size else np.zeros(0, bool)
     demux_ok = np.ones(len(table), dtype=bool)
     demux_ok[pu[~pair_ok]] = False
-    bad = {basenames[b] for b in np.unique(file_b[pf[~pair_ok]]).tolist()}
+    bad_b = np.zeros(len(basenames), np.int64)
+    bad_b[np.unique(file_b[pf[~pair_ok]])] = 1
+    if table.group is not None:  # the mismatching files of every partition
+        from .dist import reduce_max
+        bad_b = reduce_max(table.group, table.wire, bad_b)
+    bad = {basenames[b] for b in np.nonzero(bad_b)[0].tolist()}
     return demux_ok, bad
 
 
+def _gather_partitions(table: UniqueTable, results: Results, demux_ok):
+    """Multi-GPU: every partition's classified rows on rank 0, in first-occurrence order (int64 rows
+    over RCCL: first, key, count, m1, m2, class, row, demux_ok; exotic codes are rank 0's already).
+    Returns (codes, counts, m1, m2, cls, row, demux_ok) lists on rank 0, None elsewhere."""
+    from .dist import gather_rows
+
+    import torch
+
+    fast = np.nonzero(table.fast_idx >= 0)[0]
+    dok = np.ones(len(table), bool) if demux_ok is None else np.asarray(demux_ok, bool)
+    cols = [table.first.view(np.int64)[fast], table.key_of.view(np.int64)[fast], table.counts.view(np.int64)[fast],
+            results.m1[fast], results.m2[fast], results.cls[fast], results.row[fast], dok[fast]]
+    rows = torch.from_numpy(np.stack([np.asarray(c, np.int64) for c in cols], 1) if fast.size
+                            else np.zeros((0, 8), np.int64))
+    got = gather_rows(table.group, table.wire, rows)
+    if got is None:
+        return None
+    allr = np.concatenate(got, 0)
+    exo = np.nonzero(table.exo_idx >= 0)[0]
+    first = np.concatenate([allr[:, 0].view(np.uint64), table.first[exo]])
+    codes = _lib.decode_keys(allr[:, 1].view(np.uint64)) + [table.codes[j] for j in exo.tolist()]
+    counts = np.concatenate([allr[:, 2], table.counts[exo].view(np.int64)])
+    rest = [np.concatenate([allr[:, 3 + i], np.asarray(c, np.int64)[exo]])
+            for i, c in enumerate((results.m1, results.m2, results.cls, results.row, dok))]
+    o = np.argsort(first, kind="stable")
+    return ([codes[i] for i in o.tolist()], counts[o].tolist(), *[r[o].tolist() for r in rest[:4]],
+            [bool(x) for x in rest[4][o].tolist()])
+
+
 def report_analysis(table: UniqueTable, results: Results, demux_ok, out_csv_name: str) -> None:
-    """frender.py:482-501: the scan CSV (excel dialect, columns in the code's order)."""
+    """frender.py:482-501: the scan CSV (excel dialect, columns in the code's order).  On a key
+    partition (multi-GPU) rank 0 gathers every partition's rows and writes the file."""
+    if table.group is not None:
+        got = _gather_partitions(table, results, demux_ok)
+        if got is None:
+            return
+        codes, counts, m1, m2, cls, row, dok_all = got
+    else:
+        codes, counts = table.codes, table.counts.tolist()
+        m1, m2, cls, row = results.m1.tolist(), results.m2.tolist(), results.cls.tolist(), results.row.tolist()
+        dok_all = demux_ok.tolist() if demux_ok is not None else None
     print(f"Analysis complete! Writing results to {out_csv_name}")
-    if len(table) == 0:
+    if len(codes) == 0:
         raise IndexError("list index out of range")  # results[0].keys() on an empty scan (:497)
     idx1, idx2, ids = results.idx1, results.idx2, results.ids
-    m1, m2, cls, row = results.m1.tolist(), results.m2.tolist(), results.cls.tolist(), results.row.tolist()
-    counts = table.counts.tolist()
     header = ["idx1", "idx2", "matched_idx1", "matched_idx2", "read_type", "sample_name", "reads"]
-    dok = demux_ok.tolist() if demux_ok is not None else None
+    dok = dok_all if demux_ok is not None else None
     if dok is not None:
         header.append("demux_ok")
 
     def rows():
-        for j, code in enumerate(table.codes):
+        for j, code in enumerate(codes):
             parts = code.split("+")
             r = [parts[0], parts[1], idx1[m1[j]] if m1[j] >= 0 else "", idx2[m2[j]] if m2[j] >= 0 else "",
                  CLASS_NAMES[cls[j]], ids[row[j]] if row[j] >= 0 else "", counts[j]]
@@ -481,27 +580,30 @@ def frender_scan(args, ctx=None) -> dict:
     files = parse_files(spec, just_r1=True)
     ctx = ctx or default_context()
     table = tally_barcodes(cores, files, sample, ctx=ctx)
-    if table is None:  # a rank > 0 of a multi-GPU scan: rank 0 classifies and writes the outputs
-        return None
-    print("Scanning complete! Analyzing barcodes...")
+    lead = _lead(table)  # multi-GPU: every rank holds a key partition; rank 0 prints and writes
+    if lead:
+        print("Scanning complete! Analyzing barcodes...")
     results = process(cores, table, indexes, num_subs, rc_mode, ctx=ctx)
     if rc_mode:
         rc_calls = call_rc_mode_per_id(results, indexes["id"])
-        print("First round of analysis complete.")
-        report_rc_call_info(rc_calls, indexes, out_csv_name)
+        if lead:
+            print("First round of analysis complete.")
+            report_rc_call_info(rc_calls, indexes, out_csv_name)
         indexes["idx2"] = [reverse_complement(indexes["idx2"][i]) if rc_calls[i_d]["call"] else indexes["idx2"][i]
                            for i, i_d in enumerate(indexes["id"])]
-        print("\nRe-analyzing barcodes with corrected index 2 sequences...")
+        if lead:
+            print("\nRe-analyzing barcodes with corrected index 2 sequences...")
         results = process(cores, table, indexes, num_subs, False, ctx=ctx)
     demux_ok, mismatching = call_barcodes_correctly_distributed(table, results, prefix)
-    if mismatching:
-        print("Incorrectly demultiplexed barcodes found! Affected files:")
-        for a in mismatching:
-            print(a)
-    else:
-        print("It appears that all files are already correctly demultiplexed.")
+    if lead:
+        if mismatching:
+            print("Incorrectly demultiplexed barcodes found! Affected files:")
+            for a in mismatching:
+                print(a)
+        else:
+            print("It appears that all files are already correctly demultiplexed.")
     report_analysis(table, results, demux_ok, out_csv_name)
-    return {"table": table, "results": results, "out_csv": out_csv_name}
+    return {"table": table, "results": results, "out_csv": out_csv_name} if lead else None
 
 
 # the name the golden harness calls

@@ -122,6 +122,24 @@ int fr_feed(fr_ctx* ctx, const uint8_t* data, uint64_t len);
 typedef struct fr_gz fr_gz;
 fr_gz* fr_gz_open(const char* const* paths, int n_files, int threads);
 int fr_gz_feed(fr_gz* g, int i, fr_ctx* ctx);
+/* Record shards of one file (multi-GPU scans of fewer files than GPUs; SURVEY §8(e) "host cuts
+ * record-aligned chunks and deals them to GPUs"): part `part` of `nparts` of file i's decoded
+ * stream is [b_part, b_part+1), b_0 = 0, b_nparts = the end, and for 0 < j < nparts b_j = the first
+ * record start (a line start whose index from the file start is 0 mod 4, universal newlines as
+ * frender.py:159 reads them) at or after j * hint / nparts.  The function inflates the file from its
+ * start, counts line ends on the host, calls fr_begin_file_at(ctx, file_index, b_part, 0) once the
+ * part's start is known, feeds only the part's bytes, stops inflating at its end and stores b_part
+ * in *byte_base; the caller then calls fr_end_file.  Every rank that passes the same `hint` cuts the
+ * same way.  Not with -s (a sample is the head of each whole file). */
+int fr_gz_feed_part(fr_gz* g, int i, fr_ctx* ctx, int64_t file_index, int part, int nparts, uint64_t hint,
+                    uint64_t* byte_base);
+/* The cuts fr_gz_feed_part makes: bounds[0..nparts] (b_0 = 0, b_nparts = the decoded size).  Host
+ * only (no GPU context): FR_OK, or FR_ERR_IO when the file is not valid gzip. */
+int fr_gz_part_bounds(const char* path, int nparts, uint64_t hint, uint64_t* bounds);
+/* The decoded size of a .gz file as far as its trailers tell (0 when unreadable): exact for BGZF (the
+ * members' ISIZE fields) and for a single-member file of up to 4 GiB decoded; otherwise the last
+ * member's ISIZE lifted toward 4x the compressed size.  A deterministic fr_gz_feed_part hint. */
+uint64_t fr_gz_size_hint(const char* path);
 const char* fr_gz_error(const fr_gz* g);
 void fr_gz_close(fr_gz* g);
 

@@ -49,12 +49,12 @@ RESULTS_HEADER = ["idx1", "idx2", "reads", "matched_idx1", "matched_idx2", "read
 SCAN_HEADER = ["idx1", "idx2", "matched_idx1", "matched_idx2", "read_type", "sample_name", "reads"]
 
 
-def read_results(path) -> dict:
-    """D7, frender.py:645-664: code -> (read_type, sample_id)."""
+def read_results(path, strict: bool = False) -> dict:
+    """D7, frender.py:645-664: code -> (read_type, sample_id).  strict: the reference exactly."""
     with open(path, newline="") as f:
         rd = csv.reader(f)
         header = next(rd)
-        if header[0:7] == SCAN_HEADER:  # the build's documented deviation: scan's own column order
+        if header[0:7] == SCAN_HEADER and not strict:  # the build's documented deviation: scan's own order
             return {row[0] + "+" + row[1]: (row[4], row[5]) for row in rd}
         if header[0:7] != RESULTS_HEADER:
             raise AssertionError(f"${path} does not appear to be a valid frender result file!")
@@ -115,7 +115,7 @@ def demux(args) -> dict:
     und_name = f"Undetermined{'-ambiguous' if want_amb else ''}{'-index-hop' if want_hop else ''}"
     if not Path(args.r).is_file():
         raise SystemExit(f"File {Path(args.r)} not found")
-    results = read_results(Path(args.r))
+    results = read_results(Path(args.r), strict=getattr(args, "strict_header", False))
     ids = sorted({sid for _, sid in results.values()} - {""})
     if not ids and want_samples:
         print("Warning: no demuxable sample ids found in the supplied frender result file!")

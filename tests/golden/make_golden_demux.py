@@ -154,6 +154,9 @@ def all_cases():
         syn_pair_case("syn_no_samples", 12, 1000, 1, flags={"no_samples": True}),
         syn_pair_case("syn_scan_order_csv", 12, 1000, 1, results_header=SCAN_COLS,
                       flags={"reference_reads_readme_order": True}),
+        # the reference itself on scan's own column order: its AssertionError (strict parity)
+        syn_pair_case("syn_scan_order_strict", 12, 1000, 1, results_header=SCAN_COLS,
+                      flags={"strict_header": True}),
         # BASELINE config 5 shape: 96 samples, scan's own CSV fed to demux (paired, 2 lanes)
         syn_pair_case("syn96_scan_csv", 96, 20000, 2, results_header=SCAN_COLS,
                       flags={"reference_reads_readme_order": True}),
@@ -178,6 +181,7 @@ def run_reference(ref, d, flags):
                               o=flags.get("o"), no_index_hop=flags.get("no_index_hop", False),
                               no_ambiguous=flags.get("no_ambiguous", False),
                               no_undeter=flags.get("no_undeter", False), no_samples=flags.get("no_samples", False),
+                              strict_header=flags.get("strict_header", False),
                               files=[os.path.join(d, "inputs", f) for f in sorted(os.listdir(os.path.join(d, "inputs")))
                                      if f.endswith(".gz")])
     ref.args = args  # open_files() reads the module-global args (frender.py:671)

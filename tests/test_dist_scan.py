@@ -1,15 +1,17 @@
-"""The multi-GPU product path's host logic (frender_amd/dist.py: sharded_tally, merge_tables)
-over gloo on CPU: N ranks, each with a CPU stand-in context (tests/fake_ctx.py), must give rank 0
-exactly the single-rank table (codes, counts, firsts, presence, per-file records) and the same
-per-file stdout lines, on multi-file inputs with fast, wide and exotic codes, -s, duplicate
-files and a data error."""
+"""The multi-GPU scan's host logic (frender_amd/dist.py + the key-partition paths of
+frender_amd/scan.py) over gloo on CPU: N ranks, each with a CPU stand-in context
+(tests/fake_ctx.py), must write exactly the single-rank outputs (scan CSV, -rc CSV, stdout) on
+multi-file inputs with fast, wide and exotic codes, -s, duplicate files and data errors, and on a
+SINGLE file, whose records every rank tallies a part of (record-aligned cuts by the library's own
+host cutter, fr_gz_part_bounds)."""
+import argparse
 import contextlib
+import gzip
 import io
 import os
 import random
 import socket
 
-import numpy as np
 import pytest
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -17,23 +19,26 @@ import torch.multiprocessing as mp
 from frender_amd import synth
 
 
-def _inputs(d, seed):
+def _inputs(d, seed, n_files=5, dup=True):
     rng = random.Random(seed)
     sheet = synth.make_sheet(24, 8, 8)
+    sheet.write_csv(os.path.join(d, "sheet.csv"))
     files = []
-    for i in range(5):
+    for i in range(n_files):
         text = synth.generate_bytes(sheet, i * 3000, rng.randint(500, 3000), R=8, seed=seed).decode()
         extra = "".join(f"@x{j} 1:N:0:{c}\nAC\n+\nFF\n" for j, c in enumerate(
-            rng.choice(["AAAACCCCGGGG+TTTTAAAACCCC", "acgtacgt+ttttcccc", "AcGt+TTTT", "ÄCGT+ACGT", "A+C+G"])
+            rng.choice(["acgtacgt+ttttcccc", "AcGtAcGt+TTTTCCCC", "ÄCGTACGT+ACGTACGT", "ACGTACGT+ACGTACGT+GG",
+                        "ACGTNCGT+ACGTACGN"])
             for _ in range(rng.randint(0, 40))))
         p = os.path.join(d, f"f{i}_R1.fq.gz")
         synth.write_fastq_gz(p, (text + extra).encode(), level=1)
         files.append(p)
-    files.append(files[1])  # the same file twice (two file indices)
+    if dup:
+        files.append(files[1])  # the same file twice (two file indices)
     return files
 
 
-def _run(world, rank, files, sample, port, q):
+def _run(world, rank, files, sheet, flags, out_dir, port, q):
     from fake_ctx import FakeContext
 
     from frender_amd import scan
@@ -41,24 +46,27 @@ def _run(world, rank, files, sample, port, q):
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(port)
         dist.init_process_group("gloo", rank=rank, world_size=world)
+    os.makedirs(out_dir, exist_ok=True)
+    cwd = os.getcwd()
+    os.chdir(out_dir)
     buf = io.StringIO()
     err = None
-    t = None
+    args = argparse.Namespace(n=flags.get("n", 1), rc=flags.get("rc", False), c=2.0, s=flags.get("s"), o="t",
+                              p=None, b=sheet, files=list(files))
     with contextlib.redirect_stdout(buf):
         try:
-            t = scan.tally_barcodes(2, files, sample, ctx=FakeContext())
+            scan.frender_scan(args, ctx=FakeContext())
         except Exception as e:  # noqa: BLE001
             err = (type(e).__name__, str(e))
-    out = None
-    if t is not None:
-        pres = sorted(zip(t.pres_u.tolist(), t.pres_f.tolist()))
-        out = (t.codes, t.counts.tolist(), t.first.tolist(), pres, t.records, t.files)
+    os.chdir(cwd)
+    outs = {f.split("_t_")[0]: open(os.path.join(out_dir, f), "rb").read() for f in sorted(os.listdir(out_dir))}
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    res = (outs, err, buf.getvalue())
     if q is not None:
-        q.put((rank, out, err, buf.getvalue()))
-    return out, err, buf.getvalue()
+        q.put((rank, res))
+    return res
 
 
 def _free_port():
@@ -67,39 +75,97 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _multi(world, files, sample):
+def _multi(world, files, sheet, flags, tmp):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_run, args=(world, r, files, sample, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_run, args=(world, r, files, sheet, flags, os.path.join(tmp, f"rank{r}"), port, q))
+             for r in range(world)]
     for p in procs:
         p.start()
-    got = dict((r, (o, e, s)) for r, o, e, s in (q.get(timeout=180) for _ in range(world)))
+    got = dict(q.get(timeout=240) for _ in range(world))
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
     for r in range(1, world):
-        assert got[r][0] is None and got[r][2] == ""  # only rank 0 returns a table / prints
+        outs, err, out = got[r]
+        assert outs == {} and out == ""  # only rank 0 prints and writes
+        assert err is None or err[0] == "PeerFailed"
     return got[0]
 
 
-@pytest.mark.parametrize("world,sample", [(2, None), (3, 700)])
-def test_sharded_tally_equals_single(tmp_path, world, sample):
+def _norm(out: str) -> str:
+    """The affected-files lines come from a set (frender.py:636-638): their order follows string
+    hashing, which differs per process (PYTHONHASHSEED), in the reference too.  Sort that block."""
+    lines = out.split("\n")
+    if "Incorrectly demultiplexed barcodes found! Affected files:" in lines:
+        i = lines.index("Incorrectly demultiplexed barcodes found! Affected files:") + 1
+        j = next(k for k in range(i, len(lines)) if lines[k].startswith("Analysis complete!"))
+        lines[i:j] = sorted(lines[i:j])
+    return "\n".join(lines)
+
+
+def _check(tmp_path, world, files, flags):
+    sheet = os.path.join(str(tmp_path), "sheet.csv")
+    one = _run(1, 0, files, sheet, flags, os.path.join(str(tmp_path), "one"), None, None)
+    many = _multi(world, files, sheet, flags, str(tmp_path))
+    assert many[1] == one[1]
+    assert _norm(many[2]) == _norm(one[2])  # the same stdout lines, in order
+    assert many[0] == one[0]  # byte-identical CSVs
+    return one
+
+
+@pytest.mark.parametrize("world,flags", [(2, {}), (3, {"s": 700}), (2, {"rc": True, "n": 1}), (4, {"n": 2})])
+def test_sharded_scan_equals_single(tmp_path, world, flags):
     files = _inputs(str(tmp_path), seed=world)
-    one = _run(1, 0, files, sample, None, None)
-    assert one[1] is None and one[0] is not None
-    many = _multi(world, files, sample)
-    assert many[1] is None
-    assert many[0] == one[0]
-    assert many[2] == one[2]  # the same stdout lines, in file order
+    one = _check(tmp_path, world, files, flags)
+    assert one[1] is None and one[0]
 
 
-def test_sharded_tally_error_in_file_order(tmp_path):
+@pytest.mark.parametrize("world", [2, 3])
+def test_single_file_record_shards(tmp_path, world):
+    """Fewer files than ranks: every rank tallies a record-aligned part of the one file (CRLF lines
+    too), and the merged outputs are the single-rank ones."""
+    files = _inputs(str(tmp_path), seed=11, n_files=1, dup=False)
+    with gzip.open(files[0], "rb") as g:
+        text = g.read()
+    crlf = os.path.join(str(tmp_path), "crlf_R1.fq.gz")
+    with gzip.open(crlf, "wb") as g:
+        g.write(text.replace(b"\n", b"\r\n"))
+    for fs in ([files[0]], [crlf]):
+        one = _check(tmp_path, world, fs, {"rc": True})
+        assert one[1] is None
+
+
+def test_sharded_scan_error_in_file_order(tmp_path):
     files = _inputs(str(tmp_path), seed=7)
     with open(files[3], "wb") as f:  # a header without ' ' in file 3: IndexError there
-        import gzip
         f.write(gzip.compress(b"@x 1:N:0:AAAA+CCCC\nA\n+\nF\n@nospace\nA\n+\nF\n"))
-    one = _run(1, 0, files, None, None, None)
-    many = _multi(2, files, None)
+    one = _check(tmp_path, 2, files, {})
     assert one[1] == ("IndexError", "list index out of range")
-    assert many[1] == one[1] and many[2] == one[2]
+
+
+def test_part_bounds_are_record_starts(tmp_path):
+    """fr_gz_part_bounds (host only): cuts at record starts at or after j * hint / k, the same for
+    any hint source; LF, CRLF and lone-CR files."""
+    import re
+
+    from frender_amd import _lib
+    rng = random.Random(3)
+    recs = [f"@r{i} 1:N:0:ACGT+TTTT\n{'A' * rng.randint(1, 90)}\n+\n" for i in range(4000)]
+    recs = [r + "F" * (len(r.split("\n")[1])) + "\n" for r in recs]
+    for nl in ("\n", "\r\n", "\r"):
+        data = "".join(recs).replace("\n", nl).encode()
+        p = os.path.join(str(tmp_path), f"t{len(nl)}{nl == chr(13)}.fq.gz")
+        with gzip.open(p, "wb") as g:
+            g.write(data)
+        hint = _lib.GzPool.size_hint(p)
+        assert hint == len(data)  # single member, < 4 GiB: exact
+        ends = [m.end() for m in re.finditer(rb"\r\n|\r|\n", data)]
+        starts = [0] + ends[3::4]  # line starts with index 0 mod 4
+        for k in (1, 2, 3, 7):
+            b = _lib.GzPool.part_bounds(p, k, hint)
+            assert b[0] == 0 and b[-1] == len(data) and b == sorted(b)
+            for j in range(1, k):
+                t = hint * j // k
+                assert b[j] == min([s for s in starts if s >= t] + [len(data)])

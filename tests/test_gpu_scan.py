@@ -167,11 +167,11 @@ def test_speculative_commit_replay(lib, monkeypatch, log_min):
         c.close()
 
 
-@pytest.mark.parametrize("log_min", ["0", "150", "100000000"])
+@pytest.mark.parametrize("log_min", ["0", "60", "100000000"])
 def test_launch_log_commits(lib, monkeypatch, log_min):
     """Commits of at least FR_LOG_MIN pairs go to the launch log and are aggregated after the launch
     (count / scatter / LDS reduce / round-based table inserts); smaller ones insert directly.  Every
-    commit logged (0), a mix (150: these 1-tile chunks commit ~100-250 pairs), and none must give the
+    commit logged (0), a mix (60: these 2-wave-tile chunks commit ~30-110 pairs), and none must give the
     oracle's tally, including a table that has to grow between launches."""
     from frender_amd import synth
     monkeypatch.setenv("FR_LOG_MIN", log_min)
@@ -189,16 +189,17 @@ def test_launch_log_commits(lib, monkeypatch, log_min):
             c.close()
 
 
-@pytest.mark.skipif(os.environ.get("FR_RUN_PENDING") != "1",
-                    reason="written when no GPU box was available; run on hardware (FR_RUN_PENDING=1), then unskip")
 def test_heavy_chunk_switch(lib, monkeypatch):
-    """A context whose commits all go to the launch log switches its ramped launches to the heavy
-    chunk size after the first landed snapshot (fr_api.hip note_snapshot).  A 6-workgroup grid makes
-    1 MiB launches ramped; the tally over both chunk sizes must equal the oracle's."""
+    """Ramped launches switch to the heavy chunk size once at least a quarter of the chunks since the
+    reset logged their commits; the device decides at the end of each launch for the next one
+    (fr_kernels.hip note_commit) and fr_reset clears it.  A 6-workgroup grid makes 1 MiB launches
+    ramped.  Checked: a config-3-shape pass switches in the middle (its first launch walks 5-tile chunks,
+    later ones 7), a reused context's next pass over single-code data (commits never log) walks 5-tile
+    chunks again, and a third pass switches again; every tally equals the oracle's."""
     from frender_amd import synth
     from oracle.frender_oracle import tally_text
     monkeypatch.setenv("FR_GRID", "6")
-    monkeypatch.setenv("FR_LOG_MIN", "0")
+    monkeypatch.setenv("FR_LOG_MIN", "100")
     monkeypatch.setenv("FR_CHUNK_TILES", "5")
     monkeypatch.setenv("FR_CHUNK_TILES_HEAVY", "7")
     c = lib.Context(device=0, chunk_bytes=1 << 20, table_slots=1 << 16)
@@ -206,21 +207,29 @@ def test_heavy_chunk_switch(lib, monkeypatch):
         assert c.diag()["chunk_tiles"] == 5
         sheet = synth.make_sheet(384, 10, 10)
         n = 300_000
-        host = synth.generate_bytes(sheet, 0, n, R=8, seed=4)
-        p = c.device_alloc(len(host))
+        heavy_data = synth.generate_bytes(sheet, 0, n, R=8, seed=4)
+        p = c.device_alloc(len(heavy_data))
         c.synth_device(p, 0, n, 8, 4, sheet.idx1, sheet.idx2)
-        for _ in range(2):  # the second pass starts heavy
+        light = b"".join(b"@r%d 1:N:0:AAAA+CCCC\nACGT\n+\nFFFF\n" % i for i in range(400_000))
+        q = c.device_alloc(len(light))
+        c.copy_to_device(q, light)
+        for data, ptr, heavy in ((heavy_data, p, True), (light, q, False), (heavy_data, p, True)):
             c.reset()
             c.begin_file(None)
-            c.feed_device(p, len(host))
+            c.feed_device(ptr, len(data))
             st = c.end_file()
-            assert st.records == n and st.error == 0
             c.finalize()
             keys, counts, first = c.unique()
-            exp, _ = tally_text(host.decode())
+            exp, _ = tally_text(data.decode())
+            assert st.error == 0 and st.records == sum(exp.values())
             assert list(zip(lib.decode_keys(keys), counts.tolist())) == list(exp.items())
+            d, launches = c.diag(), c.timing().scan_launches
+            if heavy:  # switched after the first launch, within this pass
+                assert d["chunk_tiles"] == 7 and 0 < d["heavy_launches"] < launches, (d, launches)
+            else:
+                assert d["chunk_tiles"] == 5 and d["heavy_launches"] == 0, (d, launches)
         c.device_free(p)
-        assert c.diag()["chunk_tiles"] == 7
+        c.device_free(q)
     finally:
         c.close()
 

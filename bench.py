@@ -54,8 +54,9 @@ def parse():
                          "partition) or a binary tree into rank 0")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, one GPU per rank); gloo only to rehearse N ranks on one GPU")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02f.json"),
-                    help="per-launch HBM bytes of the tally kernel from rocprofv3 PMC (null if absent)")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r03.json"),
+                    help="per-launch HBM bytes of the tally kernel from rocprofv3 PMC (scripts/make_traffic.py); "
+                         "used only when taken on this source tree and this launch shape, else traffic is null")
     return ap.parse_args()
 
 
@@ -86,6 +87,25 @@ def table_checksum(ctx, U):
     h = rows[0] * -7046029254386353131 + rows[1] * 0x2545F4914F6CDD1D + rows[2] * -4658895280553007687
     h = h ^ (h >> 29)
     return int(h.sum().item())
+
+
+def load_traffic(path, tree, per_launch_bytes, samples, index_len, combinatorial):
+    """(HBM bytes per launch, note) from a PMC traffic file (scripts/make_traffic.py), or (None, why):
+    a file measured on another source tree (frender_amd._lib.source_tree_hash) or launch shape is
+    refused, never reported."""
+    try:
+        with open(path) as f:
+            tj = json.load(f)
+    except (OSError, ValueError):
+        return None, "no PMC traffic file"
+    name = os.path.basename(path)
+    if tj.get("tree_hash") != tree:
+        return None, f"refused {name}: measured on tree {tj.get('tree_hash')}, this tree is {tree}"
+    if not (tj.get("algorithmic_bytes_per_launch") == per_launch_bytes and tj.get("samples") == samples
+            and tj.get("index_len") == index_len and bool(tj.get("combinatorial")) == combinatorial):
+        return None, f"refused {name}: measured on another launch shape"
+    return tj.get("hbm_bytes_per_launch"), (f"{name} (tree {tree}): FETCH_SIZE x2 + WRITE_SIZE per launch, "
+                                            f"{tj.get('traffic_over_algorithmic')}x algorithmic")
 
 
 def _gz(chunk: bytes) -> bytes:
@@ -252,16 +272,8 @@ def main():
     per_launch_bytes = t_after.scan_bytes / max(launches, 1)
     per_launch_ms = scan_ms / max(launches, 1)
     achieved = per_launch_bytes / (per_launch_ms / 1e3) / 1e9 if per_launch_ms > 0 else 0.0
-    traffic = None
-    try:
-        with open(args.traffic_json) as f:
-            tj = json.load(f)
-        # PMC traffic of this exact launch shape only (bytes per launch, samples, index length)
-        if (tj.get("algorithmic_bytes_per_launch") == per_launch_bytes and tj.get("samples", 96) == args.samples
-                and tj.get("index_len", 8) == args.index_len and bool(tj.get("combinatorial", False)) == args.combinatorial):
-            traffic = tj.get("hbm_bytes_per_launch")
-    except Exception:
-        traffic = None
+    traffic, traffic_note = load_traffic(args.traffic_json, _lib.source_tree_hash(), per_launch_bytes,
+                                         args.samples, args.index_len, args.combinatorial)
 
     csum = table_checksum(ctx, U) if (world == 1 or args.merge == "a2a" or rank == 0) else 0
     if world > 1 and args.merge == "a2a":  # report the merged table's size (sum of the partitions)
@@ -293,7 +305,7 @@ def main():
                        "parallelism": f"dp{world} (record shards) + {'RCCL' if args.dist_backend == 'nccl' else 'gloo'} "
                                       + ("all-to-all hash-partitioned merge" if args.merge == "a2a" else "tree merge") if world > 1 else "1 GPU"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_note,
                          "kernel": "fr::chunk_kernel", "bytes_per_launch": int(per_launch_bytes),
                          "avg_launch_ms": round(per_launch_ms, 4), "launches_per_step": int(launches),
                          "log_aggregation_ms_per_launch": round(t_after.log_ms / max(launches, 1), 4)},

@@ -23,6 +23,23 @@ except Exception:  # pragma: no cover - torch is plumbing only
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FRENDER_HIP_LIB", os.path.join(HERE, "libfrender_hip.so"))
 
+
+def source_tree_hash() -> str:
+    """sha256 (16 hex digits) of the sources libfrender_hip.so is built from (csrc/ + the C header):
+    measurements kept under profiles/ (the PMC traffic file) name the tree they were taken on, and
+    bench.py refuses one taken on another tree."""
+    import hashlib
+
+    h = hashlib.sha256()
+    csrc = os.path.join(HERE, "csrc")
+    files = sorted(os.path.join(csrc, f) for f in os.listdir(csrc) if f.endswith((".hip", ".cpp", ".h")))
+    files.append(os.path.join(os.path.dirname(HERE), "include", "frender_amd.h"))
+    for p in files:
+        h.update(os.path.basename(p).encode() + b"\0")
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
 FR_OK = 0
 FR_SAMPLE_DONE = 5
 FR_ERR_IO = 6

@@ -15,5 +15,9 @@ if [[ ${PMC:-1} == 1 ]]; then
   timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$R/gpurun_out/prof_write" -o run \
       -- python3 "$R/bench.py" $ARGS > "$R/gpurun_out/prof_write.log" 2>&1 || { echo "pmc write failed"; exit 1; }
 fi
+if [[ ${STREAM:-0} == 1 ]]; then  # calibration: FETCH_SIZE of the stream-only ablation (no parse, no table)
+  FR_ABLATE=1 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$R/gpurun_out/prof_fetch_stream" -o run \
+      -- python3 "$R/bench.py" $ARGS > "$R/gpurun_out/prof_fetch_stream.log" 2>&1 || { echo "pmc stream fetch failed"; exit 1; }
+fi
 cd "$R"
 find gpurun_out/prof_trace -name "*kernel_stats.csv" | head -1 | xargs cat | head -20

@@ -4,10 +4,15 @@ Reads gpurun_out/prof_trace (kernel-trace --stats) and gpurun_out/prof_fetch / p
 (--pmc FETCH_SIZE / --pmc WRITE_SIZE, separate runs), writes
   profiles/<tag>_kernel_stats.csv       the --stats summary
   profiles/<tag>_pmc_<kernel>.csv       per-dispatch FETCH_SIZE / WRITE_SIZE rows of the kernel
-  profiles/traffic_r02.json             HBM bytes per launch, corrected per MI355X_MICROARCH.md:
+  profiles/$TRAFFIC_JSON                HBM bytes per launch, corrected per MI355X_MICROARCH.md:
                                         FETCH_SIZE counts 1/2 of 16-B/lane streaming reads on
-                                        gfx950 (x2), both counters in KiB.
+                                        gfx950 (x2), both counters in KiB; stamped with the
+                                        library's source tree hash (bench.py refuses another tree's)
+                                        and, when gpurun_out/prof_fetch_stream exists (a FETCH pass of
+                                        the stream-only ablation FR_ABLATE=1), the calibration of the
+                                        x2 rule on this kernel's own 16-B/lane tile loads.
 usage: python scripts/make_traffic.py <tag> [reads] [read_len] [launches_per_step]
+env:   SAMPLES / INDEX_LEN / COMBINATORIAL (the bench shape), RECLEN, PROF_DIR, TRAFFIC_JSON
 """
 import csv
 import glob
@@ -53,11 +58,23 @@ def main():
         w.writeheader()
         for r in frows + wrows:
             w.writerow(r)
+    sys.path.insert(0, ROOT)
+    from frender_amd._lib import source_tree_hash
     fkb = sum(fetch.values()) / len(fetch)
     wkb = sum(write.values()) / len(write)
     alg = reads * reclen / launches
+    stream, _ = per_dispatch(rows(src + "/prof_fetch_stream/**/*counter_collection.csv"), "FETCH_SIZE")
+    calib = None
+    if stream:  # stream-only ablation: every byte read once by 16-B/lane tile loads, nothing else
+        skb = sum(stream.values()) / len(stream)
+        calib = {"fetch_size_kb_avg": skb, "hbm_bytes_x2": int(2 * skb * 1024),
+                 "x2_over_algorithmic": round(2 * skb * 1024 / alg, 4)}
     out = {
-        "round": int(os.environ.get("ROUND", "2")),
+        "round": int(os.environ.get("ROUND", "3")),
+        "tree_hash": source_tree_hash(),
+        "samples": int(os.environ.get("SAMPLES", "96")),
+        "index_len": int(os.environ.get("INDEX_LEN", "8")),
+        "combinatorial": os.environ.get("COMBINATORIAL", "0") == "1",
         "kernel": KERNEL,
         "reads": reads,
         "read_len": read_len,
@@ -69,10 +86,12 @@ def main():
                       "-> x2; WRITE_SIZE taken as is; units KiB",
         "hbm_bytes_per_launch": int(2 * fkb * 1024 + wkb * 1024),
         "traffic_over_algorithmic": round((2 * fkb * 1024 + wkb * 1024) / alg, 4),
+        "fetch_over_algorithmic": round(2 * fkb * 1024 / alg, 4),
+        "stream_only_calibration": calib,
         "source": f"profiles/{tag}_pmc_chunk_kernel.csv (rocprofv3 --pmc FETCH_SIZE, then --pmc WRITE_SIZE, "
                   f"separate runs of bench.py {os.environ.get('PROF_ARGS', '--steps 5 --warmup 1 --no-cpu')})",
     }
-    with open(os.path.join(prof, os.environ.get("TRAFFIC_JSON", "traffic_r02.json")), "w") as fh:
+    with open(os.path.join(prof, os.environ.get("TRAFFIC_JSON", "traffic_r03.json")), "w") as fh:
         json.dump(out, fh, indent=1)
     print(json.dumps(out, indent=1))
 

@@ -50,3 +50,22 @@ def test_key_codec_roundtrip():
     keys = np.array([sum(sym[c] << (3 * i) for i, c in enumerate(s)) for s in codes], dtype=np.uint64)
     assert _lib.decode_keys(keys) == codes
     assert _lib.pack_lower("acgtx") == 1 | 2 << 3 | 3 << 6 | 4 << 9 | 7 << 12
+
+
+def test_bench_refuses_traffic_of_another_tree(tmp_path):
+    """bench.py reports PMC traffic only from a file taken on this source tree and launch shape."""
+    import json
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    from frender_amd._lib import source_tree_hash
+    tree = source_tree_hash()
+    p = str(tmp_path / "t.json")
+    rec = {"tree_hash": tree, "algorithmic_bytes_per_launch": 3.7e9, "samples": 96, "index_len": 8,
+           "combinatorial": False, "hbm_bytes_per_launch": 4000000000, "traffic_over_algorithmic": 1.08}
+    for change, ok in (({}, True), ({"tree_hash": "0" * 16}, False), ({"samples": 384}, False)):
+        with open(p, "w") as f:
+            json.dump({**rec, **change}, f)
+        t, note = bench.load_traffic(p, tree, 3.7e9, 96, 8, False)
+        assert (t == 4000000000) == ok and (note.startswith("refused") != ok), note
+    assert bench.load_traffic(str(tmp_path / "absent.json"), tree, 3.7e9, 96, 8, False)[0] is None

@@ -30,13 +30,15 @@ struct fr_ctx {
     u32 cold_cap = 8192;
     // launch log (fr_internal.h LogEntry): commits append, launch_log_aggregate folds it into the table
     LogEntry* log = nullptr;
-    LogEntry* log_sorted = nullptr;
     u64 log_cap = 0;
-    u32* log_hist = nullptr;       // aggregation scratch, (AGG_SLICES + 3) x AGG_NB + 64
+    u32 log_rcap = 0;              // entries per log region (LOG_NR regions)
+    LogEntry* log_sub = nullptr;   // the split pass's sub-region parts (LOG_NSUB x log_scap)
+    u32 log_scap = 0;
     void* log_temp = nullptr;
     size_t log_temp_bytes = 0;
     u32 log_min = 2600;            // pairs from which a commit logs (SYN-v1 config 2's full chunks commit ~1740 pairs
                                    // and are faster inserted directly; config 3's ~2680 are faster logged)
+    u32 log_hot = 4;               // a logged commit's LDS entries of >= log_hot records insert directly (FR_LOG_HOT)
     uint4* rare = nullptr;
 
     DevState* st = nullptr;
@@ -133,6 +135,16 @@ struct fr_ctx {
     u64 sheet_cap = 0;
     u64 sheet_bytes = 0;  // the blob last uploaded (h_sheet holds it)
     int cp_stride = 0;
+    int32_t* d_canon = nullptr;  // per list (idx1, idx2, rc(idx2)): the first row holding the row's value
+    u64 sheet_ver = 0;           // bumped on every upload of a different sheet
+
+    // classify neighbourhood maps (fr_internal.h NbrMap) of sheet version nbr_ver and nbr_nsubs
+    u8* d_nbr = nullptr;
+    u64 nbr_cap = 0;
+    u64 nbr_ver = ~0ull;
+    int nbr_nsubs = -1, nbr_rc = 0;
+    NbrMap nbr{};
+    bool nbr_enabled = true;  // FR_NBR=0: every code takes the row scan (A/B and tests)
 
     // finalized table
     u64 U = 0;
@@ -519,7 +531,9 @@ static int launch_range(fr_ctx* ctx, const u8* dptr, u64 len, u64 avail, int own
     a.cold = ctx->cold;
     a.log = exo_only ? nullptr : ctx->log;
     a.log_cap = ctx->log_cap;
+    a.log_rcap = ctx->log_rcap;
     a.log_min = ctx->log_min;
+    a.log_hot = ctx->log_hot;
     a.rare = ctx->rare;
     // workgroups take chunks by ticket; never more than the resident grid (cold lists are per block)
     const int grid = (int)std::min<u64>(a.num_chunks, G);
@@ -530,7 +544,7 @@ static int launch_range(fr_ctx* ctx, const u8* dptr, u64 len, u64 avail, int own
     ctx->last_valid = true;
     CK(hipEventRecord(ctx->ev_b[ctx->ev_used], ctx->stream));
     if (a.log)
-        CK(launch_log_aggregate(ctx->tab, ctx->st, ctx->log, ctx->log_sorted, ctx->log_cap, ctx->log_hist, a.file_tag,
+        CK(launch_log_aggregate(ctx->tab, ctx->st, ctx->log, ctx->log_rcap, ctx->log_sub, ctx->log_scap, a.file_tag,
                                 a.file_offset, ctx->ablate, ctx->stream));
     CK(hipEventRecord(ctx->ev_l[ctx->ev_used], ctx->stream));
     ctx->ev_used++;
@@ -562,6 +576,7 @@ fr_ctx* fr_create(int device, uint64_t chunk_bytes, uint64_t table_slots) {
     if (const char* g = getenv("FR_GRID")) ctx->grid = std::max(1, atoi(g));
     if (const char* f = getenv("FR_FLUSH_AT")) ctx->flush_at = (u32)atoi(f);
     if (const char* f = getenv("FR_ABLATE")) ctx->ablate = (u32)atoi(f);
+    if (const char* f = getenv("FR_NBR")) ctx->nbr_enabled = atoi(f) != 0;
     if (const char* f = getenv("FR_COLD_CAP")) ctx->cold_cap = (u32)std::max(1024, atoi(f));
     if ((e = dalloc(&ctx->cold, 2ull * ctx->cold_cap * (u64)ctx->grid)) != hipSuccess) return bad("cold lists", e);
     if ((e = dalloc(&ctx->rare, (u64)RARE_RING * (u64)ctx->grid)) != hipSuccess) return bad("rare rings", e);
@@ -574,14 +589,17 @@ fr_ctx* fr_create(int device, uint64_t chunk_bytes, uint64_t table_slots) {
     // FR_LOG=0 turns the log off, FR_LOG_MIN sets the threshold (pairs per commit)
     const char* fl = getenv("FR_LOG");
     if (!fl || atoi(fl) != 0) {
-        ctx->log_cap = std::min<u64>(std::max<u64>(ctx->chunk_bytes / 256, 1ull << 16), 1ull << 26);
+        // entries: 1 per 256 B of a launch (SYN-v1 config 3 logs ~1 per 700 B), in LOG_NR equal regions;
+        // a run past its region's end inserts directly
+        const u64 want = std::min<u64>(std::max<u64>(ctx->chunk_bytes / 256, 1ull << 16), 1ull << 26);
+        ctx->log_rcap = (u32)(want / LOG_NR);
+        ctx->log_cap = (u64)ctx->log_rcap * LOG_NR;
+        ctx->log_scap = (u32)std::max<u64>(2ull * ctx->log_rcap / LOG_SUBS, 64);  // 2x the mean share
         if ((e = dalloc(&ctx->log, ctx->log_cap)) != hipSuccess) return bad("launch log", e);
-        if ((e = dalloc(&ctx->log_sorted, ctx->log_cap)) != hipSuccess) return bad("launch log", e);
-        const u64 nh = (u64)(AGG_SLICES + 3) * AGG_NB + 64;  // + AggScratch::ctl
-        if ((e = dalloc(&ctx->log_hist, nh)) != hipSuccess) return bad("log histogram", e);
-        if ((e = hipMemset(ctx->log_hist, 0, nh * sizeof(u32))) != hipSuccess) return bad("log histogram", e);
+        if ((e = dalloc(&ctx->log_sub, (u64)ctx->log_scap * LOG_NSUB)) != hipSuccess) return bad("launch log parts", e);
     }
     if (const char* f = getenv("FR_LOG_MIN")) ctx->log_min = (u32)std::max(0, atoi(f));
+    if (const char* f = getenv("FR_LOG_HOT")) ctx->log_hot = (u32)std::max(1, atoi(f));
     if (const char* f = getenv("FR_CHUNK_TILES")) ctx->chunk_tiles = (u32)std::max(2, atoi(f));
     if (const char* f = getenv("FR_CHUNK_TILES_HEAVY")) ctx->chunk_tiles_heavy = (u32)std::max(2, atoi(f));
     if (const char* f = getenv("FR_RAMP")) ctx->ramp = atoi(f) != 0;
@@ -646,7 +664,7 @@ void fr_destroy(fr_ctx* ctx) {
                    ctx->d_keys, ctx->d_counts, ctx->d_first, ctx->d_keys_s, ctx->d_counts_s,
                    ctx->d_first_s, ctx->d_pos, ctx->d_perm, ctx->d_rank, ctx->d_counter, ctx->d_temp, ctx->d_bins, ctx->d_binbase, ctx->d_arr, ctx->d_rows, ctx->d_pres_u,
                    ctx->d_pres_f, ctx->d_m1, ctx->d_m2, ctx->d_row, ctx->d_rm2, ctx->d_rrow, ctx->d_cls, ctx->d_rcls,
-                   ctx->d_errw, ctx->d_errf, ctx->d_rcf, ctx->d_rcr, ctx->cold, ctx->rare, ctx->chunk_info, ctx->log, ctx->log_sorted, ctx->log_hist, ctx->log_temp};
+                   ctx->d_errw, ctx->d_errf, ctx->d_rcf, ctx->d_rcr, ctx->d_nbr, ctx->cold, ctx->rare, ctx->chunk_info, ctx->log, ctx->log_sub, ctx->log_temp};
     for (void* p : dev)
         if (p) (void)hipFree(p);
     if (ctx->h_st) (void)hipHostFree(ctx->h_st);
@@ -730,7 +748,8 @@ int fr_set_sheet(fr_ctx* ctx, int S, const uint64_t* idx1_packed, const int32_t*
     const u64 o_i2 = al(S * 8ull), o_i2rc = o_i2 + al(S * 8ull), o_name = o_i2rc + al(S * 8ull);
     const u64 o_cp1 = o_name + al(S * 4ull), o_cp2 = o_cp1 + al(ncp * 4), o_cp2rc = o_cp2 + al(ncp * 4);
     const u64 o_l1 = o_cp2rc + al(ncp * 4), o_l2 = o_l1 + (with_cp ? al(S * 4ull) : 0);
-    const u64 total = o_l2 + (with_cp ? al(S * 4ull) : 0) + 8;
+    const u64 o_canon = o_l2 + (with_cp ? al(S * 4ull) : 0);
+    const u64 total = o_canon + al(3 * S * 4ull) + 8;
     std::vector<u8> blob(total, 0);
     u8* h = blob.data();
     if (S) {
@@ -738,6 +757,14 @@ int fr_set_sheet(fr_ctx* ctx, int S, const uint64_t* idx1_packed, const int32_t*
         std::memcpy(h + o_i2, idx2_packed, S * 8ull);
         std::memcpy(h + o_i2rc, idx2rc_packed, S * 8ull);
         std::memcpy(h + o_name, name_id, S * 4ull);
+        // value ids of the neighbourhood maps: the first row with the same packed value
+        const uint64_t* lists[3] = {idx1_packed, idx2_packed, idx2rc_packed};
+        int32_t* canon = (int32_t*)(h + o_canon);
+        for (int l = 0; l < 3; ++l) {
+            std::unordered_map<u64, int32_t> first;
+            first.reserve(S * 2);
+            for (int i = 0; i < S; ++i) canon[l * S + i] = first.emplace(lists[l][i], i).first->second;
+        }
     }
     if (with_cp) {
         std::memcpy(h + o_cp1, idx1_cp, ncp * 4);
@@ -762,6 +789,7 @@ int fr_set_sheet(fr_ctx* ctx, int S, const uint64_t* idx1_packed, const int32_t*
         }
         std::memcpy(ctx->h_sheet, h, total);
         ctx->sheet_bytes = total;
+        ++ctx->sheet_ver;
         CK(hipMemcpyAsync(ctx->d_sheet, ctx->h_sheet, total, hipMemcpyHostToDevice, ctx->stream));
     }
     u8* d = ctx->d_sheet;
@@ -774,6 +802,7 @@ int fr_set_sheet(fr_ctx* ctx, int S, const uint64_t* idx1_packed, const int32_t*
     ctx->d_cp2rc = with_cp ? (u32*)(d + o_cp2rc) : nullptr;
     ctx->d_cpl1 = with_cp ? (int32_t*)(d + o_l1) : nullptr;
     ctx->d_cpl2 = with_cp ? (int32_t*)(d + o_l2) : nullptr;
+    ctx->d_canon = (int32_t*)(d + o_canon);
     ctx->cp_stride = with_cp ? cp_stride : 0;
     ctx->S = S;
     ctx->n_names = n_names;
@@ -1281,6 +1310,46 @@ static int ensure_class_scratch(fr_ctx* ctx, u64 n) {
     return FR_OK;
 }
 
+// the classify neighbourhood maps of the current sheet and nsubs (stream-ordered, rebuilt only when
+// the sheet, nsubs or the rc need changed); nbr.on = 0 when the sheet does not suit them (mixed or
+// > 21-symbol lengths, or more than NBR_MAX codes per list) or FR_NBR=0
+static int ensure_nbr(fr_ctx* ctx, const SheetArgs& sh, int nsubs, int rc) {
+    constexpr u64 NBR_MAX = 1ull << 21;
+    if (ctx->nbr_ver == ctx->sheet_ver && ctx->nbr_nsubs == nsubs && (ctx->nbr_rc || !rc)) return FR_OK;
+    ctx->nbr.on = 0;
+    ctx->nbr_ver = ctx->sheet_ver;
+    ctx->nbr_nsubs = nsubs;
+    ctx->nbr_rc = rc;
+    if (!ctx->nbr_enabled || sh.S <= 0 || nsubs < 0 || sh.L1u < 0 || sh.L1u > 21 || sh.L2u < 0 || sh.L2u > 21)
+        return FR_OK;
+    const u64 c1 = (u64)sh.S * nbr_codes_per_row(sh.L1u, nsubs), c2 = (u64)sh.S * nbr_codes_per_row(sh.L2u, nsubs);
+    if (c1 > NBR_MAX || c2 > NBR_MAX) return FR_OK;
+    const u64 n1 = std::max<u64>(pow2_at_least(2 * c1), 1024), n2 = std::max<u64>(pow2_at_least(2 * c2), 1024);
+    const u64 np = std::max<u64>(pow2_at_least(2 * (u64)sh.S), 64);
+    const u64 bytes = (n1 + 2 * n2) * sizeof(NSlot) + 2 * np * sizeof(PSlot);
+    if (bytes > ctx->nbr_cap) {
+        CK(hipStreamSynchronize(ctx->stream));  // an earlier classify may still read the old maps
+        if (ctx->d_nbr) CK(hipFree(ctx->d_nbr));
+        ctx->d_nbr = nullptr;
+        ctx->nbr_cap = 0;
+        CK(hipMalloc(&ctx->d_nbr, bytes));
+        ctx->nbr_cap = bytes;
+    }
+    NbrMap& m = ctx->nbr;
+    m.m[0] = (NSlot*)ctx->d_nbr;
+    m.m[1] = m.m[0] + n1;
+    m.m[2] = m.m[1] + n2;
+    m.p[0] = (PSlot*)(m.m[2] + n2);
+    m.p[1] = m.p[0] + np;
+    m.mmask[0] = (u32)(n1 - 1);
+    m.mmask[1] = m.mmask[2] = (u32)(n2 - 1);
+    m.pmask[0] = m.pmask[1] = (u32)(np - 1);
+    CK(hipMemsetAsync(ctx->d_nbr, 0, bytes, ctx->stream));
+    CK(launch_nbr_build(sh, ctx->d_canon, nsubs, rc, m, ctx->stream));
+    m.on = 1;
+    return FR_OK;
+}
+
 int fr_classify(fr_ctx* ctx, int num_subs, int rc_mode, int16_t* m1, int16_t* m2, uint8_t* cls, int16_t* row,
                 int16_t* rc_m2, uint8_t* rc_cls, int16_t* rc_row, int64_t* err_unique, int32_t* err_which) {
     if (ctx->S < 0) return fail(ctx, FR_ERR_INVALID, "fr_classify: no sheet");
@@ -1292,10 +1361,11 @@ int fr_classify(fr_ctx* ctx, int num_subs, int rc_mode, int16_t* m1, int16_t* m2
     CK(hipMemsetAsync(ctx->d_rcf, 0, std::max(ctx->n_names, 1) * 8, ctx->stream));
     CK(hipMemsetAsync(ctx->d_rcr, 0, std::max(ctx->n_names, 1) * 8, ctx->stream));
     SheetArgs sh{ctx->S, ctx->n_names, ctx->L1u, ctx->L2u, ctx->d_i1, ctx->d_i2, ctx->d_i2rc, ctx->d_name};
+    if ((rc = ensure_nbr(ctx, sh, num_subs, rc_mode ? 1 : 0))) return rc;
     ClassOut o{ctx->d_m1, ctx->d_m2, ctx->d_cls, ctx->d_row, ctx->d_rm2, ctx->d_rcls, ctx->d_rrow,
                ctx->d_rcf, ctx->d_rcr, ctx->d_errf, ctx->d_errw};
     CK(hipEventRecord(e0, ctx->stream));
-    CK(launch_classify(ctx->d_keys_s, ctx->d_counts_s, n, sh, num_subs, rc_mode ? 1 : 0, o, ctx->stream));
+    CK(launch_classify(ctx->d_keys_s, ctx->d_counts_s, n, sh, num_subs, rc_mode ? 1 : 0, o, ctx->nbr, ctx->stream));
     CK(hipEventRecord(e1, ctx->stream));
     u64 ef = ~0ull;
     CK(hipMemcpyAsync(&ef, ctx->d_errf, 8, hipMemcpyDeviceToHost, ctx->stream));

@@ -71,21 +71,29 @@ struct alignas(32) Overflow {
     u32 tag, pad;
 };
 
-// One tallied (code, count) pair on its way to the HBM table: a chunk's LDS-table slots and cold-list
-// misses are appended to the launch's log at the chunk's commit; after the launch the log is
-// bucketed by key hash and each bucket is aggregated in LDS, so the HBM table sees one insert per
-// distinct code per launch instead of one per commit and miss.
+// One tallied (code, count) pair on its way to the HBM table: a heavy chunk's LDS-table slots and
+// cold-list misses go to the launch log at the chunk's commit, counted in LDS by the pairs' regions
+// (log_region: the table home's top LOG_REGION_BITS bits) and appended as one run per region to that
+// region's part of the log (one cursor atomic per region and commit: runs of tens of pairs).  After
+// the launch a split pass counting-sorts every region's part by sub-region (the next LOG_SUB_BITS home
+// bits) into the sub-region parts, and one workgroup per sub-region folds its part in LDS, so the HBM
+// table sees one insert per distinct code per launch instead of one per commit and miss.
 struct alignas(16) LogEntry {
     u64 key;
     u32 off;             // min range offset of the entry's records (the launch's file tag / offset complete the ordinal)
     u32 cnt;
 };
-#ifndef FR_AGG_LOG_NB
-#define FR_AGG_LOG_NB 12
+#ifndef FR_LOG_REGION_BITS
+#define FR_LOG_REGION_BITS 6
 #endif
-constexpr int AGG_LOG_NB = FR_AGG_LOG_NB;  // log2 of the buckets of the launch-log aggregation
-constexpr int AGG_NB = 1 << AGG_LOG_NB;
-constexpr int AGG_SLICES = 512;            // count / scatter workgroups (slices of the log)
+#ifndef FR_LOG_SUB_BITS
+#define FR_LOG_SUB_BITS 3
+#endif
+constexpr int LOG_REGION_BITS = FR_LOG_REGION_BITS;
+constexpr int LOG_NR = 1 << LOG_REGION_BITS;  // launch-log regions (parts of the log, one cursor each)
+constexpr int LOG_SUB_BITS = FR_LOG_SUB_BITS;
+constexpr int LOG_SUBS = 1 << LOG_SUB_BITS;   // sub-regions per region (aggregation workgroups)
+constexpr int LOG_NSUB = LOG_NR * LOG_SUBS;    // sub-regions in all
 
 struct DevState {
     u64 lines[2];        // terminators before the current range (launch parity)
@@ -115,6 +123,9 @@ struct DevState {
     u32 commits_done;    // chunks of the current launch that finished their commit (back to 0 by the last)
     u32 heavy_launches;  // ramped launches since the reset that walked the heavy geometry (diagnostics)
     u64 chunks_total;    // chunks committed since the reset
+    u32 log_rcur[LOG_NR];  // per launch-log region: entries claimed this launch (the aggregation zeroes them)
+    u32 log_scur[LOG_NSUB];  // per sub-region: entries the split pass placed (the aggregation zeroes them)
+    u32 log_red_done;    // aggregation workgroups finished (the last zeroes it)
 };
 
 struct Table {
@@ -161,8 +172,10 @@ struct ScanArgs {
     uint4* rare;         // chunk kernel: rare-event rings, [grid][RARE_RING] (fr_kernels.hip)
     u64* chunk_info;     // chunk kernel: per chunk {line count, spec flag + guessed phase << 1 in the high word}
     LogEntry* log;       // the launch log (nullptr: commits insert into the HBM table directly)
-    u64 log_cap;
+    u64 log_cap;         // LOG_NR x log_rcap
+    u32 log_rcap;        // entries per region (a run past it inserts directly)
     u32 log_min;         // a commit of at least log_min pairs goes to the log, smaller ones straight into the table
+    u32 log_hot;         // ... except its LDS entries of at least log_hot records, which insert directly
     u32 exo_only;        // replay of a launch whose exotic list overflowed: capture exotic records only (no
                          // table updates), every chunk with its exact line phase
     u32 spec_commit;     // commit speculative chunks without waiting for their exact prefix (checked at the
@@ -201,6 +214,30 @@ struct ClassOut {
 
 enum { CLS_UNDET = 0, CLS_HOP = 1, CLS_DEMUX = 2, CLS_AMBIG = 3 };
 
+// Classify neighbourhood maps (fr_kernels.hip, nbr_*), built per (sheet, nsubs): for each sheet list
+// (idx1, idx2, rc(idx2)) every packed code within nsubs substitutions of a distinct sheet value maps
+// to that value's id = the first row holding it; a code near several distinct values is marked
+// (vmin != vmax) and classified by the exact row scan.  The pair maps give, per (idx1 id, idx2 id),
+// the rows holding both values: their count and first row.
+constexpr u64 NBR_KEY = 1ull << 63;  // occupied-slot bit of a map key (packed codes use <= 63 bits)
+struct NSlot {
+    u64 key;     // packed code | NBR_KEY, 0 = empty
+    u32 vmin_c;  // ~(smallest value id)   (atomicMax; 0 = none)
+    u32 vmax1;   // largest value id + 1   (atomicMax)
+};
+struct PSlot {
+    u64 key;      // (id1 << 32 | id2) | NBR_KEY
+    u32 cnt;      // rows holding both values
+    u32 first_c;  // ~(first such row)
+};
+struct NbrMap {
+    NSlot* m[3];  // idx1, idx2, rc(idx2)
+    u32 mmask[3];
+    PSlot* p[2];  // (idx1, idx2), (idx1, rc(idx2))
+    u32 pmask[2];
+    int on;       // 0: every code takes the row scan
+};
+
 __host__ __device__ inline u64 mix64(u64 x) {
     x ^= x >> 30;
     x *= 0xBF58476D1CE4E5B9ull;
@@ -208,6 +245,13 @@ __host__ __device__ inline u64 mix64(u64 x) {
     x *= 0x94D049BB133111EBull;
     x ^= x >> 31;
     return x;
+}
+
+// launch-log region of a code: the top bits of mix64, as the table's home slot, so a region's codes
+// live in one contiguous part of a table of at least LOG_NR slots
+__host__ __device__ inline u32 log_region(u64 key) { return (u32)(mix64(key) >> (64 - LOG_REGION_BITS)); }
+__host__ __device__ inline u32 log_subregion(u64 key) {
+    return (u32)(mix64(key) >> (64 - LOG_REGION_BITS - LOG_SUB_BITS)) & (LOG_SUBS - 1);
 }
 
 // ---- launchers (fr_kernels.hip) --------------------------------------------------
@@ -245,7 +289,12 @@ hipError_t launch_fin_scatter(const GSlot* slots, u64 nslots, const BinMap& m, c
 hipError_t launch_fin_rank(GSlot* slots, u64 nk, const BinMap& m, const u32* base, const FinRow* rows, u64* keys_o,
                            u64* counts_o, u64* first_o, hipStream_t s);
 hipError_t launch_classify(const u64* keys, const u64* counts, u64 n, SheetArgs sh, int nsubs, int rc,
-                           ClassOut o, hipStream_t s);
+                           ClassOut o, const NbrMap& nm, hipStream_t s);
+// neighbourhood codes of one sheet row: sum over d <= nsubs of C(L, d) 5^d (every query symbol)
+u64 nbr_codes_per_row(int L, int nsubs);
+// (re)build the maps of nm (already allocated and zeroed) for the sheet sh; canon = 3 x S value ids
+hipError_t launch_nbr_build(const SheetArgs& sh, const int32_t* canon, int nsubs, int rc, const NbrMap& nm,
+                            hipStream_t s);
 hipError_t launch_classify_cp(int n, const u32* q1, const int32_t* q1len, const u32* q2, const int32_t* q2len,
                               int stride, int S, const u32* s1, const int32_t* s1len, const u32* s2,
                               const int32_t* s2len, const u32* s2rc, const int32_t* name, int nsubs, int rc,
@@ -254,9 +303,10 @@ hipError_t launch_presence_scan(const GSlot* slots, u64 n, u32 tag, Presence* pr
                                 hipStream_t s);
 hipError_t launch_merge(Table t, DevState* st, const u64* keys, const u64* counts, const u64* first, u64 n,
                         hipStream_t s);
-// aggregate the launch log into the table and empty it (stream-ordered; reads log_n on the device)
-hipError_t launch_log_aggregate(Table t, DevState* st, LogEntry* log, LogEntry* sorted, u64 cap, u32* hist, u32 file_tag,
-                                u64 file_offset, u32 ablate, hipStream_t s);
+// aggregate the launch log into the table and empty it (stream-ordered; reads log_n and the region
+// cursors on the device)
+hipError_t launch_log_aggregate(Table t, DevState* st, const LogEntry* log, u32 rcap, LogEntry* sub, u32 scap,
+                                u32 file_tag, u64 file_offset, u32 ablate, hipStream_t s);
 size_t log_aggregate_temp_bytes();
 hipError_t launch_synth(u8* out, u64 r0, u64 n, int R, u64 seed, const u8* idx1, const u8* idx2, int S, int L1,
                         int L2, hipStream_t s);

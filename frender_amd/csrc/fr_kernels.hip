@@ -127,9 +127,9 @@ __device__ __forceinline__ u64 wave_sum_u64(u64 v) {
 // load only ever over-estimates `first` / under-estimates `last_tag`, so skipping is safe).
 // Returns true when this call created the slot.  No global counters are touched here.
 // ------------------------------------------------------------------------------------
-// Home slot of a key: the TOP bits of mix64(key).  The launch-log buckets (log_bucket) are its top
-// AGG_LOG_NB bits too, so for tables of >= AGG_NB slots each bucket owns one contiguous slot region and
-// log_reduce_kernel's inserts stay inside it (DRAM-page and L2 locality instead of random lines).
+// Home slot of a key: the TOP bits of mix64(key).  The launch-log regions (log_region) are its top
+// LOG_REGION_BITS bits too, so for tables of >= LOG_NR slots each region owns one contiguous slot range
+// and log_reduce_kernel's inserts stay inside it (DRAM-page and L2 locality instead of random lines).
 __device__ __forceinline__ u64 table_home(u64 key, u64 mask) {
     return mask ? mix64(key) >> __builtin_clzll(mask) : 0ull;
 }
@@ -229,13 +229,12 @@ struct ScanShared {
     u32 created;             // HBM slots this workgroup created (added to n_keys once, at exit)
     u32 flags;
     u32 last;                // this workgroup published the launch's last chunk count (runs verify_launch)
-    u32 log_pos;             // commit: next free entry of this commit's launch-log block
-    u64 log_base;            // commit: the block's first entry (~0: the block did not fit, insert directly)
     u32 spec;                // side effects are buffered (a phase in use is a guess); the chunk may be redone
     u32 spec_bad;            // a speculation buffer overflowed: redo this chunk exactly
     u32 ncold;               // cold list fill
     u32 nexo;                // buffered exotic records
     u32 err_off;             // min range offset of a header without ' ' (buffered), ~0 none
+    u32 log_on;              // commit: pairs this commit logs
     u32 exo_p[EXO_BUF], exo_start[EXO_BUF], exo_len[EXO_BUF];
 };
 
@@ -939,31 +938,107 @@ __device__ __attribute__((noinline)) void commit_buffers(ScanShared& sh, const S
     const bool flush = !(a.ablate & 8u);  // ablation 8: no HBM flush of the LDS table / cold list
     const u32 nc = flush ? min(sh.ncold, a.cold_cap) : 0u;
     const u32 nl = flush ? sh.nkeys : 0u;  // claimed LDS slots = the live ones
-    bool logged = false;
     // heavy commits (at least log_min pairs: many distinct codes per chunk) go to the launch log,
     // aggregated after the launch; lighter ones insert straight into the table
-    if (a.log && nl + nc && nl + nc >= a.log_min) {
-        // one block of the launch log for this commit's pairs (aggregated after the launch:
-        // launch_log_aggregate); a block past the log's end is blanked and the pairs inserted below
-        if (tid == 0) {
-            const u64 base = atomicAdd((unsigned long long*)&a.st->log_n, (unsigned long long)(nl + nc));
-            atomicAdd((unsigned long long*)&a.st->log_commits, 1ull);
-            sh.log_base = base + nl + nc <= a.log_cap ? base : ~0ull;
-            sh.log_pos = 0;
-            if (base + nl + nc > a.log_cap)
-                for (u64 i = base; i < a.log_cap; ++i) a.log[i] = LogEntry{0, 0, 0};
-        }
-        __syncthreads();
-        logged = sh.log_base != ~0ull;
-    }
+    bool logged = false;
     const u64* cl = a.cold + 2ull * (u64)blockIdx.x * a.cold_cap;
-    if (logged) {
-        LogEntry* out = a.log + sh.log_base;
+    // LDS scratch of the logged commit (the walks are done): per-region run counters
+    u32* rcnt = &sh.raw[0][0];
+    u32* rcur = rcnt + LOG_NR;
+    u32* rbase = rcur + LOG_NR;  // each region's run start in its part of the log
+    static_assert(3 * LOG_NR * 4 <= sizeof(sh.raw), "log region scratch");
+    constexpr int CB = 8;  // cold entries per lane with their loads in flight together
+    // a logged commit sends its hot codes (chunk count >= log_hot: few per chunk, their slots L2-warm)
+    // straight to the table; the tail goes to the log, one run per region appended to the region's part
+    if (a.log && nl + nc && nl + nc >= a.log_min) {
+        for (int i = tid; i < LOG_NR; i += WG) rcnt[i] = rcur[i] = 0;
+        __syncthreads();
         for (int i = tid; i < NS; i += WG) {
             const LSlot e = sh.ls[i];
-            if (e.key) out[atomicAdd(&sh.log_pos, 1u)] = LogEntry{e.key, e.mino, e.cnt};
+            if (e.key && e.cnt < a.log_hot) atomicAdd(&rcnt[log_region(e.key)], 1u);
         }
-        for (u32 i = tid; i < nc; i += WG) out[nl + i] = LogEntry{cl[2 * i], (u32)(cl[2 * i + 1] - make_ord(a, 0)), 1u};
+        for (u32 i0 = tid; i0 < nc; i0 += CB * WG) {
+            u64 k[CB];
+#pragma unroll
+            for (int q = 0; q < CB; ++q) k[q] = i0 + q * WG < nc ? cl[2 * (i0 + q * WG)] : 0ull;
+#pragma unroll
+            for (int q = 0; q < CB; ++q)
+                if (i0 + q * WG < nc) atomicAdd(&rcnt[log_region(k[q])], 1u);
+        }
+        if (tid == 0) sh.log_on = 0;
+        __syncthreads();
+        FR_CSTAMP(1);
+        {  // one claim per region with a run, all in flight together
+            constexpr int PR = (LOG_NR + WG - 1) / WG;
+            u32 n[PR], base[PR], tot = 0;
+#pragma unroll
+            for (int j = 0; j < PR; ++j) {
+                const int r = tid + j * WG;
+                n[j] = r < LOG_NR ? rcnt[r] : 0u;
+                tot += n[j];
+            }
+#pragma unroll
+            for (int j = 0; j < PR; ++j) base[j] = n[j] ? atomicAdd(&a.st->log_rcur[tid + j * WG], n[j]) : 0u;
+#pragma unroll
+            for (int j = 0; j < PR; ++j)
+                if (tid + j * WG < LOG_NR) rbase[tid + j * WG] = base[j];
+            if (tot) atomicAdd(&sh.log_on, tot);
+        }
+        __syncthreads();
+        FR_CSTAMP(2);
+        if (tid == 0 && sh.log_on) {
+            atomicAdd((unsigned long long*)&a.st->log_n, (unsigned long long)sh.log_on);
+            atomicAdd((unsigned long long*)&a.st->log_commits, 1ull);
+        }
+        logged = sh.log_on != 0;  // else (nothing but hot codes) every pair inserts directly
+    }
+    if (logged) {
+        constexpr int CL = NS / WG;
+        const u64 ord0 = make_ord(a, 0);
+        // a pair past its region's end inserts directly (the region's claimed range up to its end is
+        // always written: the aggregation reads min(cursor, log_rcap) entries)
+        auto put = [&](u64 k, u32 off, u32 cnt) {
+            const u32 r = log_region(k);
+            const u64 pos = (u64)rbase[r] + atomicAdd(&rcur[r], 1u);
+            if (pos < a.log_rcap) {
+                a.log[(u64)r * a.log_rcap + pos] = LogEntry{k, off, cnt};
+            } else {
+                const u64 k1[1] = {k};
+                const bool v1[1] = {true};
+                Resolved r1[1];
+                made += resolve_batch<1>(a, k1, v1, r1);
+                apply_entry(a, r1[0], k, cnt, ord0 + off);
+            }
+        };
+        u64 hk[CL];
+        bool hv[CL];
+#pragma unroll
+        for (int b = 0; b < CL; ++b) {
+            const LSlot e = sh.ls[tid + b * WG];
+            hv[b] = e.key && e.cnt >= a.log_hot;
+            hk[b] = e.key;
+            if (e.key && !hv[b]) put(e.key, e.mino, e.cnt);
+        }
+        for (u32 i0 = tid; i0 < nc; i0 += CB * WG) {
+            u64 k[CB], o[CB];
+#pragma unroll
+            for (int q = 0; q < CB; ++q) {
+                const u32 i = i0 + q * WG;
+                k[q] = i < nc ? cl[2 * i] : 0ull;
+                o[q] = i < nc ? cl[2 * i + 1] : 0ull;
+            }
+#pragma unroll
+            for (int q = 0; q < CB; ++q)
+                if (i0 + q * WG < nc) put(k[q], (u32)(o[q] - ord0), 1u);
+        }
+        Resolved rh[CL];
+        made += resolve_batch<CL>(a, hk, hv, rh);
+#pragma unroll
+        for (int b = 0; b < CL; ++b) {
+            if (!hv[b]) continue;
+            const LSlot e = sh.ls[tid + b * WG];
+            apply_entry(a, rh[b], e.key, e.cnt, make_ord(a, e.mino));
+        }
     } else if (flush) {
         constexpr int CL = NS / WG;  // LDS slots per lane; also cold entries per lane per batch
         Resolved* park = (Resolved*)&sh.raw[0][0];  // the walks are done: the tile area holds NS resolutions
@@ -1640,38 +1715,12 @@ hipError_t launch_rehash(Table dst, DevState* st, const GSlot* src, u64 nsrc, hi
 }
 
 // ------------------------------------------------------------------------------------
-// launch-log aggregation: the tally kernel's commits append (code, count, first, tag) pairs to the
-// log instead of inserting each into the HBM table (one dependent slot load plus memory-side
-// atomics per pair).  After the launch the log is bucketed by key hash (histogram per slice of the
-// log, one exclusive scan, scatter), each bucket's pairs are aggregated in LDS by one workgroup,
-// and only the distinct codes reach the HBM table -- batched, with every slot load in flight at
-// once and nothing else competing for the memory system.
+// launch-log aggregation: the tally kernel's heavy commits append their (code, count, first) pairs to
+// the launch log's regions (commit_buffers) instead of inserting each into the HBM table (one
+// dependent slot load plus memory-side atomics per pair).  After the launch the workgroups of each
+// sub-region fold its codes in LDS and only the distinct codes reach the HBM table -- batched, with
+// every slot load in flight at once, and with plain stores: the sub-regions partition the codes.
 // ------------------------------------------------------------------------------------
-// bucket of a logged code: the top bits of mix64, as the table's home slot (table_home); the LDS table
-// of log_reduce_kernel indexes by mix64's low bits, independent of these
-__device__ __forceinline__ u32 log_bucket(u64 key) { return (u32)(mix64(key) >> (64 - AGG_LOG_NB)); }
-
-__device__ __forceinline__ void log_slice(u64 n, u32 s, u64& lo, u64& hi) {
-    const u64 per = (n + AGG_SLICES - 1) / AGG_SLICES;
-    lo = min(n, (u64)s * per);
-    hi = min(n, lo + per);
-}
-
-// aggregation scratch (fr_api allocates (AGG_SLICES + 3) * AGG_NB + 64 u32, zeroed once):
-//   sh[s][b]  per-slice bucket counts        total[b]  entries per bucket (zeroed again by the count pass's last block)
-//   base[b]   first entry of bucket b         cur[b]    scatter cursor (starts at base[b])
-struct AggScratch {
-    u32* sh;
-    u32* total;
-    u32* base;
-    u32* cur;
-    u32* ctl;  // [0] count-pass blocks done, [1] reduce-pass blocks done (each back to 0 by its last block)
-    __host__ __device__ static AggScratch at(u32* p) {
-        return AggScratch{p, p + (size_t)AGG_SLICES * AGG_NB, p + (size_t)(AGG_SLICES + 1) * AGG_NB,
-                          p + (size_t)(AGG_SLICES + 2) * AGG_NB, p + (size_t)(AGG_SLICES + 3) * AGG_NB};
-    }
-};
-
 // this block is the last of the grid to pass here (counter ctr, reset for the next launch); every
 // block's earlier global writes are visible to the last one
 __device__ __forceinline__ bool last_block(u32* ctr) {
@@ -1690,102 +1739,7 @@ __device__ __forceinline__ bool last_block(u32* ctr) {
     return last != 0;
 }
 
-// pass 1: bucket counts per slice of the log, summed per bucket with one atomic per (slice, bucket)
-__global__ __launch_bounds__(256) void log_count_kernel(const LogEntry* log, const DevState* st, u64 cap, AggScratch g) {
-    const u64 n = min(st->log_n, cap);
-    if (n == 0) return;
-    __shared__ u32 h[AGG_NB];
-    for (int i = threadIdx.x; i < AGG_NB; i += 256) h[i] = 0;
-    __syncthreads();
-    u64 lo, hi;
-    log_slice(n, blockIdx.x, lo, hi);
-    for (u64 i0 = lo + threadIdx.x; i0 < hi; i0 += 8 * 256) {  // eight loads in flight per thread
-        u64 k[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const u64 i = i0 + (u64)q * 256;
-            k[q] = i < hi ? log[i].key : 0ull;
-        }
-#pragma unroll
-        for (int q = 0; q < 8; ++q)
-            if (k[q]) atomicAdd(&h[log_bucket(k[q])], 1u);
-    }
-    __syncthreads();
-    u32* row = g.sh + (size_t)blockIdx.x * AGG_NB;
-    for (int b = threadIdx.x; b < AGG_NB; b += 256) {
-        const u32 c = h[b];
-        row[b] = c;
-        if (c) atomicAdd(&g.total[b], c);
-    }
-    if (!last_block(&g.ctl[0])) return;
-    // the last block: bucket bases = exclusive scan of the totals; cursors start there
-    constexpr int PER = AGG_NB / 256;
-    __shared__ u32 ws[4];
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    u32 v[PER], sum = 0;
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-        v[j] = __hip_atomic_load(&g.total[tid * PER + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        sum += v[j];
-    }
-    u32 x = sum;  // inclusive wave scan, then across the 4 waves
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const u32 y = __shfl_up(x, d, 64);
-        if (lane >= d) x += y;
-    }
-    if (lane == 63) ws[wid] = x;
-    __syncthreads();
-    u32 run = x - sum;
-    for (int w = 0; w < wid; ++w) run += ws[w];
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-        const int b = tid * PER + j;
-        g.base[b] = run;
-        g.cur[b] = run;
-        g.total[b] = 0;  // ready for the next launch's pass 1
-        run += v[j];
-    }
-}
-
-// pass 3: each slice claims its run of every bucket (one atomic per non-empty bucket) and scatters
-__global__ __launch_bounds__(256) void log_scatter_kernel(const LogEntry* log, const DevState* st, u64 cap, AggScratch g,
-                                                          LogEntry* sorted) {
-    const u64 n = min(st->log_n, cap);
-    if (n == 0) return;
-    __shared__ u32 o[AGG_NB];
-    const u32* row = g.sh + (size_t)blockIdx.x * AGG_NB;
-    for (int b = threadIdx.x; b < AGG_NB; b += 256) {
-        const u32 c = row[b];
-        o[b] = c ? atomicAdd(&g.cur[b], c) : 0u;
-    }
-    __syncthreads();
-    u64 lo, hi;
-    log_slice(n, blockIdx.x, lo, hi);
-    for (u64 i0 = lo + threadIdx.x; i0 < hi; i0 += 8 * 256) {  // eight loads in flight per thread
-        LogEntry e[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const u64 i = i0 + (u64)q * 256;
-            e[q] = i < hi ? log[i] : LogEntry{0, 0, 0};
-        }
-        u32 pos[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) pos[q] = e[q].key ? atomicAdd(&o[log_bucket(e[q].key)], 1u) : 0u;
-#pragma unroll
-        for (int q = 0; q < 8; ++q)
-            if (e[q].key) sorted[pos[q]] = e[q];
-    }
-}
-
-#ifndef FR_AGG_LNS
-#define FR_AGG_LNS 2048
-#endif
-constexpr int AGG_LNS = FR_AGG_LNS;  // LDS slots of one bucket's aggregation
-#ifndef FR_AGG_LB
-#define FR_AGG_LB 4
-#endif
-constexpr int AGG_LB = FR_AGG_LB;  // log rows per thread in flight
+constexpr int AGG_LNS = 4096;  // LDS slots of one sub-region's aggregation (64 KB: 2 workgroups per CU)
 constexpr int AGG_PROBE = 64;
 struct alignas(16) AggSlot {
     u64 key;
@@ -1891,95 +1845,179 @@ __device__ __forceinline__ u32 insert_rows(const Table& T, DevState* st, const u
     return made;
 }
 
-// pass 4: each bucket's rows aggregated in LDS (records summed, min offset), then its distinct codes
-// inserted into the HBM table with the launch's ordinal base and file tag.  Persistent grid over the
-// buckets.
-__global__ __launch_bounds__(256) void log_reduce_kernel(Table t, DevState* st, const LogEntry* sorted, AggScratch g,
+// Split pass: every region's part of the log counting-sorted by sub-region into the sub-region parts.
+// SPLIT_WGS workgroups per region take 2048-entry tiles of its part (each wave a contiguous 512-entry
+// slab: coalesced loads); wave ballots rank each entry among its wave's entries of the same sub-region,
+// one cursor atomic per (tile, sub-region) places the tile's run, and the stores go out as runs of
+// ~256 consecutive entries.  A sub-region part that is full takes the rest directly into the table.
+constexpr int SPLIT_PER = 8;
+constexpr int SPLIT_TILE = SPLIT_PER * 256;
+#ifndef FR_SPLIT_WGS
+#define FR_SPLIT_WGS 32
+#endif
+constexpr int SPLIT_WGS = FR_SPLIT_WGS;
+__global__ __launch_bounds__(256) void log_split_kernel(Table t, DevState* st, const LogEntry* log, u32 rcap,
+                                                        LogEntry* sub, u32 scap, u32 file_tag, u64 ord0) {
+    if (st->log_n == 0) return;
+    const u32 r = blockIdx.x / SPLIT_WGS, j = blockIdx.x % SPLIT_WGS;
+    const u32 n = min(st->log_rcur[r], rcap);
+    const LogEntry* part = log + (u64)r * rcap;
+    __shared__ u32 wcnt[4][LOG_SUBS];
+    __shared__ u32 sbase[4][LOG_SUBS];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const u64 lt = (1ull << lane) - 1ull;
+    u32 made = 0;
+    for (u32 t0 = j * SPLIT_TILE; t0 < n; t0 += SPLIT_WGS * SPLIT_TILE) {
+        LogEntry e[SPLIT_PER];
+        u32 sb[SPLIT_PER], rank[SPLIT_PER];
+        u32 run[LOG_SUBS];
+#pragma unroll
+        for (int s = 0; s < LOG_SUBS; ++s) run[s] = 0;
+#pragma unroll
+        for (int q = 0; q < SPLIT_PER; ++q) {
+            const u32 i = t0 + w * 64 * SPLIT_PER + q * 64 + lane;
+            e[q] = i < n ? part[i] : LogEntry{0, 0, 0};
+        }
+#pragma unroll
+        for (int q = 0; q < SPLIT_PER; ++q) {
+            sb[q] = e[q].key ? log_subregion(e[q].key) : (u32)LOG_SUBS;
+            rank[q] = 0;
+#pragma unroll
+            for (int s = 0; s < LOG_SUBS; ++s) {
+                const u64 m = __ballot(sb[q] == (u32)s);
+                if (sb[q] == (u32)s) rank[q] = run[s] + (u32)__popcll(m & lt);
+                run[s] += (u32)__popcll(m);
+            }
+        }
+        if (lane == 0) {
+#pragma unroll
+            for (int s = 0; s < LOG_SUBS; ++s) wcnt[w][s] = run[s];
+        }
+        __syncthreads();
+        if (tid < LOG_SUBS) {
+            u32 tot = 0;
+#pragma unroll
+            for (int v = 0; v < 4; ++v) tot += wcnt[v][tid];
+            u32 b = tot ? atomicAdd(&st->log_scur[r * LOG_SUBS + tid], tot) : 0u;
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                sbase[v][tid] = b;
+                b += wcnt[v][tid];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < SPLIT_PER; ++q) {
+            if (sb[q] >= (u32)LOG_SUBS) continue;
+            const u32 pos = sbase[w][sb[q]] + rank[q];
+            if (pos < scap) {
+                sub[(u64)(r * LOG_SUBS + sb[q]) * scap + pos] = e[q];
+            } else {
+                const u64 key1[1] = {e[q].key};
+                const u32 cnt1[1] = {e[q].cnt};
+                const u64 ord1[1] = {ord0 + e[q].off};
+                const u32 tag1[1] = {file_tag};
+                const bool v1[1] = {true};
+                made += insert_rows<1>(t, st, key1, cnt1, ord1, tag1, v1);
+            }
+        }
+        __syncthreads();  // wcnt / sbase are reused by the next tile
+    }
+    add_created(st, made);
+}
+
+// One workgroup per sub-region: its part of the log (coalesced, eight entries in flight per thread)
+// folded in LDS (records summed, min offset), then its distinct codes inserted into the HBM table with
+// the launch's ordinal base and file tag.  The sub-regions partition the codes, so found and claimed
+// slots take plain stores (insert_rows EXCL).  The last workgroup empties the log for the next launch.
+__global__ __launch_bounds__(256) void log_reduce_kernel(Table t, DevState* st, const LogEntry* sub, u32 scap,
                                                          u32 file_tag, u64 ord0, u32 ablate) {
     if (st->log_n == 0) return;
     __shared__ AggSlot ls[AGG_LNS];
     u32 made = 0;
     for (int i = threadIdx.x; i < AGG_LNS; i += 256) ls[i] = AggSlot{0, 0xFFFFFFFFu, 0};
     __syncthreads();
-    for (u32 bk = blockIdx.x; bk < (u32)AGG_NB; bk += gridDim.x) {
-        const u64 lo = g.base[bk], hi = bk + 1 < (u32)AGG_NB ? (u64)g.base[bk + 1] : (u64)g.cur[bk];
-        if (lo == hi) continue;  // uniform: nothing logged for this bucket (its LDS table is still clean)
-        // AGG_LB rows per thread in flight per step (a step's loads are independent of its LDS work)
-        for (u64 i0 = lo + threadIdx.x; i0 < ((ablate & 512u) ? lo : hi); i0 += AGG_LB * 256) {  // 512: timing ablation
-            LogEntry ev[AGG_LB];
+    const u32 n = min(st->log_scur[blockIdx.x], scap);
+    const LogEntry* part = sub + (u64)blockIdx.x * scap;
+    u64 sink = 0;
+    constexpr int LB = 8;  // entries per thread in flight
+    for (u32 i0 = threadIdx.x; i0 < ((ablate & 512u) ? 0u : n); i0 += LB * 256) {  // 512: timing ablation
+        LogEntry ev[LB];
 #pragma unroll
-            for (int q = 0; q < AGG_LB; ++q) {
-                const u64 i = i0 + (u64)q * 256;
-                ev[q] = i < hi ? sorted[i] : LogEntry{0, 0, 0};
+        for (int q = 0; q < LB; ++q) ev[q] = i0 + q * 256 < n ? part[i0 + q * 256] : LogEntry{0, 0, 0};
+#pragma unroll
+        for (int q = 0; q < LB; ++q) {
+            const LogEntry e = ev[q];
+            if (!e.key) continue;
+            if (ablate & 1024u) {  // timing ablation: loads only
+                sink ^= e.key;
+                continue;
             }
-#pragma unroll
-            for (int q = 0; q < AGG_LB; ++q) {
-                const LogEntry e = ev[q];
-                if (!e.key) continue;
-                u32 h = (u32)mix64(e.key) & (AGG_LNS - 1);
-                bool done = false;
-                for (int pr = 0; pr < AGG_PROBE && !done; ++pr) {
-                    u64 k = ls[h].key;
-                    if (k == 0) {
-                        const u64 old = atomicCAS((unsigned long long*)&ls[h].key, 0ull, (unsigned long long)e.key);
-                        k = old == 0 ? e.key : old;
-                    }
-                    if (k == e.key) {
-                        atomicAdd(&ls[h].cnt, e.cnt);
-                        if (e.off < ls[h].mino) atomicMin(&ls[h].mino, e.off);
-                        done = true;
-                    }
-                    h = (h + 1) & (AGG_LNS - 1);
+            u32 h = (u32)mix64(e.key) & (AGG_LNS - 1);
+            bool done = false;
+            for (int pr = 0; pr < AGG_PROBE && !done; ++pr) {
+                u64 k = ls[h].key;
+                if (k == 0) {
+                    const u64 old = atomicCAS((unsigned long long*)&ls[h].key, 0ull, (unsigned long long)e.key);
+                    k = old == 0 ? e.key : old;
                 }
-                if (!done) {  // a full bucket table: this row goes in on its own
-                    const u64 key1[1] = {e.key};
-                    const u32 cnt1[1] = {e.cnt};
-                    const u64 ord1[1] = {ord0 + e.off};
-                    const u32 tag1[1] = {file_tag};
-                    const bool v1[1] = {true};
-                    made += insert_rows<1>(t, st, key1, cnt1, ord1, tag1, v1);
+                if (k == e.key) {
+                    atomicAdd(&ls[h].cnt, e.cnt);
+                    if (e.off < ls[h].mino) atomicMin(&ls[h].mino, e.off);
+                    done = true;
                 }
+                h = (h + 1) & (AGG_LNS - 1);
+            }
+            if (!done) {  // a full LDS table: this row goes in on its own
+                const u64 key1[1] = {e.key};
+                const u32 cnt1[1] = {e.cnt};
+                const u64 ord1[1] = {ord0 + e.off};
+                const u32 tag1[1] = {file_tag};
+                const bool v1[1] = {true};
+                made += insert_rows<1>(t, st, key1, cnt1, ord1, tag1, v1);
             }
         }
-        __syncthreads();
-        for (int i0 = threadIdx.x; i0 < ((ablate & 256u) ? 0 : AGG_LNS); i0 += 4 * 256) {  // 256: timing ablation
-            u64 key[4], ord[4];
-            u32 cnt[4], tag[4];
-            bool v[4];
+    }
+    if (sink == 1) atomicAdd((unsigned long long*)&st->stamp[7], 1ull);  // keeps the ablation's loads
+    __syncthreads();
+    for (int i0 = threadIdx.x; i0 < ((ablate & 256u) ? 0 : AGG_LNS); i0 += 4 * 256) {  // 256: timing ablation
+        u64 key[4], ord[4];
+        u32 cnt[4], tag[4];
+        bool v[4];
 #pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                const int i = i0 + b * 256;
-                const AggSlot e = i < AGG_LNS ? ls[i] : AggSlot{0, 0, 0};
-                v[b] = e.key != 0;
-                key[b] = e.key;
-                cnt[b] = e.cnt;
-                ord[b] = ord0 + e.mino;
-                tag[b] = file_tag;
-            }
-            made += insert_rows<4, true>(t, st, key, cnt, ord, tag, v);
+        for (int b = 0; b < 4; ++b) {
+            const int i = i0 + b * 256;
+            const AggSlot e = i < AGG_LNS ? ls[i] : AggSlot{0, 0, 0};
+            v[b] = e.key != 0;
+            key[b] = e.key;
+            cnt[b] = e.cnt;
+            ord[b] = ord0 + e.mino;
+            tag[b] = file_tag;
         }
-        __syncthreads();
-        for (int i = threadIdx.x; i < AGG_LNS; i += 256) ls[i] = AggSlot{0, 0xFFFFFFFFu, 0};
-        __syncthreads();
+        made += insert_rows<4, true>(t, st, key, cnt, ord, tag, v);
     }
     add_created(st, made);
-    // every block has read log_n: the last one empties the log for the next launch
-    if (last_block(&g.ctl[1]) && threadIdx.x == 0)
-        __hip_atomic_store(&st->log_n, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // every workgroup has read log_n and its cursor (the split pass read the region cursors before
+    // this launch): the last one empties the log
+    if (last_block(&st->log_red_done)) {
+        for (int i = threadIdx.x; i < LOG_NR; i += 256)
+            __hip_atomic_store(&st->log_rcur[i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int i = threadIdx.x; i < LOG_NSUB; i += 256)
+            __hip_atomic_store(&st->log_scur[i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (threadIdx.x == 0) __hip_atomic_store(&st->log_n, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 size_t log_aggregate_temp_bytes() { return 0; }
 
-hipError_t launch_log_aggregate(Table t, DevState* st, LogEntry* log, LogEntry* sorted, u64 cap, u32* hist, u32 file_tag,
-                                u64 file_offset, u32 ablate, hipStream_t s) {
-    const AggScratch g = AggScratch::at(hist);
-    // every pass reads log_n on the device and returns at once when no commit logged (the usual case
-    // for low-cardinality runs: only commits past ScanArgs::log_min pairs per 16 tiles log)
-    hipLaunchKernelGGL(log_count_kernel, dim3(AGG_SLICES), dim3(256), 0, s, log, st, cap, g);  // + bucket bases
-    hipLaunchKernelGGL(log_scatter_kernel, dim3(AGG_SLICES), dim3(256), 0, s, log, st, cap, g, sorted);
+hipError_t launch_log_aggregate(Table t, DevState* st, const LogEntry* log, u32 rcap, LogEntry* sub, u32 scap,
+                                u32 file_tag, u64 file_offset, u32 ablate, hipStream_t s) {
+    // reads log_n on the device and returns at once when no commit logged (the usual case for
+    // low-cardinality runs: only commits of at least ScanArgs::log_min pairs log)
     const u64 ord0 = ((u64)file_tag << ORD_SHIFT) | file_offset;
-    static const int rgrid = getenv("FR_AGG_GRID") ? atoi(getenv("FR_AGG_GRID")) : 1024;
-    hipLaunchKernelGGL(log_reduce_kernel, dim3(rgrid), dim3(256), 0, s, t, st, sorted, g, file_tag, ord0, ablate);
+    hipLaunchKernelGGL(log_split_kernel, dim3(LOG_NR * SPLIT_WGS), dim3(256), 0, s, t, st, log, rcap, sub, scap, file_tag,
+                       ord0);
+    hipLaunchKernelGGL(log_reduce_kernel, dim3(LOG_NSUB), dim3(256), 0, s, t, st, sub, scap, file_tag, ord0, ablate);
     return hipGetLastError();  // log_reduce_kernel's last block emptied the log
 }
 
@@ -2413,13 +2451,162 @@ __device__ __forceinline__ void class_pair_s(W q1, W q2, const u64* __restrict__
     }
 }
 
+// ------------------------------------------------------------------------------------
+// classify neighbourhood maps (fr_internal.h NbrMap): a code is classified by three map probes and
+// two pair probes instead of a scan over every sheet row
+// ------------------------------------------------------------------------------------
+__host__ __device__ inline u64 nbr_binom(int n, int k) {
+    if (k < 0 || k > n) return 0;
+    u64 r = 1;
+    for (int j = 1; j <= k; ++j) r = r * (u64)(n - k + j) / (u64)j;
+    return r;
+}
+
+u64 nbr_codes_per_row(int L, int nsubs) {
+    u64 t = 0, p5 = 1;
+    for (int d = 0; d <= nsubs && d <= L; ++d, p5 *= 5) t += nbr_binom(L, d) * p5;
+    return t;
+}
+
+template <class SL>
+__device__ __forceinline__ SL* nbr_claim(SL* t, u32 mask, u64 key) {  // the table has >= 2x free slots
+    u32 h = (u32)mix64(key) & mask;
+    for (;;) {
+        const u64 prev = atomicCAS((unsigned long long*)&t[h].key, 0ull, (unsigned long long)key);
+        if (prev == 0 || prev == key) return &t[h];
+        h = (h + 1) & mask;
+    }
+}
+
+// thread per (row, neighbour index t): t ranks (d, combination of d positions, d symbols in 1..5);
+// substitutions equal to the row's own symbol are left to the smaller d that produces the same code
+__global__ void nbr_insert_kernel(const u64* __restrict__ vals, const int32_t* __restrict__ canon, int S, int L,
+                                  int nsubs, u64 T, NSlot* m, u32 mask) {
+    const u64 g = blockIdx.x * (u64)blockDim.x + threadIdx.x;
+    if (g >= (u64)S * T) return;
+    const int i = (int)(g / T);
+    u64 t = g % T;
+    if (canon[i] != i) return;  // one insertion per distinct value
+    int d = 0;
+    u64 p5 = 1;
+    for (;; ++d, p5 *= 5) {
+        const u64 nd = nbr_binom(L, d) * p5;
+        if (t < nd) break;
+        t -= nd;
+    }
+    u64 sub = t % p5, comb = t / p5;
+    u64 v = vals[i];
+    for (int k = d; k >= 1; --k) {  // colex unranking of the position set
+        int c = k - 1;
+        while (nbr_binom(c + 1, k) <= comb) ++c;
+        comb -= nbr_binom(c, k);
+        const u64 sy = sub % 5u + 1u;
+        sub /= 5u;
+        if (((v >> (3 * c)) & 7u) == sy) return;
+        v = (v & ~(7ull << (3 * c))) | (sy << (3 * c));
+    }
+    NSlot* e = nbr_claim(m, mask, v | NBR_KEY);
+    atomicMax(&e->vmin_c, ~(u32)i);
+    atomicMax(&e->vmax1, (u32)i + 1u);
+}
+
+__global__ void nbr_pair_kernel(const int32_t* __restrict__ canon, int S, int rc, PSlot* p0, u32 m0, PSlot* p1,
+                                u32 m1) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= S) return;
+    const u64 a = (u64)(u32)canon[i] << 32;
+    PSlot* e = nbr_claim(p0, m0, a | (u32)canon[S + i] | NBR_KEY);
+    atomicAdd(&e->cnt, 1u);
+    atomicMax(&e->first_c, ~(u32)i);
+    if (rc) {
+        e = nbr_claim(p1, m1, a | (u32)canon[2 * S + i] | NBR_KEY);
+        atomicAdd(&e->cnt, 1u);
+        atomicMax(&e->first_c, ~(u32)i);
+    }
+}
+
+hipError_t launch_nbr_build(const SheetArgs& sh, const int32_t* canon, int nsubs, int rc, const NbrMap& nm,
+                            hipStream_t s) {
+    const u64* vals[3] = {sh.i1, sh.i2, sh.i2rc};
+    const int len[3] = {sh.L1u, sh.L2u, sh.L2u};
+    for (int l = 0; l < (rc ? 3 : 2); ++l) {
+        const u64 T = nbr_codes_per_row(len[l], nsubs);
+        const u64 n = (u64)sh.S * T;
+        hipLaunchKernelGGL(nbr_insert_kernel, dim3((u32)((n + 255) / 256)), dim3(256), 0, s, vals[l], canon + l * sh.S,
+                           sh.S, len[l], nsubs, T, nm.m[l], nm.mmask[l]);
+    }
+    hipLaunchKernelGGL(nbr_pair_kernel, dim3((u32)((sh.S + 255) / 256)), dim3(256), 0, s, canon, sh.S, rc, nm.p[0],
+                       nm.pmask[0], nm.p[1], nm.pmask[1]);
+    return hipGetLastError();
+}
+
+__device__ __forceinline__ int nbr_find(const NSlot* __restrict__ t, u32 mask, u64 q) {  // -1 none, -2 several
+    const u64 key = q | NBR_KEY;
+    u32 h = (u32)mix64(key) & mask;
+    for (;;) {
+        const NSlot e = t[h];
+        if (e.key == key) return ~e.vmin_c == e.vmax1 - 1u ? (int)~e.vmin_c : -2;
+        if (e.key == 0) return -1;
+        h = (h + 1) & mask;
+    }
+}
+
+__device__ __forceinline__ void pair_find(const PSlot* __restrict__ t, u32 mask, int v1, int v2, int& both, int& r) {
+    both = 0;
+    r = -1;
+    if (v1 < 0 || v2 < 0) return;
+    const u64 key = ((u64)(u32)v1 << 32) | (u32)v2 | NBR_KEY;
+    u32 h = (u32)mix64(key) & mask;
+    for (;;) {
+        const PSlot e = t[h];
+        if (e.key == key) {
+            both = (int)e.cnt;
+            r = (int)~e.first_c;
+            return;
+        }
+        if (e.key == 0) return;
+        h = (h + 1) & mask;
+    }
+}
+
+// class_pair's result from the map probes: the rows near q1 are exactly the rows holding value a1 (a
+// single distinct value), so its first row is a1 and |M1 ∩ M2| is the pair count of (a1, a2)
+__device__ __forceinline__ void class_pair_nbr(const NbrMap& nm, int a1, int a2, int a3, int& m1, int& m2, int& cls,
+                                               int& row, int& rm2, int& rcls, int& rrow) {
+    int both, r, rboth, rr;
+    pair_find(nm.p[0], nm.pmask[0], a1, a2, both, r);
+    pair_find(nm.p[1], nm.pmask[1], a1, a3, rboth, rr);
+    m1 = a1;
+    m2 = a2;
+    rm2 = a3;
+    if (m1 >= 0 && m2 >= 0) {
+        cls = both == 0 ? CLS_HOP : both == 1 ? CLS_DEMUX : CLS_AMBIG;
+        row = both == 1 ? r : -1;
+    } else {
+        cls = CLS_UNDET;
+        row = -1;
+    }
+    if (m1 >= 0 && rm2 >= 0) {
+        rcls = rboth == 0 ? CLS_HOP : rboth == 1 ? CLS_DEMUX : CLS_AMBIG;
+        rrow = rboth == 1 ? rr : -1;
+    } else {
+        rcls = CLS_UNDET;
+        rm2 = -1;
+        rrow = -1;
+    }
+    if (cls == CLS_UNDET) {
+        m1 = -1;
+        m2 = -1;
+    }
+}
+
 // One lane per unique code.  The sheet images (u32 when every entry has <= 10 symbols, else
 // u64) and the per-name rc sums live in dynamic LDS sized to the sheet; sheets too large for it
 // are read from HBM.
 template <typename W>
 __global__ __launch_bounds__(CLS_WG) void classify_kernel(const u64* keys, const u64* counts, u64 n, SheetArgs sh,
-                                                          int nsubs, int rc, ClassOut o, int sheet_in_lds,
-                                                          int names_in_lds) {
+                                                          int nsubs, int rc, ClassOut o, NbrMap nm,
+                                                          int sheet_in_lds, int names_in_lds) {
     extern __shared__ __attribute__((aligned(16))) u8 cls_lds[];
     unsigned long long* lf = (unsigned long long*)cls_lds;
     unsigned long long* lr = lf + (names_in_lds ? sh.n_names : 0);
@@ -2499,7 +2686,15 @@ __global__ __launch_bounds__(CLS_WG) void classify_kernel(const u64* keys, const
             if (sh.S > 0 && (sh.L1u == -2 || sh.L1u != n1)) err = 1;
             else if (sh.S > 0 && (sh.L2u == -2 || sh.L2u != n2)) err = 2;
             else {
-                if (FR_CLS_SCALAR && rc)
+                int a1 = -2, a2 = -2, a3 = -1;
+                if (nm.on) {
+                    a1 = nbr_find(nm.m[0], nm.mmask[0], q1);
+                    a2 = nbr_find(nm.m[1], nm.mmask[1], q2);
+                    if (rc) a3 = nbr_find(nm.m[2], nm.mmask[2], q2);
+                }
+                if (a1 != -2 && a2 != -2 && a3 != -2)
+                    class_pair_nbr(nm, a1, a2, a3, m1, m2, cls, row, rm2, rcls, rrow);
+                else if (FR_CLS_SCALAR && rc)
                     class_pair_s<W, true>((W)q1, (W)q2, sh.i1, sh.i2, sh.i2rc, sh.S, nsubs, m1, m2, cls, row, rm2,
                                           rcls, rrow);
                 else if (FR_CLS_SCALAR)
@@ -2553,7 +2748,7 @@ __global__ __launch_bounds__(CLS_WG) void classify_kernel(const u64* keys, const
 }
 
 hipError_t launch_classify(const u64* keys, const u64* counts, u64 n, SheetArgs sh, int nsubs, int rc, ClassOut o,
-                           hipStream_t s) {
+                           const NbrMap& nm, hipStream_t s) {
     if (!n) return hipSuccess;
     const u64 grid = (n + CLS_WG - 1) / CLS_WG;
     // u32 images when every sheet entry (and so every matching query) has <= 10 symbols
@@ -2568,10 +2763,10 @@ hipError_t launch_classify(const u64* keys, const u64* counts, u64 n, SheetArgs 
     const size_t lds = nb + (sheet_in_lds ? sheet_bytes : 0) + 16;
     if (narrow && (sheet_in_lds || FR_CLS_SCALAR))
         hipLaunchKernelGGL(classify_kernel<u32>, dim3((u32)grid), dim3(CLS_WG), lds, s, keys, counts, n, sh, nsubs, rc,
-                           o, sheet_in_lds, names_in_lds);
+                           o, nm, sheet_in_lds, names_in_lds);
     else
         hipLaunchKernelGGL(classify_kernel<u64>, dim3((u32)grid), dim3(CLS_WG), lds, s, keys, counts, n, sh, nsubs, rc,
-                           o, sheet_in_lds, names_in_lds);
+                           o, nm, sheet_in_lds, names_in_lds);
     return hipGetLastError();
 }
 

@@ -345,6 +345,73 @@ def test_classify_random(ctx, lib, nsubs, rc):
         assert r.tolist() == [r_exp[n] for n in names]
 
 
+@pytest.mark.parametrize("nsubs", [0, 1, 2, 3])
+@pytest.mark.parametrize("rc", [False, True])
+def test_classify_neighbourhood_maps(lib, monkeypatch, nsubs, rc):
+    """The map path (a few probes per code) against the row scan (FR_NBR=0) and the oracle on an
+    adversarial 10+10 sheet: values 1 and 2 substitutions apart (codes near several values take the
+    scan), repeated values (combinatorial rows), a lower-case and an 'x' entry, duplicated names."""
+    from frender_amd.host import reverse_complement
+    from frender_amd.scan import _sheet_names
+    from oracle.frender_oracle import classify_code
+    rng = random.Random(100 + nsubs * 2 + rc)
+    base = ["".join(rng.choice("ACGT") for _ in range(10)) for _ in range(40)]
+    near = []
+    for k, v in enumerate(base[:8]):  # neighbours of the first values at distance 1 and 2
+        w = list(v)
+        for p in rng.sample(range(10), 1 + k % 2):
+            w[p] = rng.choice([c for c in "ACGT" if c != w[p]])
+        near.append("".join(w))
+    vals1 = base + near
+    vals2 = ["".join(rng.choice("ACGT") for _ in range(10)) for _ in range(20)]
+    idx1 = [vals1[i % len(vals1)] for i in range(96)]
+    idx2 = [vals2[(i * 7) % len(vals2)] for i in range(96)]  # (idx1, idx2) pairs repeat
+    idx1[10] = idx1[10].lower()
+    idx2[11] = idx2[11][:4] + "x" + idx2[11][5:]
+    ids = [f"s{i % 80}" for i in range(96)]
+    codes = []
+    for _ in range(6000):
+        s = rng.randrange(96)
+        a = list(idx1[s].upper())
+        b = list((idx2[rng.randrange(96)] if rng.random() < 0.3 else idx2[s]).upper())
+        if rng.random() < 0.3:
+            b = list(reverse_complement("".join(b)))
+        for arr in (a, b):
+            for _ in range(rng.randint(0, 4)):
+                arr[rng.randrange(10)] = rng.choice("ACGTN")
+        codes.append("".join(a).replace("X", "A") + "+" + "".join(b).replace("X", "C"))
+    codes = list(dict.fromkeys(codes))
+    data = "".join(f"@r{i} 1:N:0:{c}\n\n+\n\n" for i, c in enumerate(codes)).encode()
+    names, nid = _sheet_names(ids)
+    outs = []
+    for nbr in ("1", "0"):
+        monkeypatch.setenv("FR_NBR", nbr)
+        c = lib.Context(device=0, chunk_bytes=1 << 20, table_slots=1 << 16)
+        try:
+            c.reset()
+            c.begin_file(None)
+            c.feed(data)
+            c.end_file()
+            c.finalize()
+            assert lib.decode_keys(c.unique()[0]) == codes
+            c.set_sheet(idx1, idx2, [reverse_complement(x) for x in idx2], nid, len(names))
+            out = c.classify(nsubs, rc)
+            keep = [k for k in out if rc or not k.startswith("rc_")]  # rc_* are left unwritten without rc
+            outs.append(({k: np.asarray(out[k]).tolist() if hasattr(out[k], "__len__") else out[k] for k in keep},
+                         [x.tolist() for x in c.rc_counts()] if rc else None))
+        finally:
+            c.close()
+    assert outs[0] == outs[1]
+    out = outs[0][0]
+    for j in rng.sample(range(len(codes)), 400):
+        e = classify_code(codes[j], 1, idx1, idx2, ids, nsubs, rc)
+        assert lib.CLASS_NAMES[out["cls"][j]] == e["read_type"], (codes[j], e)
+        assert (ids[out["row"][j]] if out["row"][j] >= 0 else "") == e["sample_name"]
+        if rc:
+            assert lib.CLASS_NAMES[out["rc_cls"][j]] == e["rc_read_type"]
+            assert (ids[out["rc_row"][j]] if out["rc_row"][j] >= 0 else "") == e["rc_sample_name"]
+
+
 @pytest.mark.parametrize("grid,cap,chunk", [(1, 1536, 1 << 24), (4, 0, 1 << 26), (64, 16, 1 << 26), (512, 1536, 1 << 30)])
 def test_many_tiles_per_workgroup(lib, monkeypatch, grid, cap, chunk):
     """Few workgroups walking many tiles each (look-back windows sliding past 64 tiles),
@@ -519,11 +586,14 @@ def test_scan_then_demux_96_samples(tmp_path, monkeypatch):
 # multi-GPU product path: `scan --gpus 2` rehearsed on this box's GPU (2 ranks, gloo)
 # ---------------------------------------------------------------------------------------
 @pytest.mark.parametrize("name", ["s96_n1_4files", "s96_n1_rc", "two_files_order", "sample_limit",
-                                  "demux_ok_samples", "same_file_twice", "wide_codes_12", "no_space_header"])
+                                  "demux_ok_samples", "same_file_twice", "wide_codes_12", "no_space_header",
+                                  # one file: every rank tallies a record-aligned part of it
+                                  "comb96_n1_rc", "cfg1_10k_s4_n0", "cr_only", "mixed_newlines", "multi_member_gz",
+                                  "bad_utf8", "gz_truncated", "s96_r150_n1"])
 def test_cli_two_ranks_match_golden(name, tmp_path):
-    """`python -m frender_amd scan --gpus 2` (files sharded over two ranks, tables merged on rank 0)
-    writes the reference's CSV bytes and per-file lines (frender.py:189-205 merge), and raises the
-    first file's error as one GPU would."""
+    """`python -m frender_amd scan --gpus 2` (files sharded over two ranks, or one file's record-aligned
+    parts, tables key-partitioned over the ranks) writes the reference's CSV bytes and per-file lines
+    (frender.py:189-205 merge), and raises the first file's error as one GPU would."""
     import os
     import re
     import subprocess

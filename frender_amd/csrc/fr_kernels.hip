@@ -1853,7 +1853,7 @@ __device__ __forceinline__ u32 insert_rows(const Table& T, DevState* st, const u
 constexpr int SPLIT_PER = 8;
 constexpr int SPLIT_TILE = SPLIT_PER * 256;
 #ifndef FR_SPLIT_WGS
-#define FR_SPLIT_WGS 32
+#define FR_SPLIT_WGS 64
 #endif
 constexpr int SPLIT_WGS = FR_SPLIT_WGS;
 __global__ __launch_bounds__(256) void log_split_kernel(Table t, DevState* st, const LogEntry* log, u32 rcap,

@@ -96,7 +96,10 @@ def _multi(world, files, sheet, flags, tmp):
 
 def _norm(out: str) -> str:
     """The affected-files lines come from a set (frender.py:636-638): their order follows string
-    hashing, which differs per process (PYTHONHASHSEED), in the reference too.  Sort that block."""
+    hashing, which differs per process (PYTHONHASHSEED), in the reference too.  Sort that block.  The
+    output names carry the minute of the run (frender.py's strftime): runs may straddle a minute."""
+    import re
+    out = re.sub(r"\d{4}-\d{2}-\d{2}_\d{4}_UTC", "<time>", out)
     lines = out.split("\n")
     if "Incorrectly demultiplexed barcodes found! Affected files:" in lines:
         i = lines.index("Incorrectly demultiplexed barcodes found! Affected files:") + 1

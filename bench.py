@@ -209,6 +209,7 @@ def main():
     ctx.synth_device(buf, rank * n, n, args.read_len, 1, sheet.idx1, sheet.idx2)
     names, nid = _sheet_names(sheet.ids)
     merge_cbs = device_callbacks(ctx)
+    wire = "cpu" if args.dist_backend == "gloo" else "cuda"  # where small collectives' tensors live
     idx2rc = [reverse_complement(x) for x in sheet.idx2]
 
     tally_timing = []
@@ -235,7 +236,7 @@ def main():
             if args.rc:
                 f, r = ctx.rc_counts()
                 if world > 1 and args.merge == "a2a":  # per-name sums over all partitions
-                    f, r = reduce_sum(dist, "cuda", list(f)), reduce_sum(dist, "cuda", list(r))
+                    f, r = reduce_sum(dist, wire, list(f)), reduce_sum(dist, wire, list(r))
                 use = [int(a) < int(b) for a, b in zip(f, r)]
                 idx2b = [reverse_complement(x) if use[nid[i]] else x for i, x in enumerate(sheet.idx2)]
                 ctx.set_sheet(sheet.idx1, idx2b, [reverse_complement(x) for x in idx2b], nid, len(names))
@@ -277,7 +278,7 @@ def main():
 
     csum = table_checksum(ctx, U) if (world == 1 or args.merge == "a2a" or rank == 0) else 0
     if world > 1 and args.merge == "a2a":  # report the merged table's size (sum of the partitions)
-        U, csum = reduce_sum(dist, "cuda", [U, csum])
+        U, csum = (int(x) for x in reduce_sum(dist, wire, [U, csum]))
     csum &= (1 << 64) - 1
     if rank == 0:
         cpu = None if (args.no_cpu or world > 1) else cpu_baseline(args, ctx, sheet, reclen)  # N=1 only

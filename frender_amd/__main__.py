@@ -44,6 +44,8 @@ def main(argv=None):
                    help="reject a results file in scan's own column order, as frender.py does (default: accept it)")
     d.add_argument("--gz-level", type=int, default=9,
                    help="gzip level of the outputs (the reference writes gzip.open's default, 9)")
+    d.add_argument("--gpus", type=int, default=1,
+                   help="GPUs (one process each; file pairs are dealt to them, rank 0 writes the outputs)")
     d.add_argument("files", nargs="+", help="Fastq file, list of fastq files, or directory path")
     d.set_defaults(cmd="demux")
     args = parser.parse_args(argv)
@@ -56,6 +58,14 @@ def main(argv=None):
         frender_scan(args)
         return 0
     if getattr(args, "cmd", None) == "demux":
+        if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+            # every rank must use the same output directory: the default names the minute
+            child = (sys.argv[1:] if argv is None else list(argv))
+            if "-d" not in child:
+                child = child + ["-d", args.d]
+            return launch_ranks(args.gpus, child)
+        if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+            return run_rank(args)
         from .demux import frender_demux
         frender_demux(args)
         return 0
@@ -64,7 +74,7 @@ def main(argv=None):
 
 
 def launch_ranks(n: int, argv: list) -> int:
-    """`scan --gpus N`: one child process per GPU (this process never touches a GPU), joined by
+    """`scan|demux --gpus N`: one child process per GPU (this process never touches a GPU), joined by
     torch.distributed over 127.0.0.1; rank 0's stdout is the command's.  A rank that fails ends the
     others; the exit status is rank 0's, or the first failure's."""
     import socket
@@ -98,8 +108,9 @@ def launch_ranks(n: int, argv: list) -> int:
 
 
 def run_rank(args) -> int:
-    """One rank of a multi-GPU scan (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* from the launcher or
-    torchrun): RCCL between GPUs (FRENDER_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs)."""
+    """One rank of a multi-GPU scan or demux (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* from the
+    launcher or torchrun): RCCL between GPUs (FRENDER_DIST_BACKEND=gloo rehearses N ranks on fewer
+    GPUs)."""
     import torch
     import torch.distributed as dist
 
@@ -112,8 +123,12 @@ def run_rank(args) -> int:
         dist.init_process_group(backend)
     from .dist import PeerFailed
     try:
-        from .scan import frender_scan
-        frender_scan(args)
+        if args.cmd == "demux":
+            from .demux import frender_demux
+            frender_demux(args)
+        else:
+            from .scan import frender_scan
+            frender_scan(args)
     except PeerFailed:  # rank 0 raises the reference's exception; this rank just fails
         return 1
     finally:

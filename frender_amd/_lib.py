@@ -102,6 +102,7 @@ _SIGS = {
     # native inflate (row f-2)
     "fr_gz_open": (P, [C.POINTER(C.c_char_p), C.c_int, C.c_int]),
     "fr_gz_feed": (C.c_int, [P, C.c_int, P]),
+    "fr_gz_next": (C.c_int, [P, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]),
     "fr_gz_feed_part": (C.c_int, [P, C.c_int, P, C.c_int64, C.c_int, C.c_int, C.c_uint64, C.POINTER(C.c_uint64)]),
     "fr_gz_size_hint": (C.c_uint64, [C.c_char_p]),
     "fr_gz_part_bounds": (C.c_int, [C.c_char_p, C.c_int, C.c_uint64, C.POINTER(C.c_uint64)]),
@@ -252,6 +253,20 @@ class GzPool:
         if rc not in (FR_OK, FR_SAMPLE_DONE):
             raise FrenderError(f"fr_gz_feed failed ({rc}): {lib.fr_gz_error(self.h).decode(errors='replace')}")
         return rc == FR_SAMPLE_DONE
+
+    def blocks(self, i: int):
+        """File i's decoded bytes, block by block (fr_gz_next; each block copied out before the next
+        call).  GzError when the file is not a valid gzip stream."""
+        ptr, n = C.c_void_p(), C.c_uint64()
+        while True:
+            rc = lib.fr_gz_next(self.h, i, C.byref(ptr), C.byref(n))
+            if rc == FR_ERR_IO:
+                raise GzError(lib.fr_gz_error(self.h).decode(errors="replace"))
+            if rc != FR_OK:
+                raise FrenderError(f"fr_gz_next failed ({rc}): {lib.fr_gz_error(self.h).decode(errors='replace')}")
+            if not n.value:
+                return
+            yield C.string_at(ptr, n.value)
 
     def _feed_part(self, i: int, ctx_handle, file_index: int, part: int, nparts: int, hint: int) -> int:
         base = C.c_uint64(0)

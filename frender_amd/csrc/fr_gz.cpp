@@ -67,6 +67,7 @@ struct fr_gz {
     std::condition_variable cv;
     std::vector<std::thread> workers;
     std::vector<std::vector<uint8_t>> spare;  // consumed blocks for reuse (no page faults per block)
+    std::vector<uint8_t> held;                // the block fr_gz_next handed out last
     int next = 0;     // next file a worker starts
     int consume = 0;  // file the consumer reads (workers stay within [consume, consume + threads))
     bool stop = false;
@@ -499,6 +500,38 @@ int fr_gz_feed(fr_gz* g, int i, fr_ctx* ctx) {
             return rc;
         }
     }
+}
+
+int fr_gz_next(fr_gz* g, int i, const uint8_t** data, uint64_t* len) {
+    *data = nullptr;
+    *len = 0;
+    if (i < 0 || i >= (int)g->files.size()) {
+        g->err = "fr_gz_next: no such file";
+        return FR_ERR_INVALID;
+    }
+    GzFile& f = g->files[i];
+    std::unique_lock<std::mutex> lk(g->m);
+    if (g->held.capacity()) {  // the block handed out last is the caller's no longer
+        if (g->spare.size() < (size_t)g->threads * g->depth) g->spare.push_back(std::move(g->held));
+        g->held = std::vector<uint8_t>();
+    }
+    // readers of several files at once (demux: R1 and R2 in lockstep) keep the furthest one
+    g->consume = std::max(g->consume, i);
+    g->cv.notify_all();
+    g->cv.wait(lk, [&] { return !f.q.empty() || f.done; });
+    if (f.q.empty()) {  // done
+        if (!f.err.empty()) {
+            g->err = f.path + ": " + f.err;
+            return FR_ERR_IO;
+        }
+        return FR_OK;
+    }
+    g->held = std::move(f.q.front());
+    f.q.pop_front();
+    g->cv.notify_all();
+    *data = g->held.data();
+    *len = g->held.size();
+    return FR_OK;
 }
 
 // ---- record-aligned parts of one file (multi-GPU scans of fewer files than GPUs) ----------------

@@ -131,13 +131,17 @@ class _GzFile:
         self.f.close()
 
 
-def open_files(name, out_dir, infix, level):
-    """frender.py:667-676."""
+def out_path(name, out_dir, infix, read) -> str:
+    """frender.py:667-676's file name of one writer."""
     if not out_dir.endswith("/"):
         out_dir += "/"
+    return f"{out_dir}{name}_frender-demux_{infix + '_' if infix else ''}{read}.fq.gz"
+
+
+def open_files(name, out_dir, infix, level):
+    """frender.py:667-676."""
     kind = _GzMembers if _LD is not None and os.environ.get("FR_DEMUX_ZLIB", "0") == "0" else _GzFile
-    return {read: kind(f"{out_dir}{name}_frender-demux_{infix + '_' if infix else ''}{read}.fq.gz", level)
-            for read in ("R1", "R2")}
+    return {read: kind(out_path(name, out_dir, infix, read), level) for read in ("R1", "R2")}
 
 
 _MATE_TAG = re.compile("_R([12])_")
@@ -167,36 +171,51 @@ def get_paired_files(files_list) -> list:
     return pairs
 
 
-def text_chunks(path, chunk=64 << 20):
+def _replay_gz_error(path):
+    """Error path only: the native inflate rejected the file.  The reference's text-mode reader
+    (frender.py:776-777) raises on it as Python's gzip does: re-read it that way to raise the same."""
+    with gzip.open(path, "rt") as f:
+        for _ in f:
+            pass
+
+
+def text_chunks(path, pool=None, index=0):
     """Decoded bytes of a .gz file as the reference's text-mode reader sees them (frender.py:776),
-    streamed: strict UTF-8 (UnicodeDecodeError otherwise, sequences may straddle chunks) and
-    universal newlines folded to '\n' (a '\r' ending a chunk waits for the next one)."""
+    streamed from the native inflate pool (fr_gz_next; a one-file pool when none is given): strict
+    UTF-8 (UnicodeDecodeError otherwise, sequences may straddle blocks) and universal newlines folded
+    to '\n' (a '\r' ending a block waits for the next one)."""
     import codecs
 
-    from .scan import _GzReader
-
-    rd = _GzReader(path, chunk)
+    own = pool is None
+    if own:
+        pool = _lib.GzPool([path], threads=1)
+        index = 0
     dec = None
     hold = b""
     try:
-        for raw in rd:
-            data = hold + raw
-            hold = b""
-            if data.endswith(b"\r"):
-                hold, data = b"\r", data[:-1]
-            if np.frombuffer(data, dtype=np.uint8).max(initial=0) >= 0x80 or dec is not None:
-                dec = dec or codecs.getincrementaldecoder("utf-8")()
-                dec.decode(data)  # raises like gzip.open(..., "rt")
-            if b"\r" in data:
-                data = data.replace(b"\r\n", b"\n").replace(b"\r", b"\n")
-            if data:
-                yield data
+        try:
+            for raw in pool.blocks(index):
+                data = hold + raw
+                hold = b""
+                if data.endswith(b"\r"):
+                    hold, data = b"\r", data[:-1]
+                if dec is not None or not data.isascii():
+                    dec = dec or codecs.getincrementaldecoder("utf-8")()
+                    dec.decode(data)  # raises like gzip.open(..., "rt")
+                if b"\r" in data:
+                    data = data.replace(b"\r\n", b"\n").replace(b"\r", b"\n")
+                if data:
+                    yield data
+        except _lib.GzError as e:
+            _replay_gz_error(path)
+            raise RuntimeError(f"native inflate rejected {path} but Python's gzip reads it: {e}") from e
         if dec is not None:
             dec.decode(b"", final=True)
         if hold:
             yield b"\n"
     finally:
-        rd.close()
+        if own:
+            pool.close()
 
 
 def read_text(path) -> bytes:
@@ -209,11 +228,12 @@ def _line_at(data: bytes, start: int) -> bytes:
     return data[start:] if e < 0 else data[start:e]
 
 
-def _demux_pair(dmx, pool, read1_file, read2_file, results, route_of, writers, window):
+def _demux_pair(dmx, pool, gz, i1, i2, read1_file, read2_file, results, route_of, writers, window):
     """One R1/R2 pair in record-aligned windows: the GPU indexes both windows, the complete
     record pairs are routed, and the bytes after the last routed record carry into the next
-    window.  Pairing stops when either mate runs out of records (zip, frender.py:777)."""
-    streams = [text_chunks(read1_file), text_chunks(read2_file)]
+    window.  Pairing stops when either mate runs out of records (zip, frender.py:777).  The mates
+    inflate on the native pool gz (files i1, i2)."""
+    streams = [text_chunks(read1_file, gz, i1), text_chunks(read2_file, gz, i2)]
     bufs = [b"", b""]
     eof = [False, False]
     pending = []  # the previous window's gzip jobs: overlap with this window's inflate and GPU work
@@ -296,19 +316,26 @@ def frender_demux(args, dev=None) -> None:
     infix = args.o
     undeter_name = f"Undetermined{'-ambiguous' if ambiguous else ''}{'-index-hop' if index_hop else ''}"
 
+    from .dist import world_group
+    group = None if dev is not None else world_group()  # demux --gpus N: one rank of N
+    lead = group is None or group.get_rank() == 0
+
     result_file = Path(args.r)
     if not Path.is_file(result_file):
         raise SystemExit(f"File {result_file} not found")
     results = parse_results_file(result_file, strict=getattr(args, "strict_header", False))
     ids = sorted({sid for _, sid in results.values()} - {""})
-    if (not ids) & samples:
+    if (not ids) & samples and lead:
         print("Warning: no demuxable sample ids found in the supplied frender result file!")
 
-    os.mkdir(args.d)
-    writers = []  # destination id -> writer pair
+    if group is None:
+        os.mkdir(args.d)
+    else:
+        _mkdir_everywhere(group, args.d)
+    writers = []  # destination id -> writer pair (N ranks: its name; rank 0 writes the files at the end)
 
     def new_writers(name):
-        writers.append(open_files(name, args.d, infix, level))
+        writers.append(open_files(name, args.d, infix, level) if group is None else name)
         return len(writers) - 1
 
     sample_dest = {sid: new_writers(sid) for sid in ids} if samples else None
@@ -345,17 +372,120 @@ def frender_demux(args, dev=None) -> None:
     pairs = get_paired_files(parse_files(spec, just_r1=False))
 
     window = int(getattr(args, "window", None) or (512 << 20))  # decoded bytes per mate per GPU pass
-    dmx = dev or _lib.Demux(int(os.environ.get("LOCAL_RANK", "0")))
+    if group is not None:
+        return _demux_ranks(group, args, dev, pairs, results, route_of, keys[fast], vals[fast], writers, window, level,
+                            infix)
+    dmx = dev or _lib.Demux(_device_index(None))
     pool = ThreadPoolExecutor(max_workers=max(2, min(32, len(writers) * 2)))
+    gz = _lib.GzPool([str(f) for pr in pairs for f in pr], threads=4)
     try:
         dmx.set_table(keys[fast], vals[fast])
-        for read1_file, read2_file in pairs:
+        for k, (read1_file, read2_file) in enumerate(pairs):
             print(f"Demultiplexing {read1_file.name}...")
-            _demux_pair(dmx, pool, read1_file, read2_file, results, route_of, writers, window)
+            _demux_pair(dmx, pool, gz, 2 * k, 2 * k + 1, read1_file, read2_file, results, route_of, writers, window)
     finally:
+        gz.close()
         pool.shutdown(wait=True)
         for w in writers:
             for f in w.values():
                 f.close()
         if dev is None:
             dmx.close()
+
+
+# ---- demux --gpus N ------------------------------------------------------------------------------
+# The reference demultiplexes its file pairs one after another into one writer pair per destination
+# (frender.py:776-814).  Here rank r of N takes pairs r, r + N, ... (whole pairs: both mates of a pair
+# must be read in lockstep), writes each pair's destinations into part files of its own, and rank 0
+# concatenates the parts in pair order into the final files.  The writers emit gzip members, so a
+# concatenation is a valid gzip stream whose text is the concatenation of the pairs' texts: the
+# reference's file content.  The first failing pair (in pair order) decides the error, raised by the
+# rank that met it, after rank 0 has written the pairs up to it.
+
+def _device_index(group) -> int:
+    """This rank's GPU: LOCAL_RANK, folded onto the visible GPUs for gloo rehearsals on one GPU."""
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if group is not None and group.get_backend() == "gloo":
+        import torch
+        local %= max(torch.cuda.device_count(), 1)
+    return local
+
+
+def _wire(group):
+    return "cpu" if group.get_backend() == "gloo" else f"cuda:{_device_index(group)}"
+
+
+def _mkdir_everywhere(group, path):
+    """Rank 0 creates the output directory (FileExistsError as the reference raises it); every rank
+    learns the outcome before anyone writes."""
+    from .dist import PeerFailed, reduce_max
+    err = None
+    if group.get_rank() == 0:
+        try:
+            os.mkdir(path)
+        except OSError as e:
+            err = e
+    if int(reduce_max(group, _wire(group), [1 if err is not None else 0])[0]):
+        if err is not None:
+            raise err
+        raise PeerFailed()
+
+
+def _demux_ranks(group, args, dev, pairs, results, route_of, keys, vals, names, window, level, infix):
+    import shutil
+
+    from .dist import PeerFailed, reduce_min
+    rank, world = group.get_rank(), group.get_world_size()
+    parts = os.path.join(args.d, ".frender-parts")
+    mine = list(range(rank, len(pairs), world))
+    gz = _lib.GzPool([str(f) for k in mine for f in pairs[k]], threads=4)
+    dmx = _lib.Demux(_device_index(group))
+    pool = ThreadPoolExecutor(max_workers=max(2, min(32, len(names) * 2)))
+    failed, exc = len(pairs), None
+    try:
+        dmx.set_table(keys, vals)
+        for j, k in enumerate(mine):
+            d = os.path.join(parts, str(k))
+            os.makedirs(d, exist_ok=True)
+            writers = [open_files(n, d, infix, level) for n in names]
+            try:
+                _demux_pair(dmx, pool, gz, 2 * j, 2 * j + 1, pairs[k][0], pairs[k][1], results, route_of, writers,
+                            window)
+            except (Exception, SystemExit) as e:  # re-raised below if it is the first in pair order
+                failed, exc = k, e
+            finally:
+                for w in writers:
+                    for f in w.values():
+                        f.close()
+            if exc is not None:
+                break
+    except (Exception, SystemExit) as e:  # before any pair (the device, the table): this rank's first pair
+        if exc is None:
+            failed, exc = (mine[0] if mine else len(pairs)), e
+    finally:
+        pool.shutdown(wait=True)
+        gz.close()
+        dmx.close()
+    first = int(reduce_min(group, _wire(group), [failed])[0])  # every rank's pairs are done here
+    last = min(first, len(pairs) - 1)
+    if rank == 0:
+        for k in range(last + 1):
+            print(f"Demultiplexing {pairs[k][0].name}...")
+        for n in names:
+            for read in ("R1", "R2"):
+                final = out_path(n, args.d, infix, read)
+                with open(final, "wb") as out:
+                    for k in range(last + 1):
+                        part = out_path(n, os.path.join(parts, str(k)), infix, read)
+                        if os.path.exists(part):
+                            with open(part, "rb") as f:
+                                shutil.copyfileobj(f, out, 16 << 20)
+                    if out.tell() == 0:  # no pair reached it: an empty gzip file, as the reference's writer
+                        out.write(gzip.compress(b"", compresslevel=level))
+    reduce_min(group, _wire(group), [0])  # the parts are read: remove them
+    if rank == 0:
+        shutil.rmtree(parts, ignore_errors=True)
+    if first < len(pairs):
+        if failed == first:
+            raise exc
+        raise PeerFailed()

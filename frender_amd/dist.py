@@ -111,56 +111,6 @@ def owner_of(keys, world: int):
     return ((keys * _MULT) >> 40).bitwise_and(0xFFFFFF).remainder(world)
 
 
-def partition_exchange(dist, device, rows):
-    """rows: [U, 3] int64 (key, count, first) on `device`.  Returns the rows this rank owns,
-    gathered from every rank ([R, 3], same device; order: by source rank, then local order)."""
-    import torch
-
-    world = dist.get_world_size()
-    wire = "cpu" if dist.get_backend() == "gloo" else device
-    dest = owner_of(rows[:, 0], world) if rows.shape[0] else torch.zeros(0, dtype=torch.int64, device=rows.device)
-    order = torch.argsort(dest, stable=True)
-    send = rows[order].contiguous().to(wire)
-    scount = torch.bincount(dest, minlength=world).to(torch.int64).to(wire)
-    rcount = torch.empty_like(scount)
-    dist.all_to_all_single(rcount, scount)
-    sc, rc = scount.tolist(), rcount.tolist()
-    recv = torch.empty((sum(rc), 3), dtype=torch.int64, device=wire)
-    dist.all_to_all_single(recv.view(-1), send.view(-1), [3 * c for c in rc], [3 * c for c in sc])
-    return recv.to(device)
-
-
-def reduce_sum(dist, device, values):
-    """All-reduce (sum) of a small int64 vector, e.g. the -rc per-name counts."""
-    import torch
-
-    wire = "cpu" if dist.get_backend() == "gloo" else device
-    t = torch.as_tensor(values, dtype=torch.int64).to(wire)
-    dist.all_reduce(t)
-    return t.cpu().tolist()
-
-
-def partition_merge_device(dist, device, ctx):
-    """The hash-partitioned merge on the HIP library: export this rank's finalized table,
-    exchange, rebuild the table from the rows this rank owns, and finalize it.  Returns the
-    size of this rank's partition of the merged table."""
-    import torch
-
-    U = int(ctx.U)
-    rows = torch.empty((3, max(U, 1)), dtype=torch.int64, device=device)
-    if U:
-        ctx.export_unique_device(rows[0].data_ptr(), rows[1].data_ptr(), rows[2].data_ptr(), U)
-    mine = partition_exchange(dist, device, rows[:, :U].t())
-    cols = mine.t().contiguous()
-    torch.cuda.current_stream().synchronize()  # the exchange landed on torch's stream
-    ctx.reset()
-    if cols.shape[1]:
-        ctx.merge_unique_device(cols[0].data_ptr(), cols[1].data_ptr(), cols[2].data_ptr(), int(cols.shape[1]))
-    n, _, _ = ctx.finalize()
-    ctx.sync()
-    return int(n)
-
-
 # ---- collectives on int64 / uint8 tensors (RCCL device buffers, or host tensors over gloo) -----
 
 def wire_of(dist, ctx):

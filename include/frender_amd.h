@@ -122,6 +122,11 @@ int fr_feed(fr_ctx* ctx, const uint8_t* data, uint64_t len);
 typedef struct fr_gz fr_gz;
 fr_gz* fr_gz_open(const char* const* paths, int n_files, int threads);
 int fr_gz_feed(fr_gz* g, int i, fr_ctx* ctx);
+/* The consumer-side alternative to fr_gz_feed (demux reads R1 and R2 in lockstep): the next decoded
+ * block of file i.  *data / *len stay valid until the next fr_gz_next or fr_gz_close on the pool;
+ * *len == 0 at the file's end.  FR_ERR_IO: not a valid gzip stream (fr_gz_error).  Replaces the
+ * reference's gzip.open(read_file, "rt") iteration in frender_demux (frender.py:776-777). */
+int fr_gz_next(fr_gz* g, int i, const uint8_t** data, uint64_t* len);
 /* Record shards of one file (multi-GPU scans of fewer files than GPUs; SURVEY §8(e) "host cuts
  * record-aligned chunks and deals them to GPUs"): part `part` of `nparts` of file i's decoded
  * stream is [b_part, b_part+1), b_0 = 0, b_nparts = the end, and for 0 < j < nparts b_j = the first

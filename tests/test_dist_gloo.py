@@ -77,26 +77,26 @@ def test_tree_merge_gloo(world, seed):
 
 
 def _worker_a2a(rank, world, port, seed, out):
-    from frender_amd.dist import owner_of, partition_exchange, reduce_sum
+    from frender_amd.dist import exchange, owner_of, reduce_sum
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     table = _table(rank, seed)
     rows = torch.tensor([[k, c, f] for k, (c, f) in sorted(table.items())], dtype=torch.int64).reshape(-1, 3)
-    mine = partition_exchange(dist, "cpu", rows)
+    mine = exchange(dist, "cpu", rows, owner_of(rows[:, 0], world))
     part = {}
     for k, c, f in mine.tolist():
         assert int(owner_of(torch.tensor([k]), world)[0]) == rank  # only codes this rank owns
         c0, f0 = part.get(k, (0, 1 << 62))
         part[k] = (c0 + c, min(f0, f))
-    total = reduce_sum(dist, "cpu", [len(part)])[0]
+    total = int(reduce_sum(dist, "cpu", [len(part)])[0])
     out.put((rank, sorted(part.items()), total))
     dist.barrier()
     dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("world,seed", [(2, 5), (3, 6), (4, 7)])
-def test_partition_exchange_gloo(world, seed):
+def test_partition_exchange_gloo(world, seed):  # dist.exchange, as partition_merge_device uses it
     """The hash-partitioned all-to-all merge: every code lands on exactly one owner and the
     union of the merged partitions equals the merged table (count = sum, first = min)."""
     ctx = mp.get_context("spawn")

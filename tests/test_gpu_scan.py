@@ -481,6 +481,7 @@ def test_merge_unique_device(lib):
 # ---------------------------------------------------------------------------------------
 from demux_harness import case_names as demux_case_names  # noqa: E402
 from demux_harness import run_case as run_demux_case  # noqa: E402
+from demux_harness import run_case_cli as run_demux_case_cli  # noqa: E402
 
 
 @pytest.mark.parametrize("name", demux_case_names())
@@ -488,6 +489,77 @@ def test_demux_golden_on_gpu(name):
     from frender_amd.demux import frender_demux
     diffs = run_demux_case(name, frender_demux)
     assert not diffs, "\n".join(diffs)
+
+
+@pytest.mark.parametrize("name", ["syn96_scan_csv", "syn_basic", "syn_crlf", "hand_lone_cr", "syn_missing_code",
+                                  "syn_bad_type", "syn_no_undet"])
+def test_demux_cli_two_ranks_golden(name):
+    """`demux --gpus 2` (pairs dealt to two ranks, rank 0 concatenating the per-pair gzip parts) on the
+    reference's golden demux cases: the same files' contents, stdout and errors."""
+    diffs = run_demux_case_cli(name, gpus=2)
+    assert not diffs, "\n".join(diffs)
+
+
+@pytest.mark.parametrize("bad_pair", [None, 3])
+def test_demux_cli_ranks_many_pairs(tmp_path, bad_pair):
+    """Seven pairs over three ranks (gloo, one GPU) against the single-rank in-process demux: every
+    writer's content, the stdout lines and, with a code missing from the results in pair 3, the
+    error of the first failing pair in pair order."""
+    import argparse
+    import contextlib
+    import gzip
+    import io
+    import subprocess
+    import sys
+    from frender_amd.demux import frender_demux
+    rng = random.Random(17)
+    codes = ["AAAA+CCCC", "GGGG+TTTT", "AAAA+TTTT", "ACGT+ACGT", "NNNN+CCCC"]
+    kinds = {"AAAA+CCCC": ("demuxable", "S1"), "GGGG+TTTT": ("demuxable", "S2"), "AAAA+TTTT": ("index_hop", ""),
+             "ACGT+ACGT": ("undetermined", ""), "NNNN+CCCC": ("ambiguous", "")}
+    inp = tmp_path / "in"
+    inp.mkdir()
+    files = []
+    for p in range(7):
+        r1, r2 = [], []
+        for i in range(rng.randint(500, 3000)):
+            c = rng.choice(codes) if not (p == bad_pair and i == 100) else "TTTT+TTTT"
+            seq = "".join(rng.choice("ACGT") for _ in range(rng.randint(0, 40)))
+            r1.append(f"@p{p}r{i} 1:N:0:{c}\n{seq}\n+\n{'F' * len(seq)}\n")
+            r2.append(f"@p{p}r{i} 2:N:0:{c}\n{seq[::-1]}\n+\n{'F' * len(seq)}\n")
+        for m, txt in ((1, r1), (2, r2)):
+            fn = inp / f"L{p}_R{m}_001.fastq.gz"
+            with gzip.open(fn, "wb") as f:
+                f.write("".join(txt).encode())
+            files.append(str(fn))
+    with open(inp / "results.csv", "w") as f:
+        f.write("idx1,idx2,reads,matched_idx1,matched_idx2,read_type,sample_name,demux_ok\r\n")
+        for c, (t, s) in kinds.items():
+            a, b = c.split("+")[0:2]
+            f.write(f"{a},{b},1,,,{t},{s},True\r\n")
+    one = tmp_path / "one"
+    buf = io.StringIO()
+    err = None
+    with contextlib.redirect_stdout(buf):
+        try:
+            frender_demux(argparse.Namespace(r=str(inp / "results.csv"), d=str(one), o=None, no_index_hop=False,
+                                             no_ambiguous=False, no_undeter=False, no_samples=False, files=files))
+        except SystemExit as e:
+            err = str(e)
+    many = tmp_path / "many"
+    env = dict(os.environ, FRENDER_DIST_BACKEND="gloo",
+               PYTHONPATH=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    r = subprocess.run([sys.executable, "-m", "frender_amd", "demux", "--gpus", "3", "-r", str(inp / "results.csv"),
+                        "-d", str(many), *files], cwd=str(tmp_path), env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert r.stdout == buf.getvalue()
+    if bad_pair is None:
+        assert r.returncode == 0 and err is None, r.stderr[-2000:]
+    else:
+        assert r.returncode != 0 and err and err in r.stderr, (err, r.stderr[-2000:])
+    assert sorted(os.listdir(many)) == sorted(os.listdir(one))
+    for fn in os.listdir(one):
+        with gzip.open(one / fn, "rb") as a, gzip.open(many / fn, "rb") as b:
+            assert a.read() == b.read(), fn
 
 
 @pytest.mark.parametrize("seed,window", [(1, None), (2, None), (3, 20000), (4, 4096)])

@@ -551,7 +551,7 @@ def test_demux_cli_ranks_many_pairs(tmp_path, bad_pair):
     r = subprocess.run([sys.executable, "-m", "frender_amd", "demux", "--gpus", "3", "-r", str(inp / "results.csv"),
                         "-d", str(many), *files], cwd=str(tmp_path), env=env, capture_output=True, text=True,
                        timeout=240)
-    assert r.stdout == buf.getvalue()
+    assert "".join(ln for ln in r.stdout.splitlines(True) if not ln.startswith("[Gloo]")) == buf.getvalue()
     if bad_pair is None:
         assert r.returncode == 0 and err is None, r.stderr[-2000:]
     else:

@@ -238,8 +238,11 @@ def main():
                 if world > 1 and args.merge == "a2a":  # per-name sums over all partitions
                     f, r = reduce_sum(dist, wire, list(f)), reduce_sum(dist, wire, list(r))
                 use = [int(a) < int(b) for a, b in zip(f, r)]
-                idx2b = [reverse_complement(x) if use[nid[i]] else x for i, x in enumerate(sheet.idx2)]
-                ctx.set_sheet(sheet.idx1, idx2b, [reverse_complement(x) for x in idx2b], nid, len(names))
+                # pass B's idx2 and its reverse complements are selections (rc(rc(x)) = x)
+                pick = [use[nid[i]] for i in range(len(sheet.idx2))]
+                idx2b = [c if u else x for u, x, c in zip(pick, sheet.idx2, idx2rc)]
+                idx2brc = [x if u else c for u, x, c in zip(pick, sheet.idx2, idx2rc)]
+                ctx.set_sheet(sheet.idx1, idx2b, idx2brc, nid, len(names))
                 ctx.classify(args.nsubs, False, to_host=False)
         ctx.sync()
         return U

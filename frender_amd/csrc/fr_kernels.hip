@@ -1940,11 +1940,19 @@ __global__ __launch_bounds__(256) void log_reduce_kernel(Table t, DevState* st, 
     const u32 n = min(st->log_scur[blockIdx.x], scap);
     const LogEntry* part = sub + (u64)blockIdx.x * scap;
     u64 sink = 0;
-    constexpr int LB = 8;  // entries per thread in flight
-    for (u32 i0 = threadIdx.x; i0 < ((ablate & 512u) ? 0u : n); i0 += LB * 256) {  // 512: timing ablation
+    constexpr int LB = 8;  // entries per thread per batch; the next batch's loads fly during this one's fold
+    const u32 nn = (ablate & 512u) ? 0u : n;  // 512: timing ablation
+    LogEntry nx[LB];
+#pragma unroll
+    for (int q = 0; q < LB; ++q) nx[q] = threadIdx.x + q * 256 < nn ? part[threadIdx.x + q * 256] : LogEntry{0, 0, 0};
+    for (u32 i0 = threadIdx.x; i0 < nn; i0 += LB * 256) {
         LogEntry ev[LB];
 #pragma unroll
-        for (int q = 0; q < LB; ++q) ev[q] = i0 + q * 256 < n ? part[i0 + q * 256] : LogEntry{0, 0, 0};
+        for (int q = 0; q < LB; ++q) {
+            ev[q] = nx[q];
+            const u32 j = i0 + LB * 256 + q * 256;
+            nx[q] = j < nn ? part[j] : LogEntry{0, 0, 0};
+        }
 #pragma unroll
         for (int q = 0; q < LB; ++q) {
             const LogEntry e = ev[q];
@@ -1980,12 +1988,15 @@ __global__ __launch_bounds__(256) void log_reduce_kernel(Table t, DevState* st, 
     }
     if (sink == 1) atomicAdd((unsigned long long*)&st->stamp[7], 1ull);  // keeps the ablation's loads
     __syncthreads();
-    for (int i0 = threadIdx.x; i0 < ((ablate & 256u) ? 0 : AGG_LNS); i0 += 4 * 256) {  // 256: timing ablation
-        u64 key[4], ord[4];
-        u32 cnt[4], tag[4];
-        bool v[4];
+    // the distinct codes into the table, FB slots per thread in flight (LDS limits this kernel to two
+    // workgroups per CU, so registers are plentiful)
+    constexpr int FB = 8;
+    for (int i0 = threadIdx.x; i0 < ((ablate & 256u) ? 0 : AGG_LNS); i0 += FB * 256) {  // 256: timing ablation
+        u64 key[FB], ord[FB];
+        u32 cnt[FB], tag[FB];
+        bool v[FB];
 #pragma unroll
-        for (int b = 0; b < 4; ++b) {
+        for (int b = 0; b < FB; ++b) {
             const int i = i0 + b * 256;
             const AggSlot e = i < AGG_LNS ? ls[i] : AggSlot{0, 0, 0};
             v[b] = e.key != 0;
@@ -1994,7 +2005,7 @@ __global__ __launch_bounds__(256) void log_reduce_kernel(Table t, DevState* st, 
             ord[b] = ord0 + e.mino;
             tag[b] = file_tag;
         }
-        made += insert_rows<4, true>(t, st, key, cnt, ord, tag, v);
+        made += insert_rows<FB, true>(t, st, key, cnt, ord, tag, v);
     }
     add_created(st, made);
     // every workgroup has read log_n and its cursor (the split pass read the region cursors before

@@ -239,9 +239,12 @@ def main():
                     f, r = reduce_sum(dist, wire, list(f)), reduce_sum(dist, wire, list(r))
                 use = [int(a) < int(b) for a, b in zip(f, r)]
                 # pass B's idx2 and its reverse complements are selections (rc(rc(x)) = x)
-                pick = [use[nid[i]] for i in range(len(sheet.idx2))]
-                idx2b = [c if u else x for u, x, c in zip(pick, sheet.idx2, idx2rc)]
-                idx2brc = [x if u else c for u, x, c in zip(pick, sheet.idx2, idx2rc)]
+                if any(use):
+                    pick = [use[nid[i]] for i in range(len(sheet.idx2))]
+                    idx2b = [c if u else x for u, x, c in zip(pick, sheet.idx2, idx2rc)]
+                    idx2brc = [x if u else c for u, x, c in zip(pick, sheet.idx2, idx2rc)]
+                else:  # no name takes rc: pass B's lists are pass A's
+                    idx2b, idx2brc = sheet.idx2, idx2rc
                 ctx.set_sheet(sheet.idx1, idx2b, idx2brc, nid, len(names))
                 ctx.classify(args.nsubs, False, to_host=False)
         ctx.sync()

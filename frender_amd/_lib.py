@@ -404,13 +404,18 @@ class Context:
 
     # ---- sheet ----------------------------------------------------------------------
     def set_sheet(self, idx1: list, idx2: list, idx2rc: list, name_id: list, n_names: int):
-        key = (tuple(idx1), tuple(idx2), tuple(idx2rc), tuple(name_id), n_names)
-        packed = self._sheet_cache.get(key)
-        if packed is None:
-            packed = self._pack_sheet(idx1, idx2, idx2rc, name_id)
-            if len(self._sheet_cache) >= 8:
-                self._sheet_cache.clear()
-            self._sheet_cache[key] = packed
+        last = getattr(self, "_sheet_last", None)
+        if last is not None and last[0] == [idx1, idx2, idx2rc, list(name_id), n_names]:
+            packed = last[1]  # the same lists as the last call (compared by value, at C speed): no re-keying
+        else:
+            key = (tuple(idx1), tuple(idx2), tuple(idx2rc), tuple(name_id), n_names)
+            packed = self._sheet_cache.get(key)
+            if packed is None:
+                packed = self._pack_sheet(idx1, idx2, idx2rc, name_id)
+                if len(self._sheet_cache) >= 8:
+                    self._sheet_cache.clear()
+                self._sheet_cache[key] = packed
+        self._sheet_last = ([list(idx1), list(idx2), list(idx2rc), list(name_id), n_names], packed)
         p1, p2, p2rc, len1, len2, nid, cp, stride = packed
         self.cp_stride = stride
         self._sheet_keep = packed

@@ -757,6 +757,18 @@ int fr_set_sheet(fr_ctx* ctx, int S, const uint64_t* idx1_packed, const int32_t*
         std::memcpy(h + o_i2, idx2_packed, S * 8ull);
         std::memcpy(h + o_i2rc, idx2rc_packed, S * 8ull);
         std::memcpy(h + o_name, name_id, S * 4ull);
+    }
+    if (with_cp) {
+        std::memcpy(h + o_cp1, idx1_cp, ncp * 4);
+        std::memcpy(h + o_cp2, idx2_cp, ncp * 4);
+        std::memcpy(h + o_cp2rc, idx2rc_cp, ncp * 4);
+        std::memcpy(h + o_l1, idx1_len, S * 4ull);
+        std::memcpy(h + o_l2, idx2_len, S * 4ull);
+    }
+    // the same sheet again (pass B without rc rows, repeated scans): the device copy is current (the
+    // canonical ids below derive from the lists, so the comparison stops before them)
+    const bool same = ctx->h_sheet && total == ctx->sheet_bytes && std::memcmp(h, ctx->h_sheet, o_canon) == 0;
+    if (!same && S) {
         // value ids of the neighbourhood maps: the first row with the same packed value
         const uint64_t* lists[3] = {idx1_packed, idx2_packed, idx2rc_packed};
         int32_t* canon = (int32_t*)(h + o_canon);
@@ -766,15 +778,6 @@ int fr_set_sheet(fr_ctx* ctx, int S, const uint64_t* idx1_packed, const int32_t*
             for (int i = 0; i < S; ++i) canon[l * S + i] = first.emplace(lists[l][i], i).first->second;
         }
     }
-    if (with_cp) {
-        std::memcpy(h + o_cp1, idx1_cp, ncp * 4);
-        std::memcpy(h + o_cp2, idx2_cp, ncp * 4);
-        std::memcpy(h + o_cp2rc, idx2rc_cp, ncp * 4);
-        std::memcpy(h + o_l1, idx1_len, S * 4ull);
-        std::memcpy(h + o_l2, idx2_len, S * 4ull);
-    }
-    // the same sheet again (pass B without rc rows, repeated scans): the device copy is current
-    const bool same = ctx->h_sheet && total == ctx->sheet_bytes && std::memcmp(h, ctx->h_sheet, total) == 0;
     if (!same) {
         CK(hipStreamSynchronize(ctx->stream));  // the previous sheet may still be in use / in flight
         if (total > ctx->sheet_cap) {

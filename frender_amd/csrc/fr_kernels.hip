@@ -2639,8 +2639,9 @@ __global__ __launch_bounds__(CLS_WG) void classify_kernel(const u64* keys, const
     const W* S2 = sheet_in_lds ? s2 : (const W*)sh.i2;
     const W* S2rc = sheet_in_lds ? s2rc : (const W*)sh.i2rc;
 
-    const u64 u = blockIdx.x * (u64)CLS_WG + threadIdx.x;
-    if (u < n) {
+    // grid-stride: the per-name sums stay in LDS over many codes (one flush per workgroup: the
+    // flush's atomics all land on the same 2 x names addresses)
+    for (u64 u = blockIdx.x * (u64)CLS_WG + threadIdx.x; u < n; u += (u64)gridDim.x * CLS_WG) {
         const u64 key = keys[u];
         // split the code at '+': idx1, idx2 = code.split("+")[0:2]  (frender.py:306), both case-folded
         // and packed 3 bits per letter (a1 c2 g3 t4 n5) like the sheet
@@ -2761,7 +2762,7 @@ __global__ __launch_bounds__(CLS_WG) void classify_kernel(const u64* keys, const
 hipError_t launch_classify(const u64* keys, const u64* counts, u64 n, SheetArgs sh, int nsubs, int rc, ClassOut o,
                            const NbrMap& nm, hipStream_t s) {
     if (!n) return hipSuccess;
-    const u64 grid = (n + CLS_WG - 1) / CLS_WG;
+    const u64 grid = std::min<u64>((n + CLS_WG - 1) / CLS_WG, 2048);
     // u32 images when every sheet entry (and so every matching query) has <= 10 symbols
     const bool narrow = sh.S > 0 && sh.L1u >= 0 && sh.L1u <= 10 && sh.L2u >= 0 && sh.L2u <= 10;
     const size_t wb = narrow ? 4 : 8;

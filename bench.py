@@ -90,28 +90,78 @@ def table_checksum(ctx, U):
 
 
 def load_traffic(path, tree, per_launch_bytes, samples, index_len, combinatorial):
-    """(HBM bytes per launch, note) from a PMC traffic file (scripts/make_traffic.py), or (None, why):
-    a file measured on another source tree (frender_amd._lib.source_tree_hash) or launch shape is
-    refused, never reported."""
+    """(HBM bytes per launch, note, VALU dict) from a PMC traffic file (scripts/make_traffic.py), or
+    (None, why, None): a file measured on another source tree (frender_amd._lib.source_tree_hash) or
+    launch shape is refused, never reported."""
     try:
         with open(path) as f:
             tj = json.load(f)
     except (OSError, ValueError):
-        return None, "no PMC traffic file"
+        return None, "no PMC traffic file", None
     name = os.path.basename(path)
     if tj.get("tree_hash") != tree:
-        return None, f"refused {name}: measured on tree {tj.get('tree_hash')}, this tree is {tree}"
+        return None, f"refused {name}: measured on tree {tj.get('tree_hash')}, this tree is {tree}", None
     if not (tj.get("algorithmic_bytes_per_launch") == per_launch_bytes and tj.get("samples") == samples
             and tj.get("index_len") == index_len and bool(tj.get("combinatorial")) == combinatorial):
-        return None, f"refused {name}: measured on another launch shape"
+        return None, f"refused {name}: measured on another launch shape", None
     return tj.get("hbm_bytes_per_launch"), (f"{name} (tree {tree}): FETCH_SIZE x2 + WRITE_SIZE per launch, "
-                                            f"{tj.get('traffic_over_algorithmic')}x algorithmic")
+                                            f"{tj.get('traffic_over_algorithmic')}x algorithmic"), tj.get("valu")
+
+
+def valu_roofline(valu, per_launch_ms):
+    """The kernel's second bound: VALU issue.  SQ_INSTS_VALU per launch (the same PMC file, same tree)
+    over this run's measured launch time, against 1024 SIMDs x 2.4 GHz / 4 cycles per wave64 VALU
+    instruction.  None without a VALU pass for this tree."""
+    if not valu or not valu.get("insts_per_launch") or per_launch_ms <= 0:
+        return None
+    g = valu["insts_per_launch"] / (per_launch_ms / 1e3) / 1e9
+    peak = valu.get("peak_g_insts_per_s", 614.4)
+    return {"achieved": round(g, 1), "peak": peak, "unit": "G wave64 VALU inst/s", "frac": round(g / peak, 4),
+            "insts_per_record": valu.get("insts_per_record")}
 
 
 def _gz(chunk: bytes) -> bytes:
     import gzip
 
     return gzip.compress(chunk, compresslevel=1)
+
+
+_E2E = None
+
+
+def e2e_scan(args, ns, d, n, cores):
+    """The product `scan` command (frender_amd.scan.frender_scan: native inflate threads, GPU tally and
+    classify, CSV writers) on the CPU baseline's own .fastq.gz files and cores: the end-to-end rate a
+    user gets from compressed files (host-inflate-bound; `value` is the HBM-resident rate).  Run
+    twice: the first run includes the context's creation (cold), the second is timed warm."""
+    import argparse
+    import contextlib
+    import io
+
+    from frender_amd import scan as S
+
+    times = []
+    for k in range(2):
+        out = os.path.join(d, f"gpu{k}")
+        os.mkdir(out)
+        cwd = os.getcwd()
+        os.chdir(out)
+        try:
+            with contextlib.redirect_stdout(io.StringIO()):
+                t0 = time.perf_counter()
+                S.frender_scan(argparse.Namespace(**vars(ns)))
+                times.append(time.perf_counter() - t0)
+        finally:
+            os.chdir(cwd)
+    def contents(sub):  # output names carry the run's minute: compare the files' bytes, not their names
+        return sorted(open(os.path.join(d, sub, f), "rb").read() for f in os.listdir(os.path.join(d, sub)))
+
+    same = contents("gpu1") == contents("out")
+    return {"value": round(n / times[1] / 1e6, 3), "unit": "M reads/s", "cold_value": round(n / times[0] / 1e6, 3),
+            "cores": cores, "outputs_equal_cpu_baseline": same,
+            "sample": f"`scan -c {cores}` (frender_amd.scan.frender_scan: native inflate, GPU tally + classify, CSV) "
+                      f"on the cpu_baseline's {cores} .fastq.gz files ({n} reads, gzip level 1); value = warm run, "
+                      f"cold_value = first run incl. context creation; host-inflate-bound"}
 
 
 def cpu_baseline(args, ctx, sheet, reclen):
@@ -161,6 +211,9 @@ def cpu_baseline(args, ctx, sheet, reclen):
                 dt = time.perf_counter() - t0
         finally:
             os.chdir(cwd)
+        e2e = e2e_scan(args, ns, d, n, cores)
+    global _E2E
+    _E2E = e2e
     cal = ""
     try:
         with open(os.path.join(ROOT, "profiles", "cpu_ref_vs_port.json")) as f:
@@ -279,7 +332,7 @@ def main():
     per_launch_bytes = t_after.scan_bytes / max(launches, 1)
     per_launch_ms = scan_ms / max(launches, 1)
     achieved = per_launch_bytes / (per_launch_ms / 1e3) / 1e9 if per_launch_ms > 0 else 0.0
-    traffic, traffic_note = load_traffic(args.traffic_json, _lib.source_tree_hash(), per_launch_bytes,
+    traffic, traffic_note, valu = load_traffic(args.traffic_json, _lib.source_tree_hash(), per_launch_bytes,
                                          args.samples, args.index_len, args.combinatorial)
 
     csum = table_checksum(ctx, U) if (world == 1 or args.merge == "a2a" or rank == 0) else 0
@@ -315,8 +368,10 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_note,
                          "kernel": "fr::chunk_kernel", "bytes_per_launch": int(per_launch_bytes),
                          "avg_launch_ms": round(per_launch_ms, 4), "launches_per_step": int(launches),
-                         "log_aggregation_ms_per_launch": round(t_after.log_ms / max(launches, 1), 4)},
+                         "log_aggregation_ms_per_launch": round(t_after.log_ms / max(launches, 1), 4),
+                         "valu_issue": valu_roofline(valu, per_launch_ms)},
             "cpu_baseline": cpu,
+            "e2e": _E2E,
         }
         print(json.dumps(out), flush=True)
     ctx.device_free(buf)

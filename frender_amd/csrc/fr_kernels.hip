@@ -1373,7 +1373,9 @@ __device__ __forceinline__ u64 walk_wave(ScanShared& sh, const ScanArgs& a, u32 
         SegRegs q;
 #pragma unroll
         for (int k = 0; k < SEG / 16; ++k) {
-            const u32x4 v = mine[k];
+            // volatile: a real LDS read.  Forwarded from the stores, the tile would stay in 16 more
+            // VGPRs (copied by 16 v_mov per tile) while the next tile's loads fill r
+            const u32x4 v = *(const volatile lds_u32x4*)&mine[k];
             q.v[k] = make_uint4(v.x, v.y, v.z, v.w);
         }
         q.nx = 0;
@@ -2551,25 +2553,31 @@ hipError_t launch_nbr_build(const SheetArgs& sh, const int32_t* canon, int nsubs
     return hipGetLastError();
 }
 
-__device__ __forceinline__ int nbr_find(const NSlot* __restrict__ t, u32 mask, u64 q) {  // -1 none, -2 several
-    const u64 key = q | NBR_KEY;
-    u32 h = (u32)mix64(key) & mask;
+// one map probe chain from a slot already loaded (the caller issues the first loads of several chains
+// together, so a code waits for one round trip per stage, not one per map)
+__device__ __forceinline__ int nbr_resolve(const NSlot* __restrict__ t, u32 mask, u64 key, u32 h, NSlot e) {
     for (;;) {
-        const NSlot e = t[h];
         if (e.key == key) return ~e.vmin_c == e.vmax1 - 1u ? (int)~e.vmin_c : -2;
         if (e.key == 0) return -1;
         h = (h + 1) & mask;
+        e = t[h];
     }
 }
 
-__device__ __forceinline__ void pair_find(const PSlot* __restrict__ t, u32 mask, int v1, int v2, int& both, int& r) {
-    both = 0;
-    r = -1;
-    if (v1 < 0 || v2 < 0) return;
-    const u64 key = ((u64)(u32)v1 << 32) | (u32)v2 | NBR_KEY;
-    u32 h = (u32)mix64(key) & mask;
+// nbr_find on the idx1, idx2 and (rc) rc(idx2) maps with the three first probes in flight together
+__device__ __forceinline__ void nbr_find3(const NbrMap& nm, u64 q1, u64 q2, bool rc, int& a1, int& a2, int& a3) {
+    const u64 k1 = q1 | NBR_KEY, k2 = q2 | NBR_KEY;
+    const u32 h1 = (u32)mix64(k1) & nm.mmask[0], h2 = (u32)mix64(k2) & nm.mmask[1], h3 = (u32)mix64(k2) & nm.mmask[2];
+    const NSlot e1 = nm.m[0][h1], e2 = nm.m[1][h2];
+    const NSlot e3 = rc ? nm.m[2][h3] : NSlot{0, 0, 0};
+    a1 = nbr_resolve(nm.m[0], nm.mmask[0], k1, h1, e1);
+    a2 = nbr_resolve(nm.m[1], nm.mmask[1], k2, h2, e2);
+    a3 = rc ? nbr_resolve(nm.m[2], nm.mmask[2], k2, h3, e3) : -1;
+}
+
+__device__ __forceinline__ void pair_resolve(const PSlot* __restrict__ t, u32 mask, u64 key, u32 h, PSlot e, int& both,
+                                             int& r) {
     for (;;) {
-        const PSlot e = t[h];
         if (e.key == key) {
             both = (int)e.cnt;
             r = (int)~e.first_c;
@@ -2577,16 +2585,23 @@ __device__ __forceinline__ void pair_find(const PSlot* __restrict__ t, u32 mask,
         }
         if (e.key == 0) return;
         h = (h + 1) & mask;
+        e = t[h];
     }
 }
 
 // class_pair's result from the map probes: the rows near q1 are exactly the rows holding value a1 (a
-// single distinct value), so its first row is a1 and |M1 ∩ M2| is the pair count of (a1, a2)
+// single distinct value), so its first row is a1 and |M1 ∩ M2| is the pair count of (a1, a2).  The two
+// pair maps' first probes are in flight together.
 __device__ __forceinline__ void class_pair_nbr(const NbrMap& nm, int a1, int a2, int a3, int& m1, int& m2, int& cls,
                                                int& row, int& rm2, int& rcls, int& rrow) {
-    int both, r, rboth, rr;
-    pair_find(nm.p[0], nm.pmask[0], a1, a2, both, r);
-    pair_find(nm.p[1], nm.pmask[1], a1, a3, rboth, rr);
+    int both = 0, r = -1, rboth = 0, rr = -1;
+    const bool f0 = a1 >= 0 && a2 >= 0, f1 = a1 >= 0 && a3 >= 0;
+    const u64 pk0 = ((u64)(u32)a1 << 32) | (u32)a2 | NBR_KEY, pk1 = ((u64)(u32)a1 << 32) | (u32)a3 | NBR_KEY;
+    const u32 ph0 = (u32)mix64(pk0) & nm.pmask[0], ph1 = (u32)mix64(pk1) & nm.pmask[1];
+    const PSlot p0 = f0 ? nm.p[0][ph0] : PSlot{0, 0, 0};
+    const PSlot p1 = f1 ? nm.p[1][ph1] : PSlot{0, 0, 0};
+    if (f0) pair_resolve(nm.p[0], nm.pmask[0], pk0, ph0, p0, both, r);
+    if (f1) pair_resolve(nm.p[1], nm.pmask[1], pk1, ph1, p1, rboth, rr);
     m1 = a1;
     m2 = a2;
     rm2 = a3;
@@ -2669,16 +2684,18 @@ __global__ __launch_bounds__(CLS_WG) void classify_kernel(const u64* keys, const
                 else q2 |= sy << (3 * (i - n1));
             }
         } else {  // fast key: symbols A1 C2 G3 T4 N5 '+'6, folded they equal the sheet's a1..n5
-            int p1 = -1, p2 = MAXSYM, len = 0;
-            for (int i = 0; i < MAXSYM; ++i) {
-                const u32 sy = (u32)(key >> (3 * i)) & 7u;
-                if (!sy) break;
-                len = i + 1;
-                if (sy == 6u) {
-                    if (p1 < 0) p1 = i;
-                    else if (p2 == MAXSYM) p2 = i;
-                }
-            }
+            // SWAR over the 21 3-bit groups: len = symbols before the first empty group; the '+'
+            // groups (== 6) among them give p1, p2 (no per-symbol loop)
+            constexpr u64 G0 = 0x1249249249249249ull & ((1ull << 63) - 1ull);  // bit 0 of each group
+            const u64 nz = (key | (key >> 1) | (key >> 2)) & G0;                // groups holding a symbol
+            const u64 empty = ~nz & G0;
+            const int len = empty ? (int)(__builtin_ctzll(empty) / 3) : MAXSYM;
+            const u64 x = key ^ (G0 * 6ull);                                    // '+' groups become 0
+            u64 pm = ~(x | (x >> 1) | (x >> 2)) & G0;
+            pm &= len < MAXSYM ? (1ull << (3 * len)) - 1ull : ~0ull;
+            const int p1 = pm ? (int)(__builtin_ctzll(pm) / 3) : -1;
+            pm &= pm - 1ull;
+            const int p2 = pm ? (int)(__builtin_ctzll(pm) / 3) : MAXSYM;
             plus = p1 >= 0;
             if (plus) {
                 n1 = p1;
@@ -2699,11 +2716,7 @@ __global__ __launch_bounds__(CLS_WG) void classify_kernel(const u64* keys, const
             else if (sh.S > 0 && (sh.L2u == -2 || sh.L2u != n2)) err = 2;
             else {
                 int a1 = -2, a2 = -2, a3 = -1;
-                if (nm.on) {
-                    a1 = nbr_find(nm.m[0], nm.mmask[0], q1);
-                    a2 = nbr_find(nm.m[1], nm.mmask[1], q2);
-                    if (rc) a3 = nbr_find(nm.m[2], nm.mmask[2], q2);
-                }
+                if (nm.on) nbr_find3(nm, q1, q2, rc != 0, a1, a2, a3);
                 if (a1 != -2 && a2 != -2 && a3 != -2)
                     class_pair_nbr(nm, a1, a2, a3, m1, m2, cls, row, rm2, rcls, rrow);
                 else if (FR_CLS_SCALAR && rc)
@@ -2762,7 +2775,6 @@ __global__ __launch_bounds__(CLS_WG) void classify_kernel(const u64* keys, const
 hipError_t launch_classify(const u64* keys, const u64* counts, u64 n, SheetArgs sh, int nsubs, int rc, ClassOut o,
                            const NbrMap& nm, hipStream_t s) {
     if (!n) return hipSuccess;
-    const u64 grid = std::min<u64>((n + CLS_WG - 1) / CLS_WG, 2048);
     // u32 images when every sheet entry (and so every matching query) has <= 10 symbols
     const bool narrow = sh.S > 0 && sh.L1u >= 0 && sh.L1u <= 10 && sh.L2u >= 0 && sh.L2u <= 10;
     const size_t wb = narrow ? 4 : 8;
@@ -2773,7 +2785,9 @@ hipError_t launch_classify(const u64* keys, const u64* counts, u64 n, SheetArgs 
     // the scalar-load path (FR_CLS_SCALAR) reads the rows from HBM; only the name sums use LDS then
     const int sheet_in_lds = (!FR_CLS_SCALAR && nb + sheet_bytes <= CLS_LDS_BYTES) ? 1 : 0;
     const size_t lds = nb + (sheet_in_lds ? sheet_bytes : 0) + 16;
-    if (narrow && (sheet_in_lds || FR_CLS_SCALAR))
+    const u64 grid = std::min<u64>((n + CLS_WG - 1) / CLS_WG, 2048);
+    const bool wide = !(narrow && (sheet_in_lds || FR_CLS_SCALAR));
+    if (!wide)
         hipLaunchKernelGGL(classify_kernel<u32>, dim3((u32)grid), dim3(CLS_WG), lds, s, keys, counts, n, sh, nsubs, rc,
                            o, nm, sheet_in_lds, names_in_lds);
     else

@@ -23,6 +23,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNEL = "fr::chunk_kernel"
+VALU_PEAK_G = 256 * 4 * 2.4 / 4  # G wave64 VALU instructions per second (MI355X: 16-lane SIMDs)
 
 
 def rows(pattern):
@@ -69,6 +70,15 @@ def main():
         skb = sum(stream.values()) / len(stream)
         calib = {"fetch_size_kb_avg": skb, "hbm_bytes_x2": int(2 * skb * 1024),
                  "x2_over_algorithmic": round(2 * skb * 1024 / alg, 4)}
+    valu, _ = per_dispatch(rows(src + "/prof_valu/**/*counter_collection.csv"), "SQ_INSTS_VALU")
+    vact, _ = per_dispatch(rows(src + "/prof_valu/**/*counter_collection.csv"), "SQ_ACTIVE_INST_VALU")
+    valu_d = None
+    if valu:  # VALU issue: wave64 instructions; one SIMD issues one per 4 cycles (16 lanes)
+        vi = sum(valu.values()) / len(valu)
+        valu_d = {"insts_per_launch": int(vi), "insts_per_record": round(vi / (reads / launches), 3),
+                  "active_quad_cycles_per_launch": int(sum(vact.values()) / len(vact)) if vact else None,
+                  "peak_g_insts_per_s": VALU_PEAK_G,
+                  "peak_note": "256 CUs x 4 SIMDs x 2.4 GHz / 4 cycles per wave64 VALU instruction"}
     out = {
         "round": int(os.environ.get("ROUND", "3")),
         "tree_hash": source_tree_hash(),
@@ -88,6 +98,7 @@ def main():
         "traffic_over_algorithmic": round((2 * fkb * 1024 + wkb * 1024) / alg, 4),
         "fetch_over_algorithmic": round(2 * fkb * 1024 / alg, 4),
         "stream_only_calibration": calib,
+        "valu": valu_d,
         "source": f"profiles/{tag}_pmc_chunk_kernel.csv (rocprofv3 --pmc FETCH_SIZE, then --pmc WRITE_SIZE, "
                   f"separate runs of bench.py {os.environ.get('PROF_ARGS', '--steps 5 --warmup 1 --no-cpu')})",
     }

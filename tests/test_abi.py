@@ -61,11 +61,17 @@ def test_bench_refuses_traffic_of_another_tree(tmp_path):
     from frender_amd._lib import source_tree_hash
     tree = source_tree_hash()
     p = str(tmp_path / "t.json")
+    valu = {"insts_per_launch": 682000000, "insts_per_record": 13.64, "peak_g_insts_per_s": 614.4}
     rec = {"tree_hash": tree, "algorithmic_bytes_per_launch": 3.7e9, "samples": 96, "index_len": 8,
-           "combinatorial": False, "hbm_bytes_per_launch": 4000000000, "traffic_over_algorithmic": 1.08}
+           "combinatorial": False, "hbm_bytes_per_launch": 4000000000, "traffic_over_algorithmic": 1.08,
+           "valu": valu}
     for change, ok in (({}, True), ({"tree_hash": "0" * 16}, False), ({"samples": 384}, False)):
         with open(p, "w") as f:
             json.dump({**rec, **change}, f)
-        t, note = bench.load_traffic(p, tree, 3.7e9, 96, 8, False)
+        t, note, v = bench.load_traffic(p, tree, 3.7e9, 96, 8, False)
         assert (t == 4000000000) == ok and (note.startswith("refused") != ok), note
+        assert (v == valu) == ok  # the VALU figures travel with the traffic file, under the same checks
+    r = bench.valu_roofline(valu, 1.45)  # 6.82e8 instructions in 1.45 ms against 614.4 G/s
+    assert r["unit"] == "G wave64 VALU inst/s" and abs(r["frac"] - 6.82e8 / 1.45e-3 / 1e9 / 614.4) < 1e-3
+    assert bench.valu_roofline(None, 1.45) is None
     assert bench.load_traffic(str(tmp_path / "absent.json"), tree, 3.7e9, 96, 8, False)[0] is None

@@ -75,6 +75,7 @@ _SIGS = {
     "fr_last_error": (C.c_char_p, [P]),
     "fr_get_timing": (C.c_int, [P, C.POINTER(Timing)]),
     "fr_sync": (C.c_int, [P]),
+    "fr_set_timing": (C.c_int, [P, C.c_int]),
     "fr_get_diag": (C.c_int, [P, P, C.c_int]),
     "fr_set_sheet": (C.c_int, [P, C.c_int, P, P, P, P, P, P, C.c_int, P, P, P, C.c_int]),
     "fr_reset": (C.c_int, [P]),
@@ -609,6 +610,10 @@ class Context:
 
     def sync(self):
         self._ck(lib.fr_sync(self.h), "fr_sync")
+
+    def set_timing(self, on: bool):
+        """HIP timing events on (default) or off (fr_set_timing): off removes their stream bubbles."""
+        self._ck(lib.fr_set_timing(self.h, 1 if on else 0), "fr_set_timing")
 
     def export_unique_device(self, keys_ptr: int, counts_ptr: int, first_ptr: int, cap: int):
         self._ck(lib.fr_export_unique_device(self.h, P(keys_ptr), P(counts_ptr), P(first_ptr), cap),

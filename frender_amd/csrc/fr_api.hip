@@ -180,6 +180,8 @@ struct fr_ctx {
     size_t ev_used = 0;
     u64 scan_launches = 0, scan_bytes = 0;
     double classify_ms = 0, finalize_ms = 0;
+    bool timing = true;  // fr_set_timing: record the timing events
+    bool fin_timed = false;  // the pending fr_finalize recorded fin_e0
 };
 
 #define CK(x)                                                                                  \
@@ -309,7 +311,7 @@ static int settle_finalize(fr_ctx* ctx) {
     ctx->fin_pending = false;
     CK(hipEventSynchronize(ctx->fin_e1));
     float ms = 0;
-    CK(hipEventElapsedTime(&ms, ctx->fin_e0, ctx->fin_e1));
+    if (ctx->fin_timed) CK(hipEventElapsedTime(&ms, ctx->fin_e0, ctx->fin_e1));
     ctx->finalize_ms = ms;
     if (*ctx->h_fin != ctx->fin_expect) return fail(ctx, FR_ERR_DEVICE, "compaction count mismatch");
     return FR_OK;
@@ -495,7 +497,8 @@ static int launch_range(fr_ctx* ctx, const u8* dptr, u64 len, u64 avail, int own
     }
     CK(hipMemsetAsync(&ctx->st->ticket, 0, 2 * sizeof(u32), ctx->stream));  // ticket, chunks_done
     ctx->st_fresh = false;
-    if (ctx->ev_used == ctx->ev_a.size()) {
+    const bool timed = ctx->timing;
+    if (timed && ctx->ev_used == ctx->ev_a.size()) {
         hipEvent_t e1, e2, e3;
         CK(hipEventCreate(&e1));
         CK(hipEventCreate(&e2));
@@ -504,7 +507,7 @@ static int launch_range(fr_ctx* ctx, const u8* dptr, u64 len, u64 avail, int own
         ctx->ev_b.push_back(e2);
         ctx->ev_l.push_back(e3);
     }
-    CK(hipEventRecord(ctx->ev_a[ctx->ev_used], ctx->stream));
+    if (timed) CK(hipEventRecord(ctx->ev_a[ctx->ev_used], ctx->stream));
     // chunking (chunk_bounds in fr_kernels.hip): ramped when the range holds both ramps and a full
     // chunk, else one uniform chunk per workgroup.  A ramped launch also carries the heavy geometry
     // when the range fits it; the kernel picks one (DevState::heavy)
@@ -542,12 +545,14 @@ static int launch_range(fr_ctx* ctx, const u8* dptr, u64 len, u64 avail, int own
     ctx->last_args = a;
     ctx->last_grid = grid;
     ctx->last_valid = true;
-    CK(hipEventRecord(ctx->ev_b[ctx->ev_used], ctx->stream));
+    if (timed) CK(hipEventRecord(ctx->ev_b[ctx->ev_used], ctx->stream));
     if (a.log)
         CK(launch_log_aggregate(ctx->tab, ctx->st, ctx->log, ctx->log_rcap, ctx->log_sub, ctx->log_scap, a.file_tag,
                                 a.file_offset, ctx->ablate, ctx->stream));
-    CK(hipEventRecord(ctx->ev_l[ctx->ev_used], ctx->stream));
-    ctx->ev_used++;
+    if (timed) {
+        CK(hipEventRecord(ctx->ev_l[ctx->ev_used], ctx->stream));
+        ctx->ev_used++;
+    }
     ctx->scan_launches++;
     ctx->scan_bytes += len;
     ctx->par ^= 1u;
@@ -732,6 +737,12 @@ int fr_get_timing(fr_ctx* ctx, fr_timing* out) {
     out->last_scan_ms = last;
     out->classify_ms = ctx->classify_ms;
     out->finalize_ms = ctx->finalize_ms;
+    return FR_OK;
+}
+
+int fr_set_timing(fr_ctx* ctx, int on) {
+    if (!ctx) return FR_ERR_INVALID;
+    ctx->timing = on != 0;
     return FR_OK;
 }
 
@@ -1127,7 +1138,8 @@ int fr_finalize(fr_ctx* ctx, uint64_t* n_unique, uint64_t* n_presence, uint64_t*
         CK(dalloc(&ctx->d_rank, cap));
         ctx->ucap = cap;
     }
-    CK(hipEventRecord(e0, ctx->stream));
+    if (ctx->timing) CK(hipEventRecord(e0, ctx->stream));
+    ctx->fin_timed = ctx->timing;
     // one context's own ordinals: bin them (fin_* kernels); merged rows (any file tag): radix sort
     BinMap bm{0, 0, 0, 0, 0};
     u64 nbins = 0;
@@ -1367,15 +1379,16 @@ int fr_classify(fr_ctx* ctx, int num_subs, int rc_mode, int16_t* m1, int16_t* m2
     if ((rc = ensure_nbr(ctx, sh, num_subs, rc_mode ? 1 : 0))) return rc;
     ClassOut o{ctx->d_m1, ctx->d_m2, ctx->d_cls, ctx->d_row, ctx->d_rm2, ctx->d_rcls, ctx->d_rrow,
                ctx->d_rcf, ctx->d_rcr, ctx->d_errf, ctx->d_errw};
-    CK(hipEventRecord(e0, ctx->stream));
+    const bool timed = ctx->timing;
+    if (timed) CK(hipEventRecord(e0, ctx->stream));
     CK(launch_classify(ctx->d_keys_s, ctx->d_counts_s, n, sh, num_subs, rc_mode ? 1 : 0, o, ctx->nbr, ctx->stream));
-    CK(hipEventRecord(e1, ctx->stream));
+    if (timed) CK(hipEventRecord(e1, ctx->stream));
     u64 ef = ~0ull;
     CK(hipMemcpyAsync(&ef, ctx->d_errf, 8, hipMemcpyDeviceToHost, ctx->stream));
     CK(hipStreamSynchronize(ctx->stream));
     if (int src = settle_finalize(ctx)) return src;  // landed with the classify: no extra round trip
     float ms = 0;
-    CK(hipEventElapsedTime(&ms, e0, e1));
+    if (timed) CK(hipEventElapsedTime(&ms, e0, e1));
     ctx->classify_ms = ms;
     if (err_unique) *err_unique = ef == ~0ull ? -1 : (int64_t)ef;
     if (err_which) {

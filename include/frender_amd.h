@@ -74,6 +74,11 @@ fr_ctx* fr_create(int device, uint64_t chunk_bytes, uint64_t table_slots);
 void fr_destroy(fr_ctx* ctx);
 const char* fr_last_error(const fr_ctx* ctx);
 int fr_get_timing(fr_ctx* ctx, fr_timing* out);
+/* on != 0 (the default): HIP timing events around every tally launch, its launch-log aggregation,
+ * fr_finalize and fr_classify (fr_get_timing's figures).  on = 0: none are recorded (each event
+ * record is a bubble of a few microseconds on the stream); fr_get_timing then reports zeros for the
+ * work done while off.  Results do not depend on it. */
+int fr_set_timing(fr_ctx* ctx, int on);
 int fr_sync(fr_ctx* ctx);
 /* diagnostics: {look-back max polls, total polls, keys, overflow, presence, exotic, grid, slots,
  * 8 phase stamps, speculation replays, exotic-only replays} */

@@ -947,3 +947,25 @@ def test_first_occurrence_bins(lib, mode):
     exp = oracle_tally(files)
     assert recs == exp[1]
     assert list(got.items()) == list(exp[0].items())
+
+
+@pytest.mark.gpu
+def test_timing_events_off_same_table(lib):
+    """fr_set_timing(0) drops the HIP timing events only: the same table, zero timings."""
+    from frender_amd import synth
+    sheet = synth.make_sheet(8, 8, 8, seed=5)
+    data = synth.generate_bytes(sheet, 0, 30000, R=8, seed=7)
+    out = []
+    for on in (True, False):
+        c = lib.Context(device=0, chunk_bytes=1 << 20, table_slots=1 << 16)
+        c.set_timing(on)
+        c.reset()
+        c.begin_file(None)
+        c.feed(data)
+        st = c.end_file()
+        U, _, _ = c.finalize()
+        t = c.timing()
+        out.append((st.records, U, [a.tolist() for a in c.unique()]))
+        assert (t.scan_ms > 0) == on and (t.finalize_ms > 0) == on and t.scan_launches > 0
+        c.close()
+    assert out[0] == out[1]

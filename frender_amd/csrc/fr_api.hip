@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstddef>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -495,7 +496,7 @@ static int launch_range(fr_ctx* ctx, const u8* dptr, u64 len, u64 avail, int own
         ctx->epoch = 1;
         a.epoch = 1;
     }
-    CK(hipMemsetAsync(&ctx->st->ticket, 0, 2 * sizeof(u32), ctx->stream));  // ticket, chunks_done
+    // ticket / chunks_done / exits are zero here: the reset image, or the previous launch's last workgroup
     ctx->st_fresh = false;
     const bool timed = ctx->timing;
     if (timed && ctx->ev_used == ctx->ev_a.size()) {
@@ -669,7 +670,7 @@ void fr_destroy(fr_ctx* ctx) {
                    ctx->d_keys, ctx->d_counts, ctx->d_first, ctx->d_keys_s, ctx->d_counts_s,
                    ctx->d_first_s, ctx->d_pos, ctx->d_perm, ctx->d_rank, ctx->d_counter, ctx->d_temp, ctx->d_bins, ctx->d_binbase, ctx->d_arr, ctx->d_rows, ctx->d_pres_u,
                    ctx->d_pres_f, ctx->d_m1, ctx->d_m2, ctx->d_row, ctx->d_rm2, ctx->d_rrow, ctx->d_cls, ctx->d_rcls,
-                   ctx->d_errw, ctx->d_errf, ctx->d_rcf, ctx->d_rcr, ctx->d_nbr, ctx->cold, ctx->rare, ctx->chunk_info, ctx->log, ctx->log_sub, ctx->log_temp};
+                   ctx->d_errw, ctx->d_errf, ctx->d_nbr, ctx->cold, ctx->rare, ctx->chunk_info, ctx->log, ctx->log_sub, ctx->log_temp};
     for (void* p : dev)
         if (p) (void)hipFree(p);
     if (ctx->h_st) (void)hipHostFree(ctx->h_st);
@@ -878,10 +879,9 @@ int fr_begin_file_at(fr_ctx* ctx, int64_t file_index, uint64_t byte_base, int64_
     ctx->exo_new_file = 0;
     ctx->exo_records_file = 0;
     ctx->last_valid = false;
-    // per-file device flags + line carry
-    CK(hipMemsetAsync(&ctx->st->lines[0], 0, 2 * sizeof(u64), ctx->stream));
-    CK(hipMemsetAsync(&ctx->st->err_nospace, 0xFF, sizeof(u64), ctx->stream));
-    CK(hipMemsetAsync(&ctx->st->nonascii, 0, 2 * sizeof(u32), ctx->stream));
+    // per-file device flags + line carry: DevState's per-file block, from the pinned reset image
+    static_assert(offsetof(DevState, utf8_bad) + sizeof(u32) - offsetof(DevState, lines) == 32, "per-file block");
+    CK(hipMemcpyAsync(&ctx->st->lines[0], &ctx->h_zero->lines[0], 32, hipMemcpyHostToDevice, ctx->stream));
     ctx->h_st->lines[0] = ctx->h_st->lines[1] = 0;  // the snapshot stays exact
     ctx->h_st->err_nospace = ~0ull;
     ctx->h_st->nonascii = ctx->h_st->utf8_bad = 0;
@@ -1304,7 +1304,7 @@ int fr_get_exotic_table(fr_ctx* ctx, uint64_t* counts, uint64_t* first, uint64_t
 static int ensure_class_scratch(fr_ctx* ctx, u64 n) {
     if (n <= ctx->ccap && ctx->n_names <= ctx->rc_names_cap && ctx->d_errf) return FR_OK;
     void* old[] = {ctx->d_m1, ctx->d_m2, ctx->d_row, ctx->d_rm2, ctx->d_rrow, ctx->d_cls, ctx->d_rcls, ctx->d_errw,
-                   ctx->d_errf, ctx->d_rcf, ctx->d_rcr};
+                   ctx->d_errf};  // d_rcf / d_rcr live inside d_errf's block
     for (void* p : old)
         if (p) CK(hipFree(p));
     const u64 cap = std::max<u64>(std::max(n, ctx->ccap), 1024);
@@ -1316,10 +1316,11 @@ static int ensure_class_scratch(fr_ctx* ctx, u64 n) {
     CK(dalloc(&ctx->d_cls, cap));
     CK(dalloc(&ctx->d_rcls, cap));
     CK(dalloc(&ctx->d_errw, cap));
-    CK(dalloc(&ctx->d_errf, 1));
+    // one block zeroed by one memset per classify: ~(first error index) (0: none), then the rc sums
     const int names = std::max(ctx->n_names, 1);
-    CK(dalloc(&ctx->d_rcf, names));
-    CK(dalloc(&ctx->d_rcr, names));
+    CK(dalloc(&ctx->d_errf, 1 + 2 * (u64)names));
+    ctx->d_rcf = ctx->d_errf + 1;
+    ctx->d_rcr = ctx->d_rcf + names;
     ctx->ccap = cap;
     ctx->rc_names_cap = names;
     return FR_OK;
@@ -1372,9 +1373,8 @@ int fr_classify(fr_ctx* ctx, int num_subs, int rc_mode, int16_t* m1, int16_t* m2
     int rc = ensure_class_scratch(ctx, n);
     if (rc) return rc;
     hipEvent_t e0 = ctx->cls_e0, e1 = ctx->cls_e1;
-    CK(hipMemsetAsync(ctx->d_errf, 0xFF, 8, ctx->stream));
-    CK(hipMemsetAsync(ctx->d_rcf, 0, std::max(ctx->n_names, 1) * 8, ctx->stream));
-    CK(hipMemsetAsync(ctx->d_rcr, 0, std::max(ctx->n_names, 1) * 8, ctx->stream));
+    // the whole block: d_rcr sits rc_names_cap entries after d_rcf, however many names this sheet has
+    CK(hipMemsetAsync(ctx->d_errf, 0, (1 + 2 * (u64)ctx->rc_names_cap) * 8, ctx->stream));
     SheetArgs sh{ctx->S, ctx->n_names, ctx->L1u, ctx->L2u, ctx->d_i1, ctx->d_i2, ctx->d_i2rc, ctx->d_name};
     if ((rc = ensure_nbr(ctx, sh, num_subs, rc_mode ? 1 : 0))) return rc;
     ClassOut o{ctx->d_m1, ctx->d_m2, ctx->d_cls, ctx->d_row, ctx->d_rm2, ctx->d_rcls, ctx->d_rrow,
@@ -1384,8 +1384,9 @@ int fr_classify(fr_ctx* ctx, int num_subs, int rc_mode, int16_t* m1, int16_t* m2
     CK(launch_classify(ctx->d_keys_s, ctx->d_counts_s, n, sh, num_subs, rc_mode ? 1 : 0, o, ctx->nbr, ctx->stream));
     if (timed) CK(hipEventRecord(e1, ctx->stream));
     u64 ef = ~0ull;
-    CK(hipMemcpyAsync(&ef, ctx->d_errf, 8, hipMemcpyDeviceToHost, ctx->stream));
+    CK(hipMemcpyAsync(&ef, ctx->d_errf, 8, hipMemcpyDeviceToHost, ctx->stream));  // ~index, 0 none
     CK(hipStreamSynchronize(ctx->stream));
+    ef = ~ef;  // the kernel kept ~(first error index): 0 -> ~0, none
     if (int src = settle_finalize(ctx)) return src;  // landed with the classify: no extra round trip
     float ms = 0;
     if (timed) CK(hipEventElapsedTime(&ms, e0, e1));

@@ -96,9 +96,15 @@ constexpr int LOG_SUBS = 1 << LOG_SUB_BITS;   // sub-regions per region (aggrega
 constexpr int LOG_NSUB = LOG_NR * LOG_SUBS;    // sub-regions in all
 
 struct DevState {
+    // per-file block (contiguous: fr_begin_file resets it with one copy from the reset image)
     u64 lines[2];        // terminators before the current range (launch parity)
-    u32 ticket;          // chunk ticket, zeroed before every launch
-    u32 chunks_done;     // chunks that published their line count (zeroed with the ticket)
+    u64 err_nospace;     // min file offset of a header without ' ' (~0 = none)
+    u32 nonascii;        // a byte >= 0x80 was seen in the current file
+    u32 utf8_bad;
+    // per launch: the launch's last workgroup to exit zeroes them for the next launch
+    u32 ticket;          // chunk ticket
+    u32 chunks_done;     // chunks that published their line count
+    u32 exits;           // workgroups that left the chunk loop
     u32 spin_fail;
     u32 spec_fail;       // a committed speculative chunk's guessed line phase was wrong (host redoes the feed)
     u64 n_keys;
@@ -106,9 +112,6 @@ struct DevState {
     u64 n_presence;
     u64 n_exotic;
     u64 exo_pool_used;
-    u64 err_nospace;     // min file offset of a header without ' ' (~0 = none)
-    u32 nonascii;        // a byte >= 0x80 was seen in the current file
-    u32 utf8_bad;
     u32 cap_flags;       // 1 presence, 2 overflow list, 4 exotic pool
     u32 spin_max;        // diagnostics: longest look-back wait (polls)
     u64 spin_total;      // diagnostics: total look-back polls that found a window not ready
@@ -208,7 +211,7 @@ struct ClassOut {
     int16_t* rc_row;
     u64* rc_f;           // per name
     u64* rc_r;
-    u64* err_first;      // min unique index with an error (~0 none)
+    u64* err_first;      // ~(min unique index with an error), 0 none (zero-initialised with the rc sums)
     int32_t* err_which;  // per unique (optional): 1 idx1 len, 2 idx2 len, 3 no '+'
 };
 

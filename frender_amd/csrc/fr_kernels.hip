@@ -1641,6 +1641,13 @@ __global__ __launch_bounds__(WG, FR_OCC) void chunk_kernel(ScanArgs args) {
         if (sh.created) atomicAdd((unsigned long long*)&a.st->n_keys, (unsigned long long)sh.created);
         if (sh.flags & 1u) atomicOr(&a.st->nonascii, 1u);
         if (sh.flags & 2u) atomicOr(&a.st->utf8_bad, 1u);
+        // every workgroup has taken its last ticket: the last one out zeroes the launch's counters
+        // for the next launch (stream order makes the plain stores visible to it)
+        if (atomicAdd(&a.st->exits, 1u) == gridDim.x - 1u) {
+            a.st->ticket = 0;
+            a.st->chunks_done = 0;
+            a.st->exits = 0;
+        }
     }
 }
 
@@ -2737,7 +2744,7 @@ __global__ __launch_bounds__(CLS_WG) void classify_kernel(const u64* keys, const
             }
         }
         if (err) {
-            atomicMin((unsigned long long*)o.err_first, (unsigned long long)u);
+            atomicMax((unsigned long long*)o.err_first, (unsigned long long)~u);  // = min u
             if (o.err_which) o.err_which[u] = err;
         } else if (o.err_which) {
             o.err_which[u] = 0;

@@ -2757,7 +2757,8 @@ __global__ __launch_bounds__(CLS_WG) void classify_kernel(const u64* keys, const
             o.rc_m2[u] = (int16_t)rm2;
             o.rc_cls[u] = (u8)rcls;
             o.rc_row[u] = (int16_t)rrow;
-            const u64 cnt = counts[u];
+            // the record count only where a sum takes it (most codes are hops or undetermined)
+            const u64 cnt = (cls == CLS_DEMUX || rcls == CLS_DEMUX) ? counts[u] : 0ull;
             if (cls == CLS_DEMUX) {
                 const int nm = sh.name[row];
                 if (names_in_lds) atomicAdd(&lf[nm], (unsigned long long)cnt);

@@ -45,7 +45,7 @@ constexpr u32 SPIN_MAX = 1u << 24;   // look-back spin bound (then FR_ERR_DEVICE
 constexpr int ORD_SHIFT = 44;        // ordinal = file_tag << 44 | file byte offset
 constexpr int EXO_BUF = 32;          // chunk kernel: exotic records buffered while speculating
 #ifndef FR_PHASE_LINES
-#define FR_PHASE_LINES 24
+#define FR_PHASE_LINES 16
 #endif
 constexpr int PHASE_LINES = FR_PHASE_LINES;  // lines the chunk phase guess looks at (>= 8)
 constexpr u32 RARE_RING = 8192;      // chunk kernel: rare events queued per workgroup (a quarter per wave)

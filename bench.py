@@ -54,6 +54,12 @@ def parse():
                          "partition) or a binary tree into rank 0")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, one GPU per rank); gloo only to rehearse N ranks on one GPU")
+    ap.add_argument("--rank-check", action="store_true",
+                    help="launcher check: every rank joins the process group over gloo, rank 0 prints the world "
+                         "size it sees, nothing touches a GPU")
+    ap.add_argument("--pin-json", default=os.path.join(ROOT, "tests", "golden", "cfg2_pin.json"),
+                    help="the reference's own rows for BASELINE config 2 (tests/golden/make_golden_cfg2.py): at N=1 "
+                         "on that exact shape the classified table must reproduce them (checked after timing)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r03.json"),
                     help="per-launch HBM bytes of the tally kernel from rocprofv3 PMC (scripts/make_traffic.py); "
                          "used only when taken on this source tree and this launch shape, else traffic is null")
@@ -230,11 +236,60 @@ def cpu_baseline(args, ctx, sheet, reclen):
                       f"files (level 1), {cores} workers: {dt:.2f} s{cal}"}
 
 
+def pin_check(args, ctx, sheet, idx2rc, nid, names):
+    """BASELINE config 2 at N=1: the benchmarked table (the last timed step's), classified, must equal
+    the reference's own tally_barcodes + process rows on the same records (tests/golden/cfg2_pin.json:
+    unique codes, sha256 over every row in order, first/last 1000 rows).  Outside the timed region."""
+    from frender_amd import _lib, synth
+
+    with open(args.pin_json) as f:
+        pin = json.load(f)
+    keys, counts, _ = ctx.unique()
+    ctx.set_sheet(sheet.idx1, sheet.idx2, idx2rc, nid, len(names))
+    out = ctx.classify(args.nsubs, False)
+    digest, first, last = synth.rows_digest(_lib.decode_keys(keys), counts, out, sheet.idx1, sheet.idx2, sheet.ids)
+    ok = (len(keys) == pin["unique_codes"] and digest == pin["rows_sha256"] and first == pin["first_rows"]
+          and last == pin["last_rows"])
+    if not ok:
+        raise SystemExit(f"bench: the benchmarked table differs from the reference's rows ({args.pin_json}): "
+                         f"{len(keys)} vs {pin['unique_codes']} codes, sha256 {digest} vs {pin['rows_sha256']}")
+    return {"file": os.path.relpath(args.pin_json, ROOT), "unique_codes": pin["unique_codes"],
+            "rows_sha256": digest, "equal": True,
+            "source": "reference frender.py tally_barcodes + process on the same records (imported in the "
+                      "build container by tests/golden/make_golden_cfg2.py)"}
+
+
+def rank_check(world):
+    """--rank-check: the launcher's ranks meet over gloo; rank 0 prints the world size they agree on."""
+    import torch
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo")
+    t = torch.ones(1, dtype=torch.int64)
+    dist.all_reduce(t)
+    if dist.get_rank() == 0:
+        print(json.dumps({"rank_check": True, "world": world, "ranks_joined": int(t.item())}), flush=True)
+    dist.destroy_process_group()
+    return 0
+
+
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # `bench.py --gpus N` without a launcher: one child rank per GPU, before anything touches a GPU
+        from frender_amd.dist import launch_ranks
+        return launch_ranks(args.gpus, sys.argv[1:], cmd=[sys.executable, os.path.abspath(__file__)])
+    world = int(env_world or "1")
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a measurement of "
+              f"{world} GPU(s) as {args.gpus}", file=sys.stderr)
+        return 2
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.rank_check:
+        return rank_check(world) if world > 1 else (print(json.dumps({"rank_check": True, "world": 1,
+                                                                      "ranks_joined": 1})) or 0)
     dist = None
     if world > 1:
         import torch
@@ -344,6 +399,9 @@ def main():
     if world > 1 and args.merge == "a2a":  # report the merged table's size (sum of the partitions)
         U, csum = (int(x) for x in reduce_sum(dist, wire, [U, csum]))
     csum &= (1 << 64) - 1
+    pinned = None
+    if world == 1 and config_name(args) == "BASELINE config 2" and os.path.exists(args.pin_json):
+        pinned = pin_check(args, ctx, sheet, idx2rc, nid, names)
     if rank == 0:
         cpu = None if (args.no_cpu or world > 1) else cpu_baseline(args, ctx, sheet, reclen)  # N=1 only
         value = world * n / (ms / 1e3) / 1e6
@@ -366,7 +424,7 @@ def main():
                                    f"decoded FASTQ resident in HBM",
                        "reads_per_gpu": n, "bytes_per_record": reclen, "samples": args.samples,
                        "nsubs": args.nsubs, "rc": bool(args.rc), "unique_codes": int(U),
-                       "table_checksum": f"{csum:016x}",
+                       "table_checksum": f"{csum:016x}", "reference_pin": pinned,
                        "parallelism": f"dp{world} (record shards) + {'RCCL' if args.dist_backend == 'nccl' else 'gloo'} "
                                       + ("all-to-all hash-partitioned merge" if args.merge == "a2a" else "tree merge") if world > 1 else "1 GPU"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -383,7 +441,8 @@ def main():
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

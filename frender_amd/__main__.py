@@ -5,6 +5,9 @@ import sys
 from datetime import datetime, timezone
 
 
+from .dist import launch_ranks
+
+
 def main(argv=None):
     parser = argparse.ArgumentParser(prog="frender_amd")
     sub = parser.add_subparsers()
@@ -71,40 +74,6 @@ def main(argv=None):
         return 0
     parser.print_help()
     return 2
-
-
-def launch_ranks(n: int, argv: list) -> int:
-    """`scan|demux --gpus N`: one child process per GPU (this process never touches a GPU), joined by
-    torch.distributed over 127.0.0.1; rank 0's stdout is the command's.  A rank that fails ends the
-    others; the exit status is rank 0's, or the first failure's."""
-    import socket
-    import subprocess
-    import time
-
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-    procs = []
-    for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, "-m", "frender_amd", *argv], env=env,
-                                      stdout=None if r == 0 else subprocess.DEVNULL))
-    codes = [None] * n
-    while any(c is None for c in codes):
-        for r, p in enumerate(procs):
-            if codes[r] is None:
-                codes[r] = p.poll()
-        if any(c not in (None, 0) for c in codes):  # a failed rank: the others cannot finish
-            time.sleep(2)
-            for r, p in enumerate(procs):
-                if p.poll() is None:
-                    p.terminate()
-            for r, p in enumerate(procs):
-                codes[r] = p.wait()
-            break
-        time.sleep(0.05)
-    return codes[0] if codes[0] else next((c for c in codes if c), 0)
 
 
 def run_rank(args) -> int:

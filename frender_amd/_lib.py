@@ -87,6 +87,7 @@ _SIGS = {
     "fr_finalize": (C.c_int, [P, u64p, u64p, u64p]),
     "fr_get_unique": (C.c_int, [P, P, P, P]),
     "fr_get_presence": (C.c_int, [P, P, P]),
+    "fr_get_presence_counts": (C.c_int, [P, P, P]),
     "fr_exotic_sizes": (C.c_int, [P, u64p, u64p, u64p]),
     "fr_get_exotic_table": (C.c_int, [P, P, P, P, P, P, P]),
     "fr_classify": (C.c_int, [P, C.c_int, C.c_int, P, P, P, P, P, P, P, P, P]),
@@ -504,6 +505,14 @@ class Context:
         f = np.empty(self.NP, dtype=np.uint32)
         self._ck(lib.fr_get_presence(self.h, _ptr(u), _ptr(f)), "fr_get_presence")
         return u, f
+
+    def presence_counts(self, n_exotic_pairs: int):
+        """Reads of each presence pair's code in the pair's file (fr_get_presence_counts): aligned with
+        presence() and with exotic_table()'s pairs (n_exotic_pairs of them)."""
+        c = np.empty(self.NP, dtype=np.uint64)
+        e = np.empty(int(n_exotic_pairs), dtype=np.uint64)
+        self._ck(lib.fr_get_presence_counts(self.h, _ptr(c), _ptr(e)), "fr_get_presence_counts")
+        return c, e
 
     def exotic_table(self):
         """The scan's exotic codes aggregated by the library: (codes as bytes, counts, first

@@ -26,7 +26,6 @@ struct fr_ctx {
     std::string err;
     int grid = 0;
     u32 flush_at = NS * 3 / 4;
-    u32 ablate = 0;
     u64* cold = nullptr;
     u32 cold_cap = 8192;
     // launch log (fr_internal.h LogEntry): commits append, launch_log_aggregate folds it into the table
@@ -109,11 +108,13 @@ struct fr_ctx {
     struct ExoCode {
         u64 count, first;
         u32 last_tag;
+        u32 last_pair;  // its presence pair of the last file that held it
     };
     std::unordered_map<std::string, u32> exo_index;
     std::vector<std::string> exo_str;     // first-appearance order of the drains
     std::vector<ExoCode> exo_codes;
     std::vector<u32> exo_pres_code, exo_pres_file;
+    std::vector<u64> exo_pres_count;      // records of the code in the pair's file
     u64 exo_new_file = 0;                 // distinct exotic codes of the current file
     u64 exo_records_file = 0;             // exotic records of the current file
     bool host_feed = false;               // launches come from fr_feed (each checked before the next)
@@ -165,6 +166,7 @@ struct fr_ctx {
     u64 n_pres = 0;
     u64 pmap_cap = 0;
     u32 *d_pres_u = nullptr, *d_pres_f = nullptr;
+    u64* d_pres_c = nullptr;  // per pair: the code's running count at its file's end (mod 2^44)
     u64 n_exo = 0;  // exotic codes of the finalized scan
 
     // classify scratch
@@ -383,7 +385,7 @@ static int drain_exotic(fr_ctx* ctx) {
             k = (u32)ctx->exo_codes.size();
             ctx->exo_index.emplace(code, k);
             ctx->exo_str.push_back(std::move(code));
-            ctx->exo_codes.push_back({0, ~0ull, 0});
+            ctx->exo_codes.push_back({0, ~0ull, 0, 0});
         } else {
             k = it->second;
         }
@@ -393,10 +395,13 @@ static int drain_exotic(fr_ctx* ctx) {
         const u32 tag = (u32)(ord[i] >> ORD_SHIFT);
         if (e.last_tag != tag) {  // a file's records all carry its tag; files are scanned in order
             e.last_tag = tag;
+            e.last_pair = (u32)ctx->exo_pres_code.size();
             ctx->exo_pres_code.push_back(k);
             ctx->exo_pres_file.push_back(tag - 1u);
+            ctx->exo_pres_count.push_back(0);
             ctx->exo_new_file++;
         }
+        ctx->exo_pres_count[e.last_pair] += 1;
     }
     ctx->exo_records_file += n;
     return FR_OK;
@@ -480,7 +485,6 @@ static int launch_range(fr_ctx* ctx, const u8* dptr, u64 len, u64 avail, int own
     a.own_end = own_end;
     a.pre_valid = pre_valid;
     a.flush_at = ctx->flush_at;
-    a.ablate = ctx->ablate;
     a.max_records = ctx->max_records;
     a.st = ctx->st;
     a.tiles = ctx->tiles;
@@ -549,7 +553,7 @@ static int launch_range(fr_ctx* ctx, const u8* dptr, u64 len, u64 avail, int own
     if (timed) CK(hipEventRecord(ctx->ev_b[ctx->ev_used], ctx->stream));
     if (a.log)
         CK(launch_log_aggregate(ctx->tab, ctx->st, ctx->log, ctx->log_rcap, ctx->log_sub, ctx->log_scap, a.file_tag,
-                                a.file_offset, ctx->ablate, ctx->stream));
+                                a.file_offset, ctx->stream));
     if (timed) {
         CK(hipEventRecord(ctx->ev_l[ctx->ev_used], ctx->stream));
         ctx->ev_used++;
@@ -581,7 +585,6 @@ fr_ctx* fr_create(int device, uint64_t chunk_bytes, uint64_t table_slots) {
     ctx->grid = prop.multiProcessorCount * per_cu;
     if (const char* g = getenv("FR_GRID")) ctx->grid = std::max(1, atoi(g));
     if (const char* f = getenv("FR_FLUSH_AT")) ctx->flush_at = (u32)atoi(f);
-    if (const char* f = getenv("FR_ABLATE")) ctx->ablate = (u32)atoi(f);
     if (const char* f = getenv("FR_NBR")) ctx->nbr_enabled = atoi(f) != 0;
     if (const char* f = getenv("FR_COLD_CAP")) ctx->cold_cap = (u32)std::max(1024, atoi(f));
     if ((e = dalloc(&ctx->cold, 2ull * ctx->cold_cap * (u64)ctx->grid)) != hipSuccess) return bad("cold lists", e);
@@ -669,7 +672,7 @@ void fr_destroy(fr_ctx* ctx) {
                    ctx->tab.exo_off, ctx->tab.exo_len, ctx->tab.exo_pool, ctx->dbuf[0], ctx->dbuf[1], ctx->d_sheet,
                    ctx->d_keys, ctx->d_counts, ctx->d_first, ctx->d_keys_s, ctx->d_counts_s,
                    ctx->d_first_s, ctx->d_pos, ctx->d_perm, ctx->d_rank, ctx->d_counter, ctx->d_temp, ctx->d_bins, ctx->d_binbase, ctx->d_arr, ctx->d_rows, ctx->d_pres_u,
-                   ctx->d_pres_f, ctx->d_m1, ctx->d_m2, ctx->d_row, ctx->d_rm2, ctx->d_rrow, ctx->d_cls, ctx->d_rcls,
+                   ctx->d_pres_f, ctx->d_pres_c, ctx->d_m1, ctx->d_m2, ctx->d_row, ctx->d_rm2, ctx->d_rrow, ctx->d_cls, ctx->d_rcls,
                    ctx->d_errw, ctx->d_errf, ctx->d_nbr, ctx->cold, ctx->rare, ctx->chunk_info, ctx->log, ctx->log_sub, ctx->log_temp};
     for (void* p : dev)
         if (p) (void)hipFree(p);
@@ -854,6 +857,7 @@ int fr_reset(fr_ctx* ctx) {
     ctx->exo_codes.clear();
     ctx->exo_pres_code.clear();
     ctx->exo_pres_file.clear();
+    ctx->exo_pres_count.clear();
     ctx->last_valid = false;
     ctx->ev_used = 0;
     ctx->scan_launches = ctx->scan_bytes = 0;
@@ -1230,12 +1234,14 @@ int fr_finalize(fr_ctx* ctx, uint64_t* n_unique, uint64_t* n_presence, uint64_t*
     if (np > ctx->pmap_cap) {
         if (ctx->d_pres_u) CK(hipFree(ctx->d_pres_u));
         if (ctx->d_pres_f) CK(hipFree(ctx->d_pres_f));
+        if (ctx->d_pres_c) CK(hipFree(ctx->d_pres_c));
         CK(dalloc(&ctx->d_pres_u, np));
         CK(dalloc(&ctx->d_pres_f, np));
+        CK(dalloc(&ctx->d_pres_c, np));
         ctx->pmap_cap = np;
     }
     CK(launch_presence_map(ctx->tab.slots, ctx->tab.mask, ctx->tab.pres, np, ctx->d_pres_u, ctx->d_pres_f,
-                           ctx->stream));
+                           ctx->d_pres_c, ctx->stream));
     *ctx->h_fin = 0;
     if (nbins)  // the scan's last entry: every live slot counted once
         CK(hipMemcpyAsync(ctx->h_fin, ctx->d_binbase + nbins, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
@@ -1269,6 +1275,29 @@ int fr_get_presence(fr_ctx* ctx, uint32_t* unique_idx, uint32_t* file_idx) {
     if (!n) return FR_OK;
     CK(hipMemcpy(unique_idx, ctx->d_pres_u, n * 4, hipMemcpyDeviceToHost));
     CK(hipMemcpy(file_idx, ctx->d_pres_f, n * 4, hipMemcpyDeviceToHost));
+    return FR_OK;
+}
+
+int fr_get_presence_counts(fr_ctx* ctx, uint64_t* counts, uint64_t* exotic_counts) {
+    if (int src = settle_finalize(ctx)) return src;
+    const u64 n = ctx->n_pres;
+    if (counts && n) {
+        // pairs are appended file by file (fr_end_file), so a code's pairs come in file order and its
+        // count in a file is its running count there minus the running count at its previous pair
+        std::vector<u32> u(n);
+        CK(hipMemcpy(u.data(), ctx->d_pres_u, n * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(counts, ctx->d_pres_c, n * 8, hipMemcpyDeviceToHost));
+        std::vector<u64> last(ctx->U, 0);
+        const u64 m = (1ull << (64 - PRES_TAG_BITS)) - 1ull;
+        for (u64 i = 0; i < n; ++i) {
+            if (u[i] >= ctx->U) return fail(ctx, FR_ERR_DEVICE, "presence pair without a unique code");
+            const u64 snap = counts[i];
+            counts[i] = (snap - last[u[i]]) & m;
+            last[u[i]] = snap;
+        }
+    }
+    const u64 ne = ctx->exo_pres_count.size();
+    if (exotic_counts && ne) std::memcpy(exotic_counts, ctx->exo_pres_count.data(), ne * 8);
     return FR_OK;
 }
 

@@ -60,10 +60,15 @@ struct alignas(32) GSlot {           // open-addressing slot, one 32-B sector
     u32 uidx;                        // compact index (set by fr_finalize)
 };
 
+// One (code, file) presence pair, appended by presence_scan_kernel at the file's end (R10), with the
+// code's running count at that moment: the per-file count (the reference's per-file dict,
+// frender.py:171-177) is the difference to the code's previous pair (fr_get_presence_counts).  A file
+// holds < 2^42 records (ordinal offsets are < 2^44 bytes and records >= 4 bytes), so the count kept
+// modulo 2^44 gives exact differences.
+constexpr int PRES_TAG_BITS = 20;    // file tags are < 2^20 (ordinal = tag << 44 | offset)
 struct alignas(16) Presence {
     u64 key;
-    u32 tag;
-    u32 pad;
+    u64 tc;                          // (running count mod 2^44) << 20 | file tag
 };
 
 struct alignas(32) Overflow {
@@ -160,7 +165,6 @@ struct ScanArgs {
     int pre_valid;       // buf[-16..-1] readable (device-split ranges)
     u32 flush_at;        // LDS table key cap: past it, new codes go to the HBM table directly
     i64 max_records;     // -s, <= 0: none
-    u32 ablate;          // timing ablation bits (FR_ABLATE; 0 in production): 1 parse, 2 encode, 4 insert
     u32 chunk_tiles;     // chunk kernel: tiles per chunk (a workgroup's contiguous unit)
     u32 num_chunks;
     u32 ramp_g;          // 0: uniform chunks of chunk_tiles.  Else the first ramp_g chunks grow and the
@@ -272,7 +276,7 @@ hipError_t launch_order(const u64* first_in, const u32* pos_in, u64 n, u64* firs
 hipError_t launch_gather(const u32* perm, u64 n, const u64* keys, const u64* counts, u64* keys_o,
                          u64* counts_o, u32* rank, hipStream_t s);
 hipError_t launch_presence_map(const GSlot* slots, u64 mask, const Presence* pres, u64 n, u32* uidx,
-                               u32* file_idx, hipStream_t s);
+                               u32* file_idx, u64* snap, hipStream_t s);
 // first-occurrence order by binning (fr_finalize without merged rows)
 struct BinMap {
     u64 span;       // byte span given to each file tag (>= every ordinal offset)
@@ -309,7 +313,7 @@ hipError_t launch_merge(Table t, DevState* st, const u64* keys, const u64* count
 // aggregate the launch log into the table and empty it (stream-ordered; reads log_n and the region
 // cursors on the device)
 hipError_t launch_log_aggregate(Table t, DevState* st, const LogEntry* log, u32 rcap, LogEntry* sub, u32 scap,
-                                u32 file_tag, u64 file_offset, u32 ablate, hipStream_t s);
+                                u32 file_tag, u64 file_offset, hipStream_t s);
 size_t log_aggregate_temp_bytes();
 hipError_t launch_synth(u8* out, u64 r0, u64 n, int R, u64 seed, const u8* idx1, const u8* idx2, int S, int L1,
                         int L2, hipStream_t s);

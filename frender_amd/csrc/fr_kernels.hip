@@ -48,13 +48,17 @@ namespace fr {
 #define FR_TRACE(...) do { } while (0)
 #endif
 
-// FR_OUTLINE_COLD=1 keeps the rare paths out of line (measured slower: the calls make the
-// hot loop save registers to scratch)
-#if FR_OUTLINE_COLD
-#define FR_COLD __attribute__((noinline))
-#else
-#define FR_COLD __forceinline__
+#define FR_COLD __forceinline__  // rare paths stay inline (out of line, the calls made the hot loop spill)
+
+// Timing ablations exist only in experiment builds: scripts/build_exp.sh NAME
+// "-DFR_ABLATE=<bits>" (1 no header parse, 2 no code encode, 4 no LDS insert, 8 no commit flush,
+// 64 commit counts, 128 plain stores in the commit (wrong counts), 256/512/1024 launch-log passes).
+// The product build has FR_ABLATE = 0: every ablation branch folds away at compile time, and nothing
+// read at run time (no environment variable, no kernel argument) can select one.
+#ifndef FR_ABLATE
+#define FR_ABLATE 0
 #endif
+constexpr u32 ABLATE = FR_ABLATE;
 
 // ------------------------------------------------------------------------------------
 // small helpers
@@ -437,7 +441,7 @@ __device__ FR_COLD bool utf8_segment_ok(const ScanArgs& a, int s0, int n) {
 
 template <bool DRAIN = false>
 __device__ __forceinline__ void count_code(ScanShared& sh, const ScanArgs& a, u32 p, u64 key) {
-    if ((a.ablate & 4u) || a.exo_only) {  // ablation / exotic-only replay: skip the hash insert
+    if ((ABLATE & 4u) || a.exo_only) {  // ablation / exotic-only replay: skip the hash insert
         asm volatile("" ::"v"(key));
         return;
     }
@@ -887,7 +891,7 @@ __device__ __forceinline__ void apply_entry(const ScanArgs& a, const Resolved& r
         return;
     }
     GSlot* sl = &T.slots[r.slot];
-    if (a.ablate & 128u) {  // timing ablation: plain stores instead of atomics (wrong counts)
+    if (ABLATE & 128u) {  // timing ablation: plain stores instead of atomics (wrong counts)
         sl->count = cnt;
         return;
     }
@@ -928,14 +932,14 @@ __device__ __attribute__((noinline)) void commit_buffers(ScanShared& sh, const S
     __syncthreads();
     FR_CSTAMP(0);
     u32 made = 0;
-    if (a.ablate & 64u) {  // diag: flushed LDS slots and cold entries per commit
+    if (ABLATE & 64u) {  // diag: flushed LDS slots and cold entries per commit
         u32 live = 0;
         for (int i = tid; i < NS; i += WG) live += sh.ls[i].key != 0;
         if (live) atomicAdd((unsigned long long*)&a.st->stamp[4], (unsigned long long)live);
         if (tid == 0) atomicAdd((unsigned long long*)&a.st->stamp[5], (unsigned long long)min(sh.ncold, a.cold_cap));
         if (tid == 0) atomicAdd((unsigned long long*)&a.st->stamp[6], 1ull);
     }
-    const bool flush = !(a.ablate & 8u);  // ablation 8: no HBM flush of the LDS table / cold list
+    const bool flush = !(ABLATE & 8u);  // ablation 8: no HBM flush of the LDS table / cold list
     const u32 nc = flush ? min(sh.ncold, a.cold_cap) : 0u;
     const u32 nl = flush ? sh.nkeys : 0u;  // claimed LDS slots = the live ones
     // heavy commits (at least log_min pairs: many distinct codes per chunk) go to the launch log,
@@ -1275,7 +1279,7 @@ __device__ __forceinline__ bool encode_uniform(const ScanShared& sh, u32 wid, u3
 __device__ __forceinline__ void parse_header(ScanShared& sh, const ScanArgs& a, u32 wid, u32 tile0, u32 p, u32 bl) {
     u32 start = 0, n = 0;
     const int r = locate_code(sh, wid, p, bl, start, n);
-    if (a.ablate & 2u) {
+    if (ABLATE & 2u) {
         asm volatile("" ::"v"(start), "v"(n), "v"(r));
         return;
     }
@@ -1391,7 +1395,7 @@ __device__ __forceinline__ u64 walk_wave(ScanShared& sh, const ScanArgs& a, u32 
         sh.bcol[wid][lane] = sc.col;
         sh.beol[wid][lane] = sc.eol;
         lds_fence();
-        if (parse && !uniform_flag(sh.spec_bad) && !(a.ablate & 1u)) parse_own_headers(sh, a, t, sc, L0 + lines, lane, wid);
+        if (parse && !uniform_flag(sh.spec_bad) && !(ABLATE & 1u)) parse_own_headers(sh, a, t, sc, L0 + lines, lane, wid);
         lines += sc.wtot;
     }
     lds_fence();
@@ -1940,7 +1944,7 @@ __global__ __launch_bounds__(256) void log_split_kernel(Table t, DevState* st, c
 // the launch's ordinal base and file tag.  The sub-regions partition the codes, so found and claimed
 // slots take plain stores (insert_rows EXCL).  The last workgroup empties the log for the next launch.
 __global__ __launch_bounds__(256) void log_reduce_kernel(Table t, DevState* st, const LogEntry* sub, u32 scap,
-                                                         u32 file_tag, u64 ord0, u32 ablate) {
+                                                         u32 file_tag, u64 ord0) {
     if (st->log_n == 0) return;
     __shared__ AggSlot ls[AGG_LNS];
     u32 made = 0;
@@ -1950,7 +1954,7 @@ __global__ __launch_bounds__(256) void log_reduce_kernel(Table t, DevState* st, 
     const LogEntry* part = sub + (u64)blockIdx.x * scap;
     u64 sink = 0;
     constexpr int LB = 8;  // entries per thread per batch; the next batch's loads fly during this one's fold
-    const u32 nn = (ablate & 512u) ? 0u : n;  // 512: timing ablation
+    const u32 nn = (ABLATE & 512u) ? 0u : n;  // 512: timing ablation
     LogEntry nx[LB];
 #pragma unroll
     for (int q = 0; q < LB; ++q) nx[q] = threadIdx.x + q * 256 < nn ? part[threadIdx.x + q * 256] : LogEntry{0, 0, 0};
@@ -1966,7 +1970,7 @@ __global__ __launch_bounds__(256) void log_reduce_kernel(Table t, DevState* st, 
         for (int q = 0; q < LB; ++q) {
             const LogEntry e = ev[q];
             if (!e.key) continue;
-            if (ablate & 1024u) {  // timing ablation: loads only
+            if (ABLATE & 1024u) {  // timing ablation: loads only
                 sink ^= e.key;
                 continue;
             }
@@ -2000,7 +2004,7 @@ __global__ __launch_bounds__(256) void log_reduce_kernel(Table t, DevState* st, 
     // the distinct codes into the table, FB slots per thread in flight (LDS limits this kernel to two
     // workgroups per CU, so registers are plentiful)
     constexpr int FB = 8;
-    for (int i0 = threadIdx.x; i0 < ((ablate & 256u) ? 0 : AGG_LNS); i0 += FB * 256) {  // 256: timing ablation
+    for (int i0 = threadIdx.x; i0 < ((ABLATE & 256u) ? 0 : AGG_LNS); i0 += FB * 256) {  // 256: timing ablation
         u64 key[FB], ord[FB];
         u32 cnt[FB], tag[FB];
         bool v[FB];
@@ -2031,13 +2035,13 @@ __global__ __launch_bounds__(256) void log_reduce_kernel(Table t, DevState* st, 
 size_t log_aggregate_temp_bytes() { return 0; }
 
 hipError_t launch_log_aggregate(Table t, DevState* st, const LogEntry* log, u32 rcap, LogEntry* sub, u32 scap,
-                                u32 file_tag, u64 file_offset, u32 ablate, hipStream_t s) {
+                                u32 file_tag, u64 file_offset, hipStream_t s) {
     // reads log_n on the device and returns at once when no commit logged (the usual case for
     // low-cardinality runs: only commits of at least ScanArgs::log_min pairs log)
     const u64 ord0 = ((u64)file_tag << ORD_SHIFT) | file_offset;
     hipLaunchKernelGGL(log_split_kernel, dim3(LOG_NR * SPLIT_WGS), dim3(256), 0, s, t, st, log, rcap, sub, scap, file_tag,
                        ord0);
-    hipLaunchKernelGGL(log_reduce_kernel, dim3(LOG_NSUB), dim3(256), 0, s, t, st, sub, scap, file_tag, ord0, ablate);
+    hipLaunchKernelGGL(log_reduce_kernel, dim3(LOG_NSUB), dim3(256), 0, s, t, st, sub, scap, file_tag, ord0);
     return hipGetLastError();  // log_reduce_kernel's last block emptied the log
 }
 
@@ -2166,20 +2170,21 @@ hipError_t launch_set_uidx(GSlot* slots, u64 mask, const u64* keys, u64 n, const
 }
 
 __global__ void presence_map_kernel(const GSlot* slots, u64 mask, const Presence* pres, u64 n, u32* uidx,
-                                    u32* file_idx) {
+                                    u32* file_idx, u64* snap) {
     for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
         const Presence p = pres[i];
         const GSlot* s = table_find(slots, mask, p.key);
         uidx[i] = s ? s->uidx : 0xFFFFFFFFu;
-        file_idx[i] = p.tag - 1u;
+        file_idx[i] = (u32)(p.tc & ((1u << PRES_TAG_BITS) - 1u)) - 1u;
+        snap[i] = p.tc >> PRES_TAG_BITS;
     }
 }
 
 hipError_t launch_presence_map(const GSlot* slots, u64 mask, const Presence* pres, u64 n, u32* uidx,
-                               u32* file_idx, hipStream_t s) {
+                               u32* file_idx, u64* snap, hipStream_t s) {
     if (!n) return hipSuccess;
     const int grid = (int)std::min<u64>((n + 255) / 256, 8192);
-    hipLaunchKernelGGL(presence_map_kernel, dim3(grid), dim3(256), 0, s, slots, mask, pres, n, uidx, file_idx);
+    hipLaunchKernelGGL(presence_map_kernel, dim3(grid), dim3(256), 0, s, slots, mask, pres, n, uidx, file_idx, snap);
     return hipGetLastError();
 }
 
@@ -2285,7 +2290,8 @@ __global__ void merge_kernel(Table t, DevState* st, const u64* keys, const u64* 
 }
 
 // per-file presence (R10) and the per-file distinct-code count (frender.py:175): after a
-// file, exactly the slots whose last_tag is that file's tag hold a code seen in it.  A workgroup
+// file, exactly the slots whose last_tag is that file's tag hold a code seen in it.  Each pair keeps
+// the code's running count (its per-file count is the difference to the code's previous pair).  A workgroup
 // takes PS_K x 256 consecutive slots, one slot per lane per step with all the loads in flight
 // together, reserves its output run with one atomic and writes its hits in slot order.
 constexpr int PS_K = 16;
@@ -2329,8 +2335,9 @@ __global__ __launch_bounds__(CWG) void presence_scan_kernel(const GSlot* slots, 
         if ((hits >> k) & 1u) {
             const u64 kk = bbase + wc[k * (CWG / 64) + wid] + (u64)__popcll(m[k] & below);
             if (kk < cap) {
-                pres[kk].key = slots[b0 + (u64)k * CWG + tid].key;
-                pres[kk].tag = tag;
+                const GSlot* sl = &slots[b0 + (u64)k * CWG + tid];
+                pres[kk].key = sl->key;
+                pres[kk].tc = (sl->count << PRES_TAG_BITS) | (u64)tag;  // count mod 2^44, file tag
             } else {
                 atomicOr(&st->cap_flags, 1u);
             }
@@ -2417,8 +2424,8 @@ __device__ __forceinline__ void class_pair(W q1, W q2, const W* s1, const W* s2,
         rm2 = -1;
         rrow = -1;
     }
-    if (cls == CLS_UNDET) {
-        m1 = -1;
+    if (cls == CLS_UNDET) {  // pass A keeps matched_idx1 from the rc call (frender.py:319-323)
+        if (rcls == CLS_UNDET) m1 = -1;
         m2 = -1;
     }
 }
@@ -2465,8 +2472,8 @@ __device__ __forceinline__ void class_pair_s(W q1, W q2, const u64* __restrict__
         rm2 = -1;
         rrow = -1;
     }
-    if (cls == CLS_UNDET) {
-        m1 = -1;
+    if (cls == CLS_UNDET) {  // pass A keeps matched_idx1 from the rc call (frender.py:319-323)
+        if (rcls == CLS_UNDET) m1 = -1;
         m2 = -1;
     }
 }
@@ -2627,8 +2634,8 @@ __device__ __forceinline__ void class_pair_nbr(const NbrMap& nm, int a1, int a2,
         rm2 = -1;
         rrow = -1;
     }
-    if (cls == CLS_UNDET) {
-        m1 = -1;
+    if (cls == CLS_UNDET) {  // pass A keeps matched_idx1 from the rc call (frender.py:319-323)
+        if (rcls == CLS_UNDET) m1 = -1;
         m2 = -1;
     }
 }
@@ -2850,6 +2857,7 @@ __global__ void classify_cp_kernel(int n, const u32* q1, const int32_t* q1len, c
             int rm1;
             class_of_cp(q1 + (u64)u * stride, n1, q2 + (u64)u * stride, n2, s1, s2rc, stride, S, nsubs, rm1, rm2,
                         rcls, rrow);
+            if (cls == CLS_UNDET && rcls != CLS_UNDET) m1 = rm1;  // matched_idx1 of pass A (frender.py:319-323)
             if (cls == CLS_DEMUX && rcls == CLS_DEMUX && name[row] != name[rrow]) {
                 cls = rcls = CLS_AMBIG;
                 row = rrow = -1;

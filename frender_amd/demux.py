@@ -438,11 +438,13 @@ def _demux_ranks(group, args, dev, pairs, results, route_of, keys, vals, names, 
     rank, world = group.get_rank(), group.get_world_size()
     parts = os.path.join(args.d, ".frender-parts")
     mine = list(range(rank, len(pairs), world))
-    gz = _lib.GzPool([str(f) for k in mine for f in pairs[k]], threads=4)
-    dmx = _lib.Demux(_device_index(group))
+    gz = dmx = None
     pool = ThreadPoolExecutor(max_workers=max(2, min(32, len(names) * 2)))
     failed, exc = len(pairs), None
     try:
+        # opened inside the try: a rank whose pool or device fails still joins the collectives below
+        gz = _lib.GzPool([str(f) for k in mine for f in pairs[k]], threads=4)
+        dmx = _lib.Demux(_device_index(group))
         dmx.set_table(keys, vals)
         for j, k in enumerate(mine):
             d = os.path.join(parts, str(k))
@@ -464,8 +466,10 @@ def _demux_ranks(group, args, dev, pairs, results, route_of, keys, vals, names, 
             failed, exc = (mine[0] if mine else len(pairs)), e
     finally:
         pool.shutdown(wait=True)
-        gz.close()
-        dmx.close()
+        if gz is not None:
+            gz.close()
+        if dmx is not None:
+            dmx.close()
     first = int(reduce_min(group, _wire(group), [failed])[0])  # every rank's pairs are done here
     last = min(first, len(pairs) - 1)
     if rank == 0:

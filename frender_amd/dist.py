@@ -223,9 +223,51 @@ def partition_merge_device(dist, device, ctx):
 
 # ---- product path ------------------------------------------------------------------------------
 
+def launch_ranks(n: int, argv: list, cmd: list | None = None) -> int:
+    """`scan|demux --gpus N` (and `bench.py --gpus N`): one child process per GPU (this process never
+    touches a GPU), joined by torch.distributed over 127.0.0.1; rank 0's stdout is the command's.  A
+    rank that fails ends the others; the exit status is rank 0's, or the first failure's.  cmd: the
+    child's program (default `python -m frender_amd`)."""
+    import os
+    import socket
+    import subprocess
+    import sys
+    import time
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([*(cmd or [sys.executable, "-m", "frender_amd"]), *argv], env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    codes = [None] * n
+    while any(c is None for c in codes):
+        for r, p in enumerate(procs):
+            if codes[r] is None:
+                codes[r] = p.poll()
+        if any(c not in (None, 0) for c in codes):  # a failed rank: the others cannot finish
+            time.sleep(2)
+            for r, p in enumerate(procs):
+                if p.poll() is None:
+                    p.terminate()
+            for r, p in enumerate(procs):
+                codes[r] = p.wait()
+            break
+        time.sleep(0.05)
+    return codes[0] if codes[0] else next((c for c in codes if c), 0)
+
+
+
 class PeerFailed(Exception):
     """Raised on ranks > 0 when a scan fails: rank 0 raises the reference's exception, in the
     reference's order, and the launcher exits with rank 0's status."""
+
+
+class _Skip(Exception):
+    """Internal: skip this rank's local table after a recorded failure."""
 
 
 def world_group():
@@ -271,16 +313,17 @@ def plan_shards(files, world: int, sample=None) -> list:
     return [[u] for u in units]
 
 
-def _exo_blob(ecodes, ecounts, efirst, epc, epf) -> bytes:
+def _exo_blob(ecodes, ecounts, efirst, epc, epf, epn) -> bytes:
     """This rank's exotic-code table as bytes: counts, then per code (length, count, first), the
-    (code, file) presence pairs and the code bytes (no pickling)."""
+    (code, file, reads in the file) presence triples and the code bytes (no pickling)."""
     import numpy as np
 
     n, m = len(ecodes), len(epc)
     head = np.array([n, m], dtype=np.int64)
     meta = np.array([[len(c), int(k), int(f)] for c, k, f in zip(ecodes, ecounts, efirst)],
                     dtype=np.uint64).reshape(-1, 3)
-    pairs = np.stack([np.asarray(epc, np.int64), np.asarray(epf, np.int64)], 1) if m else np.zeros((0, 2), np.int64)
+    pairs = (np.stack([np.asarray(epc, np.int64), np.asarray(epf, np.int64), np.asarray(epn, np.int64)], 1) if m
+             else np.zeros((0, 3), np.int64))
     return head.tobytes() + meta.tobytes() + pairs.tobytes() + b"".join(bytes(c) for c in ecodes)
 
 
@@ -291,37 +334,40 @@ def _exo_unblob(blob: bytes):
     o = 16
     meta = np.frombuffer(blob[o:o + 24 * n], dtype=np.uint64).reshape(n, 3)
     o += 24 * n
-    pairs = np.frombuffer(blob[o:o + 16 * m], dtype=np.int64).reshape(m, 2)
-    o += 16 * m
+    pairs = np.frombuffer(blob[o:o + 24 * m], dtype=np.int64).reshape(m, 3)
+    o += 24 * m
     codes = []
     for ln in meta[:, 0].tolist():
         codes.append(blob[o:o + ln])
         o += ln
-    return codes, meta[:, 1], meta[:, 2], pairs[:, 0], pairs[:, 1]
+    return codes, meta[:, 1], meta[:, 2], pairs[:, 0], pairs[:, 1], pairs[:, 2]
 
 
 def _merge_exotic(blobs):
     """Rank 0: the exotic codes of every rank merged by byte string (count = sum, first = min,
-    presence = union), in first-seen order (build_table orders them by first ordinal)."""
+    presence = union, per-file reads = sum), in first-seen order (build_table orders them by first
+    ordinal)."""
     import numpy as np
 
     exo: dict = {}
     for b in blobs:
-        codes, counts, first, pc, pf = _exo_unblob(b)
+        codes, counts, first, pc, pf, pn = _exo_unblob(b)
         for c, k, f in zip(codes, counts.tolist(), first.tolist()):
-            e = exo.setdefault(c, [0, (1 << 64) - 1, set()])
+            e = exo.setdefault(c, [0, (1 << 64) - 1, {}])
             e[0] += int(k)
             e[1] = min(e[1], int(f))
-        for c, f in zip(pc.tolist(), pf.tolist()):
-            exo[codes[c]][2].add(int(f))
+        for c, f, k in zip(pc.tolist(), pf.tolist(), pn.tolist()):
+            per = exo[codes[c]][2]
+            per[int(f)] = per.get(int(f), 0) + int(k)
     ecodes = list(exo)
     return (ecodes, np.array([exo[c][0] for c in ecodes], dtype=np.uint64),
             np.array([exo[c][1] for c in ecodes], dtype=np.uint64),
             np.array([i for i, c in enumerate(ecodes) for _ in exo[c][2]], dtype=np.int64),
-            np.array([f for c in ecodes for f in sorted(exo[c][2])], dtype=np.int64))
+            np.array([f for c in ecodes for f in sorted(exo[c][2])], dtype=np.int64),
+            np.array([exo[c][2][f] for c in ecodes for f in sorted(exo[c][2])], dtype=np.uint64))
 
 
-ERR_NOSPACE, ERR_UTF8, ERR_GZ = 0, 1, 2  # columns of the per-file error flags
+ERR_NOSPACE, ERR_UTF8, ERR_GZ, ERR_OTHER = 0, 1, 2, 3  # columns of the per-file error flags
 
 
 def sharded_tally(dist, ctx, files, sample, cores):
@@ -340,11 +386,17 @@ def sharded_tally(dist, ctx, files, sample, cores):
     wire = wire_of(dist, ctx)
     F = len(files)
     mine = plan_shards(files, world, sample)[rank]
-    ctx.reset()
+    # Any failure on this rank is recorded, never raised before the collectives below (a rank that
+    # left them would hang its peers): data errors by their file's flags, anything else (a device or
+    # library error) as ERR_OTHER of its file, or of row F when it is tied to no file; the rank that
+    # met it raises it once every rank knows, the others raise PeerFailed.
     records = np.zeros(F, np.int64)
-    flags = np.zeros((F, 3), np.int64)
-    pool = _lib.GzPool([files[fi] for fi, _, _ in mine], threads=max(1, int(cores)))
+    flags = np.zeros((F + 1, 4), np.int64)
+    other: dict = {}  # file index (F: none) -> this rank's exception
+    pool = None
     try:
+        ctx.reset()
+        pool = _lib.GzPool([files[fi] for fi, _, _ in mine], threads=max(1, int(cores)))
         for k, (fi, part, nparts) in enumerate(mine):
             try:
                 if nparts == 1:
@@ -362,49 +414,90 @@ def sharded_tally(dist, ctx, files, sample, cores):
                     ctx.end_file()
                 except Exception:  # noqa: BLE001 - the file is reported through its flag
                     pass
+            except Exception as e:  # noqa: BLE001 - raised after the collectives
+                flags[fi, ERR_OTHER] = 1
+                other.setdefault(fi, e)
+                break  # the context may be unusable: this rank stops tallying
+    except Exception as e:  # noqa: BLE001 - the pool or the reset: no file to blame
+        flags[F, ERR_OTHER] = 1
+        other.setdefault(F, e)
     finally:
-        pool.close()
+        if pool is not None:
+            pool.close()
     # ---- the local table: rows, presence pairs, exotic codes ---------------------------------
-    ctx.finalize()
-    keys, _, _ = ctx.unique()
-    pu, pf = ctx.presence()
-    exo_local = ctx.exotic_table()
-    rows = ctx.export_rows(wire)
-    pairs = torch.as_tensor(np.stack([keys[np.asarray(pu, np.int64)].view(np.int64), np.asarray(pf, np.int64)], 1)
-                            if len(pu) else np.zeros((0, 2), np.int64))
+    empty3 = np.zeros((0, 3), np.int64)
+    try:
+        if other:
+            raise _Skip()
+        ctx.finalize()
+        keys, _, _ = ctx.unique()
+        pu, pf = ctx.presence()
+        exo_local = ctx.exotic_table()
+        pn, epn = ctx.presence_counts(len(exo_local[3]))
+        exo_local = (*exo_local, epn)
+        rows = ctx.export_rows(wire)
+        # (key, file, reads of the key in this rank's share of the file) presence triples
+        pairs = torch.as_tensor(np.stack([keys[np.asarray(pu, np.int64)].view(np.int64), np.asarray(pf, np.int64),
+                                          np.asarray(pn, np.uint64).view(np.int64)], 1)
+                                if len(pu) else empty3)
+    except Exception as e:  # noqa: BLE001 - this rank joins the exchange with nothing
+        if not isinstance(e, _Skip):
+            flags[F, ERR_OTHER] = 1
+            other.setdefault(F, e)
+        rows, pairs = torch.as_tensor(empty3), torch.as_tensor(empty3)
+        exo_local = ([], np.zeros(0, np.uint64), np.zeros(0, np.uint64), np.zeros(0, np.int64), np.zeros(0, np.int64),
+                     np.zeros(0, np.uint64))
     # ---- step 2: every row and pair to the key's owner; the partition's table -----------------
     k64 = torch.zeros(0, dtype=torch.int64)
     my_rows = exchange(dist, wire, rows, owner_of(rows[:, 0], world) if rows.shape[0] else k64)
     my_pairs = exchange(dist, wire, pairs, owner_of(pairs[:, 0], world) if pairs.shape[0] else k64).cpu().numpy()
-    ctx.reset()
-    ctx.merge_rows(my_rows)
-    ctx.finalize()
-    pkeys, pcounts, pfirst = ctx.unique()
+    pkeys = pcounts = pfirst = np.zeros(0, np.uint64)
+    if other:  # a failed rank joins the exchange but keeps nothing
+        my_pairs = my_pairs[:0]
+    else:
+        try:
+            ctx.reset()
+            ctx.merge_rows(my_rows)
+            ctx.finalize()
+            pkeys, pcounts, pfirst = ctx.unique()
+        except Exception as e:  # noqa: BLE001 - raised after the collectives
+            flags[F, ERR_OTHER] = 1
+            other.setdefault(F, e)
+            my_pairs = my_pairs[:0]
     if my_pairs.shape[0]:
-        pk = np.unique(my_pairs, axis=0)  # (key, file), each once
+        pk, inv = np.unique(my_pairs[:, :2], axis=0, return_inverse=True)  # (key, file), each once
+        reads = np.zeros(pk.shape[0], np.int64)
+        np.add.at(reads, inv.reshape(-1), my_pairs[:, 2])  # a file cut into parts: the parts' reads summed
         srt = np.argsort(pkeys.view(np.int64), kind="stable")
         idx = srt[np.searchsorted(pkeys.view(np.int64)[srt], pk[:, 0])]
         o = np.lexsort((pk[:, 1], idx))
-        p_u, p_f = idx[o].astype(np.int64), pk[o, 1]
+        p_u, p_f, p_n = idx[o].astype(np.int64), pk[o, 1], reads[o].astype(np.uint64)
     else:
         p_u = p_f = np.zeros(0, np.int64)
+        p_n = np.zeros(0, np.uint64)
     blobs = gather_bytes(dist, wire, _exo_blob(*exo_local))
     if rank == 0:
-        ecodes, ecounts, efirst, epc, epf = _merge_exotic(blobs)
+        ecodes, ecounts, efirst, epc, epf, epn = _merge_exotic(blobs)
     else:
-        ecodes, ecounts, efirst, epc, epf = [], np.zeros(0, np.uint64), np.zeros(0, np.uint64), \
-            np.zeros(0, np.int64), np.zeros(0, np.int64)
+        ecodes, ecounts, efirst, epc, epf, epn = [], np.zeros(0, np.uint64), np.zeros(0, np.uint64), \
+            np.zeros(0, np.int64), np.zeros(0, np.int64), np.zeros(0, np.uint64)
     # ---- global per-file numbers: records, distinct codes ("new barcodes"), errors -------------
     distinct = np.bincount(p_f, minlength=F)[:F] + np.bincount(epf, minlength=F)[:F] if F else np.zeros(0)
-    records = reduce_sum(dist, wire, records)
-    distinct = reduce_sum(dist, wire, distinct)
-    flags = reduce_max(dist, wire, flags.reshape(-1)).reshape(F, 3) if F else flags
+    # one reduce for records and distinct codes, one for the flags
+    sums = reduce_sum(dist, wire, np.concatenate([records, np.asarray(distinct, np.int64)]))
+    records, distinct = sums[:F], sums[F:]
+    flags = reduce_max(dist, wire, flags.reshape(-1)).reshape(F + 1, 4)
     names = [str(os.path.basename(p)) for p in files]
     # rank 0 decides which file fails first, as one GPU would (a flagged file's replay through
     # Python's gzip may find that the reference reads it fine, e.g. bad bytes past a -s sample)
-    failed = -1
+    failed, err = -1, None
     if rank == 0:
-        for fi in range(F):
+        for fi in range(F + 1):
+            if flags[fi, ERR_OTHER]:  # a library / device failure on some rank: that rank raises it
+                failed = fi
+                break
+            if fi == F:
+                break
             print(f"Tallying barcodes from {names[fi]}...", end="")
             if flags[fi].any():
                 try:
@@ -420,13 +513,15 @@ def sharded_tally(dist, ctx, files, sample, cores):
             print(scan.found_line(int(distinct[fi]), int(records[fi])))
     failed = int(reduce_max(dist, wire, [failed])[0])
     if failed >= 0:
-        if rank == 0:
+        if failed in other:
+            raise other[failed]
+        if rank == 0 and err is not None:
             raise err
-        raise PeerFailed("scan failed (rank 0 reports it)")
+        raise PeerFailed("scan failed (the rank that met it reports it)")
     if rank == 0:
         print(type([]), F)
-    t = {"keys": pkeys, "counts": pcounts, "first": pfirst, "pu": p_u, "pf": p_f, "ecodes": ecodes,
-         "ecounts": ecounts, "efirst": efirst, "epc": epc, "epf": epf}
+    t = {"keys": pkeys, "counts": pcounts, "first": pfirst, "pu": p_u, "pf": p_f, "pn": p_n, "ecodes": ecodes,
+         "ecounts": ecounts, "efirst": efirst, "epc": epc, "epf": epf, "epn": epn}
     table = scan.build_table(t, names, [int(x) for x in records])
     table.group, table.wire = dist, wire
     return table

@@ -22,9 +22,7 @@ from __future__ import annotations
 import csv
 import gzip
 import os
-import queue
 import re
-import threading
 from itertools import islice
 from datetime import datetime, timezone
 from pathlib import Path
@@ -34,7 +32,6 @@ import numpy as np
 from . import _lib
 from .host import find_barcode_file, get_cores, get_indexes, parse_files, reverse_complement
 
-READ_CHUNK = 64 << 20
 UNDET, HOP, DEMUX, AMBIG = 0, 1, 2, 3
 CLASS_NAMES = _lib.CLASS_NAMES
 ORD_SHIFT = 44
@@ -57,7 +54,8 @@ def default_context() -> _lib.Context:
 class UniqueTable:
     """The merged tally: codes in (file, first occurrence) order (R4/R5)."""
 
-    def __init__(self, codes, counts, first, fast_idx, exo_idx, pres_u, pres_f, files, records, key_of=None):
+    def __init__(self, codes, counts, first, fast_idx, exo_idx, pres_u, pres_f, files, records, key_of=None,
+                 pres_n=None):
         self.codes = codes            # list[str], merged order
         self.counts = counts          # uint64
         self.first = first            # uint64 ordinals (file_index+1) << 44 | byte offset
@@ -65,6 +63,7 @@ class UniqueTable:
         self.exo_idx = exo_idx        # merged -> index in the exotic list, or -1
         self.pres_u = pres_u          # (unique, file) presence pairs
         self.pres_f = pres_f
+        self.pres_n = pres_n          # reads of the pair's code in the pair's file (per-file tables)
         self.files = files            # basenames in input order
         self.records = records        # records per file
         self.key_of = key_of          # merged -> packed key (fast / wide codes), 0 for exotic codes
@@ -77,47 +76,6 @@ class UniqueTable:
     def as_dict(self) -> dict:
         """barcode_counter["total"] as a plain dict (small inputs / tests)."""
         return {c: int(n) for c, n in zip(self.codes, self.counts)}
-
-
-class _GzReader:
-    """Inflate one .gz file in a helper thread (zlib releases the GIL) into a bounded queue of
-    decoded chunks.  tally_barcodes keeps up to `cores` of these running ahead of the file the
-    GPU is consuming: the reference parallelises over files with a Pool (frender.py:189-193);
-    here the files inflate in parallel and the GPU tallies them in order."""
-
-    def __init__(self, path, chunk=READ_CHUNK, depth=2):
-        self.q: queue.Queue = queue.Queue(maxsize=depth)
-        self.stop = threading.Event()
-        self.t = threading.Thread(target=self._work, args=(path, chunk), daemon=True)
-        self.t.start()
-
-    def _work(self, path, chunk):
-        try:
-            with gzip.open(path, "rb") as g:
-                while not self.stop.is_set():
-                    b = g.read(chunk)
-                    self.q.put(b)
-                    if not b:
-                        return
-        except BaseException as e:  # noqa: BLE001 - re-raised in the consumer
-            self.q.put(e)
-
-    def __iter__(self):
-        while True:
-            item = self.q.get()
-            if isinstance(item, BaseException):
-                raise item
-            if not item:
-                return
-            yield item
-
-    def close(self):
-        self.stop.set()
-        while self.t.is_alive():
-            try:
-                self.q.get_nowait()
-            except queue.Empty:
-                self.t.join(0.01)
 
 
 def _replay_decode_error(path, sample):
@@ -194,8 +152,9 @@ def local_table(ctx) -> dict:
     keys, counts, first = ctx.unique()
     pu, pf = ctx.presence()
     ecodes, ecounts, efirst, epc, epf = ctx.exotic_table()
-    return {"keys": keys, "counts": counts, "first": first, "pu": pu, "pf": pf,
-            "ecodes": ecodes, "ecounts": ecounts, "efirst": efirst, "epc": epc, "epf": epf}
+    pn, epn = ctx.presence_counts(len(epc))
+    return {"keys": keys, "counts": counts, "first": first, "pu": pu, "pf": pf, "pn": pn,
+            "ecodes": ecodes, "ecounts": ecounts, "efirst": efirst, "epc": epc, "epf": epf, "epn": epn}
 
 
 def build_table(t: dict, names, records) -> UniqueTable:
@@ -219,9 +178,10 @@ def build_table(t: dict, names, records) -> UniqueTable:
     epc, epf = np.asarray(t["epc"], dtype=np.int64), np.asarray(t["epf"], dtype=np.int64)
     pres_u = np.concatenate([pos[pu], pos[nf + epc]])
     pres_f = np.concatenate([pf, epf])
+    pres_n = np.concatenate([np.asarray(t["pn"], dtype=np.uint64), np.asarray(t["epn"], dtype=np.uint64)])
     key_of = np.concatenate([np.asarray(keys, dtype=np.uint64), np.zeros(len(exo_codes), np.uint64)])[order]
     return UniqueTable(codes, np.concatenate([counts, exo_counts])[order], all_first[order], fast_idx, exo_idx,
-                       pres_u, pres_f, list(names), list(records), key_of)
+                       pres_u, pres_f, list(names), list(records), key_of, pres_n)
 
 
 def tally_barcodes(cores, files, sample=None, ctx=None) -> UniqueTable:
@@ -266,6 +226,7 @@ class Results:
             self.rc_row = np.full(n, -1, np.int16)
         self.rc_f = None
         self.rc_r = None
+        self.n_total = n              # codes of the whole scan (all key partitions of a multi-GPU scan)
         self.idx1 = self.idx2 = self.ids = None
         self.names = None
 
@@ -353,10 +314,12 @@ def process(cores, table: UniqueTable, indexes: dict, num_subs: int, rc_mode: bo
         f, r = ctx.rc_counts() if fsel.size else (np.zeros(len(names), np.uint64), np.zeros(len(names), np.uint64))
         res.rc_f = f + f_add
         res.rc_r = r + r_add
-        if table.group is not None:  # the per-name sums of every partition (frender.py:367-373)
+        if table.group is not None:  # the per-name sums of every partition (frender.py:367-373), one reduce
             from .dist import reduce_sum
-            res.rc_f = reduce_sum(table.group, table.wire, res.rc_f.astype(np.int64)).astype(np.uint64)
-            res.rc_r = reduce_sum(table.group, table.wire, res.rc_r.astype(np.int64)).astype(np.uint64)
+            k = len(names)
+            v = reduce_sum(table.group, table.wire, np.concatenate([res.rc_f.astype(np.int64), res.rc_r.astype(np.int64),
+                                                                  [n]]))
+            res.rc_f, res.rc_r, res.n_total = v[:k].astype(np.uint64), v[k:2 * k].astype(np.uint64), int(v[2 * k])
     return res
 
 
@@ -387,7 +350,7 @@ def _first_error_everywhere(table, errs):
 
 def call_rc_mode_per_id(results: Results, ids) -> dict:
     """frender.py:354-388: per distinct name, use rc idx2 iff its reads beat the forward ones."""
-    if len(results.cls) == 0:
+    if results.n_total == 0:  # an empty partition of a non-empty multi-GPU scan is not an empty scan
         raise IndexError("list index out of range")  # results_list[0] on an empty scan (:364)
     assert results.rc, ("It looks like this frender result csv was not generated with the -rc flag. Either specify a "
                         "different result csv, or run this command without setting the -rc flag.")

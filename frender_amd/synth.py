@@ -245,3 +245,27 @@ def make_dataset(outdir: str, sheet: Sheet, n_reads: int, n_files: int = 1, R: i
         write_fastq_gz(p, generate_bytes(sheet, int(a), int(b - a), R=R, seed=seed, rc_names=rc_names), level=level)
         paths.append(p)
     return paths
+
+
+CLASS_NAMES = ("undetermined", "index_hop", "demuxable", "ambiguous")
+
+
+def rows_digest(codes, counts, out, idx1, idx2, ids, keep: int = 1000):
+    """sha256 over a classified unique table in its order, one line per code
+    f"{code}\\t{reads}\\t{matched_idx1}\\t{matched_idx2}\\t{read_type}\\t{sample_name}\\n" (the row format
+    of tests/golden/cfg2_pin.json, which tests/golden/make_golden_cfg2.py computed from the reference's
+    own tally_barcodes + process), plus the first and last `keep` lines.  `out` holds fr_classify's
+    m1 / m2 / cls / row arrays."""
+    import hashlib
+
+    m1, m2, cls, row = (np.asarray(out[k]).tolist() for k in ("m1", "m2", "cls", "row"))
+    h = hashlib.sha256()
+    lines = []
+    n = len(codes)
+    for j, (c, k) in enumerate(zip(codes, np.asarray(counts).tolist())):
+        line = (f"{c}\t{k}\t{idx1[m1[j]] if m1[j] >= 0 else ''}\t{idx2[m2[j]] if m2[j] >= 0 else ''}\t"
+                f"{CLASS_NAMES[cls[j]]}\t{ids[row[j]] if row[j] >= 0 else ''}\n")
+        h.update(line.encode())
+        if j < keep or j >= n - keep:
+            lines.append(line)
+    return h.hexdigest(), lines[:keep], lines[-keep:] if n >= keep else lines

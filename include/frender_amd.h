@@ -168,6 +168,11 @@ int fr_finalize(fr_ctx* ctx, uint64_t* n_unique, uint64_t* n_presence, uint64_t*
 int fr_get_unique(fr_ctx* ctx, uint64_t* keys, uint64_t* counts, uint64_t* first_ordinal);
 /* (unique index, file index) for every file a fast-path key occurs in (R10 demux_ok) */
 int fr_get_presence(fr_ctx* ctx, uint32_t* unique_idx, uint32_t* file_idx);
+/* The reads of each presence pair's code in the pair's file: the values of the reference's per-file
+ * tables, barcode_counter[basename][code] (scan_file's file_barcodes, frender.py:171-177, kept by
+ * tally_barcodes at :204-205).  counts[n_presence] aligns with fr_get_presence, exotic_counts with
+ * fr_get_exotic_table's presence pairs; either may be NULL. */
+int fr_get_presence_counts(fr_ctx* ctx, uint64_t* counts, uint64_t* exotic_counts);
 /* Codes outside both key forms ("exotic": mixed case, other bytes, more than 24 letters, a part
  * longer than 21, two or more '+'), aggregated over the scan by exact byte string inside the
  * library: the device captures each such record's code bytes, the library drains them after the

@@ -98,10 +98,10 @@ class FakeContext:
                 st.exotic += 1
             else:
                 tab = self.tab
-            e = tab.setdefault(key, [0, 1 << 64, set()])
+            e = tab.setdefault(key, [0, 1 << 64, {}])
             e[0] += 1
             e[1] = min(e[1], ordv)
-            e[2].add(self.fi)
+            e[2][self.fi] = e[2].get(self.fi, 0) + 1
             seen.add(key)
             st.records += 1
         st.new_keys = len(seen)
@@ -121,6 +121,12 @@ class FakeContext:
         pu = [i for i, k in enumerate(self.order) for _ in self.tab[k][2]]
         pf = [f for k in self.order for f in sorted(self.tab[k][2])]
         return np.array(pu, dtype=np.uint32), np.array(pf, dtype=np.uint32)
+
+    def presence_counts(self, n_exotic_pairs):
+        c = [self.tab[k][2][f] for k in self.order for f in sorted(self.tab[k][2])]
+        e = [self.exo[k][2][f] for k in self.exo for f in sorted(self.exo[k][2])]
+        assert len(e) == n_exotic_pairs
+        return np.array(c, dtype=np.uint64), np.array(e, dtype=np.uint64)
 
     def exotic_table(self):
         codes = list(self.exo)
@@ -148,7 +154,7 @@ class FakeContext:
     def merge_unique_device(self, kp, cp, fp, n):
         keys, counts, first = (np.frombuffer(self.mem[h], dtype=np.uint64)[:n] for h in (kp, cp, fp))
         for k, c, f in zip(keys.tolist(), counts.tolist(), first.tolist()):
-            e = self.tab.setdefault(k, [0, 1 << 64, set()])
+            e = self.tab.setdefault(k, [0, 1 << 64, {}])
             e[0] += c
             e[1] = min(e[1], f)
 
@@ -166,7 +172,7 @@ class FakeContext:
     def merge_rows(self, rows):
         a = rows.cpu().numpy().view(np.uint64)
         for k, c, f in a.tolist():
-            e = self.tab.setdefault(k, [0, 1 << 64, set()])
+            e = self.tab.setdefault(k, [0, 1 << 64, {}])
             e[0] += c
             e[1] = min(e[1], f)
 

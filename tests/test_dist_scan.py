@@ -53,9 +53,14 @@ def _run(world, rank, files, sheet, flags, out_dir, port, q):
     err = None
     args = argparse.Namespace(n=flags.get("n", 1), rc=flags.get("rc", False), c=2.0, s=flags.get("s"), o="t",
                               p=None, b=sheet, files=list(files))
+    ctx = FakeContext()
+    if flags.get("boom_rank") == rank:  # a library failure on this rank (not a data error)
+        def boom(*a, **k):
+            raise RuntimeError("boom")
+        ctx.end_file = boom
     with contextlib.redirect_stdout(buf):
         try:
-            scan.frender_scan(args, ctx=FakeContext())
+            scan.frender_scan(args, ctx=ctx)
         except Exception as e:  # noqa: BLE001
             err = (type(e).__name__, str(e))
     os.chdir(cwd)
@@ -172,3 +177,40 @@ def test_part_bounds_are_record_starts(tmp_path):
             for j in range(1, k):
                 t = hint * j // k
                 assert b[j] == min([s for s in starts if s >= t] + [len(data)])
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_rc_low_cardinality_empty_partitions(tmp_path, world):
+    """-rc over N ranks when the scan has one or two distinct codes: most key partitions are empty, and
+    an empty partition is not an empty scan (the rc call needs the global count)."""
+    sheet = synth.make_sheet(4, 8, 8)
+    sheet.write_csv(os.path.join(str(tmp_path), "sheet.csv"))
+    files = []
+    for i, codes in enumerate([[f"{sheet.idx1[0]}+{sheet.idx2[0]}"] * 5,
+                               [f"{sheet.idx1[0]}+{sheet.idx2[0]}", f"{sheet.idx1[1]}+{sheet.idx2[1]}"] * 3]):
+        p = os.path.join(str(tmp_path), f"f{i}_R1.fq.gz")
+        synth.write_fastq_gz(p, "".join(f"@r{j} 1:N:0:{c}\nA\n+\nF\n" for j, c in enumerate(codes)).encode())
+        files.append(p)
+    for fs in ([files[0]], files):
+        one = _check(tmp_path, world, fs, {"rc": True, "n": 1})
+        assert one[1] is None and one[0]
+
+
+def test_rank_failure_is_raised_not_hung(tmp_path):
+    """A non-data failure on rank 1 (its context raises) is recorded, rank 1 still joins every
+    collective and raises its own exception afterwards; rank 0 raises PeerFailed; nothing hangs."""
+    files = _inputs(str(tmp_path), seed=5, n_files=3, dup=False)
+    sheet = os.path.join(str(tmp_path), "sheet.csv")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_run, args=(2, r, files, sheet, {"boom_rank": 1}, os.path.join(str(tmp_path), f"r{r}"),
+                                            port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=240) for _ in range(2))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert got[1][1] == ("RuntimeError", "boom")
+    assert got[0][1][0] == "PeerFailed"

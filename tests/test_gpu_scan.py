@@ -320,7 +320,8 @@ def test_classify_random(ctx, lib, nsubs, rc):
     keys, counts, _ = ctx.unique()
     assert lib.decode_keys(keys) == codes
     names, nid = _sheet_names(ids)
-    ctx.set_sheet(idx1, idx2, [reverse_complement(x) for x in idx2], nid, len(names))
+    idx2rc = [reverse_complement(x) for x in idx2]
+    ctx.set_sheet(idx1, idx2, idx2rc, nid, len(names))
     out = ctx.classify(nsubs, rc)
     assert out["err_unique"] == -1
     f_exp = {n: 0 for n in names}
@@ -329,10 +330,11 @@ def test_classify_random(ctx, lib, nsubs, rc):
         e = classify_code(code, 1, idx1, idx2, ids, nsubs, rc)
         got_t = lib.CLASS_NAMES[out["cls"][j]]
         assert got_t == e["read_type"], (code, got_t, e)
-        assert (idx1[out["m1"][j]] if out["m1"][j] >= 0 else "") == e["matched_idx1"] or rc
+        assert (idx1[out["m1"][j]] if out["m1"][j] >= 0 else "") == e["matched_idx1"], (code, e)
         assert (idx2[out["m2"][j]] if out["m2"][j] >= 0 else "") == e["matched_idx2"]
         assert (ids[out["row"][j]] if out["row"][j] >= 0 else "") == e["sample_name"]
         if rc:
+            assert (idx2rc[out["rc_m2"][j]] if out["rc_m2"][j] >= 0 else "") == e["matched_rc_idx2"], (code, e)
             assert lib.CLASS_NAMES[out["rc_cls"][j]] == e["rc_read_type"]
             assert (ids[out["rc_row"][j]] if out["rc_row"][j] >= 0 else "") == e["rc_sample_name"]
             if e["sample_name"]:
@@ -969,3 +971,113 @@ def test_timing_events_off_same_table(lib):
         assert (t.scan_ms > 0) == on and (t.finalize_ms > 0) == on and t.scan_launches > 0
         c.close()
     assert out[0] == out[1]
+
+
+def test_bench_geometry_pinned_to_reference(lib):
+    """bench.py's exact workload and launch geometry (BASELINE config 2: 100M SYN-v1 records in HBM,
+    one device feed cut into two 3.7 GB launches of the 1024-workgroup ramped grid, 4 Mi initial
+    slots, speculative commits, heavy-chunk switch) against the REFERENCE's own tally_barcodes +
+    process on the same records (tests/golden/cfg2_pin.json, tests/golden/make_golden_cfg2.py): the
+    unique-code count, every row in order (sha256) and the first/last 1000 rows verbatim.  Two steps
+    on one context, as the bench runs them."""
+    import json
+
+    from frender_amd import synth
+    from frender_amd.host import reverse_complement
+    from frender_amd.scan import _sheet_names
+
+    with open(os.path.join(os.path.dirname(__file__), "golden", "cfg2_pin.json")) as f:
+        pin = json.load(f)
+    n = pin["reads"]
+    sheet = synth.make_sheet(96, 8, 8)
+    reclen = synth.record_length(8, 8, 8)
+    c = lib.Context(device=0, chunk_bytes=(4 << 30) - (1 << 20), table_slots=1 << 22)
+    buf = c.device_alloc(n * reclen + 64)
+    try:
+        c.synth_device(buf, 0, n, 8, 1, sheet.idx1, sheet.idx2)
+        names, nid = _sheet_names(sheet.ids)
+        for step in range(2):
+            c.set_timing(step == 1)
+            c.reset()
+            c.begin_file(None, file_index=0, byte_base=0)
+            c.feed_device(buf, n * reclen)
+            st = c.end_file()
+            assert st.records == pin["total_reads"] and st.error == 0
+            assert c.timing().scan_launches in (0, 2)
+            U, _, _ = c.finalize()
+            assert U == pin["unique_codes"]
+            keys, counts, _ = c.unique()
+            c.set_sheet(sheet.idx1, sheet.idx2, [reverse_complement(x) for x in sheet.idx2], nid, len(names))
+            out = c.classify(1, False)
+            digest, first, last = synth.rows_digest(lib.decode_keys(keys), counts, out, sheet.idx1, sheet.idx2,
+                                                    sheet.ids)
+            assert first == pin["first_rows"] and last == pin["last_rows"], step
+            assert digest == pin["rows_sha256"], step
+    finally:
+        c.device_free(buf)
+        c.close()
+
+
+@pytest.mark.parametrize("mode", ["host", "device"])
+def test_per_file_counts(lib, mode):
+    """fr_get_presence_counts: the reads of each code in each file (the reference's per-file tables,
+    frender.py:171-177), fast, wide and exotic codes, over several files and a table that grows."""
+    from oracle.frender_oracle import tally_text
+    from frender_amd import synth
+    rng = random.Random(11)
+    sheet = synth.make_sheet(24, 8, 8)
+    files = []
+    for i in range(4):
+        text = synth.generate_bytes(sheet, i * 50000, rng.randint(20000, 60000), R=8, seed=9).decode()
+        extra = "".join(f"@x{j} 1:N:0:{rng.choice(['acgtacgt+ttttcccc', 'AcGt+TTTT', 'ACGTACGTACGT+ACGTACGTAC'])}"
+                        f"\nAC\n+\nFF\n" for j in range(rng.randint(0, 300)))
+        files.append((text + extra).encode())
+    c = lib.Context(device=0, chunk_bytes=1 << 20, table_slots=1 << 12)
+    try:
+        c.reset()
+        for data in files:
+            c.begin_file(None)
+            if mode == "device":
+                p = c.device_alloc(len(data) + 16)
+                c.copy_to_device(p, data)
+                c.feed_device(p, len(data))
+                c.end_file()
+                c.device_free(p)
+            else:
+                c.feed(data)
+                c.end_file()
+        c.finalize()
+        keys, _, _ = c.unique()
+        pu, pf = c.presence()
+        ecodes, _, _, epc, epf = c.exotic_table()
+        pn, epn = c.presence_counts(len(epc))
+        codes = lib.decode_keys(keys)
+        got = {}
+        for u, f, k in zip(pu.tolist(), pf.tolist(), pn.tolist()):
+            got[(codes[u], f)] = k
+        for u, f, k in zip(epc.tolist(), epf.tolist(), epn.tolist()):
+            got[(ecodes[u].decode(), f)] = k
+        exp = {}
+        for f, data in enumerate(files):
+            for code, k in tally_text(data.decode())[0].items():
+                exp[(code, f)] = k
+        assert got == exp
+    finally:
+        c.close()
+
+
+def test_stray_ablation_env_has_no_effect(lib, monkeypatch):
+    """Timing ablations are compile-time only (FR_ABLATE in experiment builds): a stray FR_ABLATE in
+    the environment of the product library changes nothing (128 used to turn the commit's atomics
+    into plain stores)."""
+    from frender_amd import synth
+    sheet = synth.make_sheet(24, 8, 8)
+    data = synth.generate_bytes(sheet, 0, 300000, R=8, seed=4)
+    for v in ("128", "15"):
+        monkeypatch.setenv("FR_ABLATE", v)
+        c = lib.Context(device=0, chunk_bytes=1 << 22, table_slots=1 << 14)
+        try:
+            got = gpu_tally(c, lib, [data])
+        finally:
+            c.close()
+        assert_same(got, oracle_tally([data]))

@@ -35,3 +35,31 @@ def test_synthetic_inputs_are_stable(name):
 def test_oracle_multicore_identical():
     """frender.py:189-193 / :395-411: the Pool fan-out must not change the output."""
     assert not run_case("s96_n1_4files", frender_oracle.scan, extra={"c": 4.0}, check_stdout=False)
+
+
+def test_oracle_cfg2_prefix_pinned():
+    """The oracle on the first 1M records of the benchmarked workload (BASELINE config 2) reproduces
+    the reference's own tally_barcodes + process rows (tests/golden/cfg2_pin_1m.json, made by
+    tests/golden/make_golden_cfg2.py with the reference imported)."""
+    import json
+    from multiprocessing import Pool
+
+    from frender_amd import synth
+    from oracle import frender_oracle as O
+
+    with open(os.path.join(os.path.dirname(__file__), "golden", "cfg2_pin_1m.json")) as f:
+        pin = json.load(f)
+    sheet = synth.make_sheet(96, 8, 8)
+    counts, records = O.tally_text(synth.generate_bytes(sheet, 0, pin["reads"], R=8, seed=1).decode())
+    assert records == pin["total_reads"] and len(counts) == pin["unique_codes"]
+    codes = list(counts)
+    with Pool(4) as pool:
+        res = pool.starmap(O.classify_code, [(c, counts[c], sheet.idx1, sheet.idx2, sheet.ids, 1, False) for c in codes])
+    out = {"m1": [sheet.idx1.index(r["matched_idx1"]) if r["matched_idx1"] else -1 for r in res],
+           "m2": [sheet.idx2.index(r["matched_idx2"]) if r["matched_idx2"] else -1 for r in res],
+           "cls": [synth.CLASS_NAMES.index(r["read_type"]) for r in res],
+           "row": [sheet.ids.index(r["sample_name"]) if r["sample_name"] else -1 for r in res]}
+    digest, first, last = synth.rows_digest(codes, [counts[c] for c in codes], out, sheet.idx1, sheet.idx2,
+                                            sheet.ids, keep=len(pin["first_rows"]))
+    assert first == pin["first_rows"] and last == pin["last_rows"]
+    assert digest == pin["rows_sha256"]

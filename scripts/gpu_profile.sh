@@ -17,8 +17,9 @@ if [[ ${PMC:-1} == 1 ]]; then
   timeout -k 10 400 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES --output-format csv -d "$R/gpurun_out/prof_valu" -o run \
       -- python3 "$R/bench.py" $ARGS > "$R/gpurun_out/prof_valu.log" 2>&1 || { echo "pmc valu failed"; exit 1; }
 fi
-if [[ ${STREAM:-0} == 1 ]]; then  # calibration: FETCH_SIZE of the stream-only ablation (no parse, no table)
-  FR_ABLATE=1 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$R/gpurun_out/prof_fetch_stream" -o run \
+if [[ ${STREAM:-0} == 1 ]]; then  # calibration: FETCH_SIZE of the stream-only ablation (no parse, no table):
+  # the experiment build scripts/build_exp.sh stream "-DFR_ABLATE=1" (ablations are compile-time only)
+  FRENDER_HIP_LIB="$R/frender_amd/libfrender_hip_exp_stream.so" timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$R/gpurun_out/prof_fetch_stream" -o run \
       -- python3 "$R/bench.py" $ARGS > "$R/gpurun_out/prof_fetch_stream.log" 2>&1 || { echo "pmc stream fetch failed"; exit 1; }
 fi
 cd "$R"

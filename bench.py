@@ -46,7 +46,7 @@ def parse():
     ap.add_argument("--nsubs", type=int, default=1)
     ap.add_argument("--rc", action="store_true")
     ap.add_argument("--combinatorial", action="store_true", help="12x8 combinatorial sheet (config 4 shape)")
-    ap.add_argument("--cpu-reads", type=int, default=12_000_000, help="bounded sample for the CPU baseline (~10-25 s on 8 cores)")
+    ap.add_argument("--cpu-reads", type=int, default=24_000_000, help="bounded sample for the CPU baseline (~10-20 s on 8 cores)")
     ap.add_argument("--cpu-cores", type=int, default=8)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--merge", choices=["a2a", "tree"], default="a2a",

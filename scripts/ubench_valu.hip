@@ -1,0 +1,145 @@
+// ubench_valu.hip — wave64 VALU issue rate of the tally kernel's integer instruction mix on gfx950
+// ("what bounds chunk_kernel").
+//
+// Each lane runs ITERS iterations of 8 independent dependency chains of one instruction kind
+// (inline asm, so the instruction and its count are exact), at 1, 2, 4 and 8 waves per SIMD (one
+// workgroup of 256 x W lanes per CU; W = 8 as two workgroups of 1024).  Each wave stamps
+// s_memtime (shader clock) around its loop.  Reported per kind and waves/SIMD:
+//   cyc/inst/wave  = the wave's loop cycles / its instructions (one wave's issue interval)
+//   SIMD issue     = waves per SIMD / cyc/inst/wave  (wave64 instructions per SIMD per cycle)
+//   chip G inst/s  = every wave's instructions / kernel wall time (HIP events)
+// The kinds are the tally loop's: v_and_b32, v_perm_b32 (the 8-entry classify lookups),
+// v_dot4_u32_u8 (bitmap gathers), v_add_u32 with DPP row_shr (line-count scan), v_ffbl_b32 /
+// v_ffbh_u32 (window bit search), v_lshrrev_b64 (64-bit windows), v_alignbit_b32, and "mix": the
+// classify of one dword as the kernel issues it (3 AND-masks, 3 v_perm, 2 AND, 3 v_dot4).
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/ubench_valu.hip -o scripts/ubench_valu
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdint>
+#include <cstdlib>
+#include <vector>
+
+typedef uint32_t u32;
+typedef uint64_t u64;
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
+
+enum { K_AND, K_PERM, K_DOT4, K_DPP, K_FFBL, K_SHR64, K_ALIGN, K_MIX, K_N };
+static const char* NAMES[K_N] = {"v_and_b32", "v_perm_b32", "v_dot4_u32_u8", "v_add_u32 dpp row_shr", "v_ffbl_b32",
+                                  "v_lshrrev_b64", "v_alignbit_b32", "classify mix (11 VALU)"};
+static const int INSTS[K_N] = {1, 1, 1, 1, 1, 1, 1, 11};  // VALU instructions per chain step
+
+template <int K>
+__device__ __forceinline__ void step(u32 (&x)[8], u64 (&y)[8], u32 a, u32 b) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        if constexpr (K == K_AND) {
+            asm volatile("v_and_b32 %0, %0, %1" : "+v"(x[i]) : "v"(a));
+        } else if constexpr (K == K_PERM) {
+            asm volatile("v_perm_b32 %0, %1, %2, %0" : "+v"(x[i]) : "v"(a), "v"(b));
+        } else if constexpr (K == K_DOT4) {
+            asm volatile("v_dot4_u32_u8 %0, %0, %1, %0" : "+v"(x[i]) : "v"(a));
+        } else if constexpr (K == K_DPP) {
+            asm volatile("v_add_u32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "+v"(x[i]));
+        } else if constexpr (K == K_FFBL) {
+            asm volatile("v_ffbl_b32 %0, %0" : "+v"(x[i]));
+        } else if constexpr (K == K_SHR64) {
+            asm volatile("v_lshrrev_b64 %0, 1, %0" : "+v"(y[i]));
+        } else if constexpr (K == K_ALIGN) {
+            asm volatile("v_alignbit_b32 %0, %0, %1, 7" : "+v"(x[i]) : "v"(a));
+        } else {  // the classify of one dword: masks, three 8-entry lookups, two ANDs, three gathers
+            u32 m0, m1, m2, l0, l1, l2;
+            asm volatile(
+                "v_and_b32 %0, 0x07070707, %6\n\t"
+                "v_lshrrev_b32 %1, 3, %6\n\t"
+                "v_and_b32 %1, 0x07070707, %1\n\t"
+                "v_perm_b32 %3, %7, %8, %0\n\t"
+                "v_perm_b32 %4, %8, %7, %1\n\t"
+                "v_lshrrev_b32 %2, 6, %6\n\t"
+                "v_perm_b32 %5, 0, %7, %2\n\t"
+                "v_and_b32 %3, %3, %4\n\t"
+                "v_and_b32 %3, %3, %5\n\t"
+                "v_dot4_u32_u8 %6, %3, %7, %6\n\t"
+                "v_dot4_u32_u8 %6, %3, %8, %6"
+                : "=&v"(m0), "=&v"(m1), "=&v"(m2), "=&v"(l0), "=&v"(l1), "=&v"(l2), "+v"(x[i])
+                : "v"(a), "v"(b));
+        }
+    }
+}
+
+template <int K>
+__global__ void valu_kernel(u32* out, u64* cyc, int iters, u32 a, u32 b) {
+    u32 x[8];
+    u64 y[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        x[i] = threadIdx.x * 7u + i;
+        y[i] = ((u64)x[i] << 32) | x[i];
+    }
+    __syncthreads();
+    const u64 t0 = __builtin_amdgcn_s_memtime();
+    for (int it = 0; it < iters; ++it) step<K>(x, y, a, b);
+    const u64 t1 = __builtin_amdgcn_s_memtime();
+    u32 acc = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc ^= x[i] ^ (u32)y[i] ^ (u32)(y[i] >> 32);
+    out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+    if ((threadIdx.x & 63) == 0) cyc[(blockIdx.x * blockDim.x + threadIdx.x) >> 6] = t1 - t0;
+}
+
+template <int K>
+static void run(int wps, int ncu, int iters) {
+    const int per_wg = wps >= 8 ? 1024 : 256 * wps;
+    const int grid = wps >= 8 ? 2 * ncu : ncu;
+    const int threads = grid * per_wg, waves = threads / 64;
+    u32* out;
+    u64* cyc;
+    CK(hipMalloc(&out, threads * 4));
+    CK(hipMalloc(&cyc, waves * 8));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    hipLaunchKernelGGL(valu_kernel<K>, dim3(grid), dim3(per_wg), 0, 0, out, cyc, iters / 10, 0x08040201u, 0x80402010u);
+    CK(hipDeviceSynchronize());
+    CK(hipEventRecord(e0));
+    hipLaunchKernelGGL(valu_kernel<K>, dim3(grid), dim3(per_wg), 0, 0, out, cyc, iters, 0x08040201u, 0x80402010u);
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    std::vector<u64> c(waves);
+    CK(hipMemcpy(c.data(), cyc, waves * 8, hipMemcpyDeviceToHost));
+    double mean = 0;
+    for (u64 v : c) mean += (double)v;
+    mean /= waves;
+    const double inst_wave = (double)iters * 8 * INSTS[K];
+    const double cpi = mean / inst_wave;
+    const double chip = inst_wave * waves / (ms * 1e-3) / 1e9;
+    printf("%-24s waves/SIMD %d  cyc/inst/wave %6.2f  SIMD issue %5.3f inst/cyc  chip %7.1f G inst/s  (%.3f ms)\n",
+           NAMES[K], wps, cpi, wps / cpi, chip, ms);
+    CK(hipFree(out));
+    CK(hipFree(cyc));
+}
+
+template <int K>
+static void sweep(int ncu, int iters) {
+    for (int w : {1, 2, 4, 8}) run<K>(w, ncu, iters);
+}
+
+int main(int argc, char** argv) {
+    const int iters = argc > 1 ? atoi(argv[1]) : 20000;
+    hipDeviceProp_t p;
+    CK(hipGetDeviceProperties(&p, 0));
+    printf("%s: %d CUs, clock %d kHz; s_memtime counts shader cycles\n", p.gcnArchName, p.multiProcessorCount,
+           p.clockRate);
+    const int ncu = p.multiProcessorCount;
+    sweep<K_AND>(ncu, iters);
+    sweep<K_PERM>(ncu, iters);
+    sweep<K_DOT4>(ncu, iters);
+    sweep<K_DPP>(ncu, iters);
+    sweep<K_FFBL>(ncu, iters);
+    sweep<K_SHR64>(ncu, iters);
+    sweep<K_ALIGN>(ncu, iters);
+    sweep<K_MIX>(ncu, iters / 4);
+    return 0;
+}

@@ -109,6 +109,12 @@ _SIGS = {
     "fr_gz_size_hint": (C.c_uint64, [C.c_char_p]),
     "fr_gz_part_bounds": (C.c_int, [C.c_char_p, C.c_int, C.c_uint64, C.POINTER(C.c_uint64)]),
     "fr_gz_error": (C.c_char_p, [P]),
+    "fr_gz_part_open": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_int),
+                                  u64p, u64p]),
+    "fr_gz_part_data": (C.c_int, [P, C.c_uint64, C.POINTER(C.c_void_p), u64p, u64p, u64p]),
+    "fr_gz_part_feed": (C.c_int, [P, P, C.c_int64, C.c_uint64, u64p]),
+    "fr_gz_part_error": (C.c_char_p, [P]),
+    "fr_gz_part_close": (None, [P]),
     "fr_gz_close": (None, [P]),
     # demux (row f-1)
     "fr_dmx_create": (P, [C.c_int]),
@@ -308,6 +314,64 @@ class GzPool:
             pass
 
 
+class GzPart:
+    """One record part of a BGZF file decoded on its own, without inflating what precedes it
+    (fr_gz_part_*, include/frender_amd.h).  open() returns None for a file that is not BGZF."""
+
+    def __init__(self, h, lines: int, inflated: int):
+        self.h, self.lines, self.inflated = h, lines, inflated
+        self.base = None
+        self.length = None
+
+    @classmethod
+    def open(cls, path, part: int, nparts: int, threads: int = 1):
+        h, bg, lines, infl = C.c_void_p(), C.c_int(), C.c_uint64(), C.c_uint64()
+        rc = lib.fr_gz_part_open(os.fsencode(str(path)), int(part), int(nparts), max(1, int(threads)), C.byref(h),
+                                 C.byref(bg), C.byref(lines), C.byref(infl))
+        if rc == FR_ERR_IO:
+            raise GzError(f"{path}: a BGZF member does not decode")
+        if rc != FR_OK:
+            raise FrenderError(f"fr_gz_part_open failed ({rc})")
+        return cls(h, int(lines.value), int(infl.value)) if bg.value else None
+
+    def _ck(self, rc, what):
+        if rc == FR_ERR_IO:
+            raise GzError(lib.fr_gz_part_error(self.h).decode(errors="replace"))
+        if rc not in (FR_OK, FR_SAMPLE_DONE):
+            raise FrenderError(f"{what} failed ({rc}): {lib.fr_gz_part_error(self.h).decode(errors='replace')}")
+
+    def _cut(self, lines_before: int):
+        d, n, b, infl = C.c_void_p(), C.c_uint64(), C.c_uint64(), C.c_uint64()
+        self._ck(lib.fr_gz_part_data(self.h, int(lines_before), C.byref(d), C.byref(n), C.byref(b), C.byref(infl)),
+                 "fr_gz_part_data")
+        self.inflated, self.base, self.length = int(infl.value), int(b.value), int(n.value)
+        return d, n.value
+
+    def data(self, lines_before: int):
+        """The part's records (bytes) and their file offset, given the terminators before its range."""
+        d, n = self._cut(lines_before)
+        return (C.string_at(d, n) if n else b""), self.base
+
+    def feed(self, ctx_handle, file_index: int, lines_before: int) -> int:
+        """fr_gz_part_feed into a context's scan; returns the part's byte base."""
+        b = C.c_uint64()
+        self._ck(lib.fr_gz_part_feed(self.h, ctx_handle, int(file_index), int(lines_before), C.byref(b)),
+                 "fr_gz_part_feed")
+        self._cut(lines_before)  # the cut is known now: records its size and the bytes inflated
+        return int(b.value)
+
+    def close(self):
+        if self.h:
+            lib.fr_gz_part_close(self.h)
+            self.h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class Demux:
     """One GPU's demux state (fr_dmx): see include/frender_amd.h."""
 
@@ -477,6 +541,13 @@ class Context:
         """Begin file_index at part `part` of `nparts` of pool file i's records and feed that part
         (fr_gz_feed_part; call fr_end_file after); returns the part's byte base."""
         return pool._feed_part(i, self.h, file_index, part, nparts, hint)
+
+    def feed_gz_part_counted(self, part: "GzPart", file_index: int, lines_before: int) -> int:
+        """Begin file_index at a BGZF part's first record and feed its records (fr_gz_part_feed; call
+        fr_end_file after); returns the part's byte base."""
+        base = part.feed(self.h, file_index, lines_before)
+        part.base = base
+        return base
 
     def feed_device(self, dev_ptr: int, nbytes: int):
         self._ck(lib.fr_feed_device(self.h, P(dev_ptr), nbytes), "fr_feed_device")

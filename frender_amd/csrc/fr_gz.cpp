@@ -784,6 +784,320 @@ int fr_gz_feed_part(fr_gz* g, int i, fr_ctx* ctx, int64_t file_index, int part, 
 
 }  // extern "C"
 
+// ---- BGZF record parts without a prefix inflate (multi-GPU scans of fewer files than GPUs) -----
+// A BGZF file's members carry their compressed size (header) and decoded size (trailer), so the
+// decoded offset of every member is known from the headers alone and a rank can decode its own part
+// of the file without inflating what precedes it.  The part's targets are member starts: M_j = the
+// decoded offset of the first member starting at or after j * total / k (M_0 = 0, M_k = total).
+// Record cuts still need the exact line count before them, so the rank first decodes its members
+// [M_j, M_j+1) (plus the member before, for the byte before M_j, and the members after M_j+1 up to the
+// next record start), counts the line terminators whose terminating byte lies in [M_j, M_j+1) (host
+// side), the ranks exchange those counts (frender_amd/dist.py: one all-reduce), and the part is
+// [b_j, b_j+1): b_j = the first record start at or after M_j under the lines before M_j.  Each rank
+// inflates its part plus at most a member or two on either side.  Single-member streams cannot be
+// entered mid-stream (a deflate block's start is unknown without decoding what precedes it):
+// fr_gz_feed_part keeps inflating those from their start.
+
+namespace {
+
+// the member table of a BGZF file from its headers and trailers alone; false when the file is not
+// wholly BGZF members (NUL padding at the end allowed) or cannot be read
+bool bgzf_table(FILE* fp, uint64_t csize, std::vector<Member>& ms) {
+    ms.clear();
+    uint64_t pos = 0, dst = 0;
+    uint8_t h[18];
+    while (pos < csize) {
+        if (fseek(fp, (long)pos, SEEK_SET) != 0 || fread(h, 1, 1, fp) != 1) return false;
+        if (h[0] == 0) {  // trailing NUL padding only
+            std::vector<uint8_t> rest(csize - pos - 1);
+            if (!rest.empty() && fread(rest.data(), 1, rest.size(), fp) != rest.size()) return false;
+            for (uint8_t c : rest)
+                if (c) return false;
+            break;
+        }
+        if (csize - pos < 26 || fseek(fp, (long)pos, SEEK_SET) != 0 || fread(h, 1, 18, fp) != 18) return false;
+        if (h[0] != 0x1f || h[1] != 0x8b || h[2] != 8 || !(h[3] & 4) || le16(h + 10) != 6 || h[12] != 'B' ||
+            h[13] != 'C' || le16(h + 14) != 2)
+            return false;
+        const uint64_t bsize = le16(h + 16) + 1u;
+        uint8_t t[4];
+        if (bsize < 26 || pos + bsize > csize || fseek(fp, (long)(pos + bsize - 4), SEEK_SET) != 0 ||
+            fread(t, 1, 4, fp) != 4)
+            return false;
+        const uint64_t isize = le32(t);
+        if (isize > BGZF_MAX_BLOCK) return false;
+        ms.push_back(Member{(size_t)pos, (size_t)bsize, (size_t)dst, (size_t)isize});
+        dst += isize;
+        pos += bsize;
+    }
+    return !ms.empty();
+}
+
+// decode members [k0, k1) of an open BGZF file into out (member m at m.dst - ms[k0].dst): the
+// compressed bytes of the range are read once, then libdeflate (this thread plus up to threads - 1
+// helpers) or zlib per member
+bool bgzf_decode_range(FILE* fp, const std::vector<Member>& ms, size_t k0, size_t k1, int threads,
+                       std::vector<uint8_t>& out) {
+    out.clear();
+    if (k0 >= k1) return true;
+    const size_t c0 = ms[k0].off, c1 = ms[k1 - 1].off + ms[k1 - 1].len;
+    std::vector<uint8_t> in(c1 - c0);
+    if (fseek(fp, (long)c0, SEEK_SET) != 0 || fread(in.data(), 1, in.size(), fp) != in.size()) return false;
+    const size_t base = ms[k0].dst;
+    out.resize(ms[k1 - 1].dst + ms[k1 - 1].isize - base);
+    const Libdeflate* ld = libdeflate();
+    std::atomic<size_t> next{k0};
+    std::atomic<bool> ok{true};
+    auto run = [&]() {
+        void* d = ld ? ld->alloc() : nullptr;
+        if (ld && !d) {
+            ok = false;
+            return;
+        }
+        for (size_t k; ok && (k = next.fetch_add(1)) < k1;) {
+            const Member& m = ms[k];
+            const uint8_t* src = in.data() + (m.off - c0);
+            uint8_t* dst = out.data() + (m.dst - base);
+            if (ld) {
+                size_t used = 0, produced = 0;
+                const int r = ld->gzip_ex(d, src, m.len, dst, m.isize, &used, &produced);
+                if (r != 0 || used != m.len || produced != m.isize) ok = false;
+            } else {  // zlib, one gzip member (CRC and length checked by inflate)
+                z_stream zs;
+                std::memset(&zs, 0, sizeof(zs));
+                if (inflateInit2(&zs, 16 + MAX_WBITS) != Z_OK) {
+                    ok = false;
+                    continue;
+                }
+                zs.next_in = const_cast<uint8_t*>(src);
+                zs.avail_in = (uInt)m.len;
+                zs.next_out = dst;
+                zs.avail_out = (uInt)m.isize;
+                const int r = inflate(&zs, Z_FINISH);
+                if (r != Z_STREAM_END || zs.avail_in != 0 || zs.total_out != m.isize) ok = false;
+                inflateEnd(&zs);
+            }
+        }
+        if (d) ld->release(d);
+    };
+    const int nh = (int)std::min<size_t>(std::max(threads, 1) - 1, k1 - k0 - 1);
+    std::vector<std::thread> helpers;
+    for (int t = 0; t < nh; ++t) helpers.emplace_back(run);
+    run();
+    for (auto& h : helpers) h.join();
+    return ok;
+}
+
+// first member whose decoded start is at or after x (ms.size() when none)
+size_t member_at_or_after(const std::vector<Member>& ms, uint64_t x) {
+    size_t lo = 0, hi = ms.size();
+    while (lo < hi) {
+        const size_t mid = (lo + hi) / 2;
+        if (ms[mid].dst < x) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+}  // namespace
+
+struct fr_gz_part {
+    FILE* fp = nullptr;
+    std::vector<Member> ms;
+    uint64_t total = 0;         // decoded size of the file
+    uint64_t M0 = 0, M1 = 0;    // the part's member range [M0, M1) (decoded offsets)
+    size_t kn = 0;              // first member not decoded yet (past data's end)
+    uint64_t dbase = 0;         // decoded offset of data[0]
+    std::vector<uint8_t> data;  // decoded bytes [dbase, dbase + data.size())
+    uint64_t lines = 0;         // terminators whose terminating byte lies in [M0, M1)
+    uint64_t inflated = 0;      // decoded bytes produced for this part
+    int threads = 1;
+    std::string err;
+};
+
+namespace {
+
+// decode further members until data reaches at least decoded offset `want` (or the file's end)
+bool part_extend(fr_gz_part* p, uint64_t want) {
+    while (p->dbase + p->data.size() < std::min(want, p->total) && p->kn < p->ms.size()) {
+        size_t k1 = p->kn + 1;
+        while (k1 < p->ms.size() && k1 - p->kn < 16) ++k1;  // a few members at a time
+        std::vector<uint8_t> more;
+        if (!bgzf_decode_range(p->fp, p->ms, p->kn, k1, p->threads, more)) return false;
+        p->inflated += more.size();
+        p->data.insert(p->data.end(), more.begin(), more.end());
+        p->kn = k1;
+    }
+    return true;
+}
+
+// byte at decoded offset x (-1 past the file's end); data must cover it
+inline int part_byte(const fr_gz_part* p, uint64_t x) {
+    if (x >= p->total) return -1;
+    return p->data[x - p->dbase];
+}
+
+// the first record start at or after x, given L = terminators in [0, x) counted with x's own
+// universal-newline convention (a '\r' at x - 1 counts when byte x is not '\n'); p->total when none
+bool part_cut(fr_gz_part* p, uint64_t x, uint64_t L, uint64_t& cut) {
+    if (x == 0) {
+        cut = 0;
+        return true;
+    }
+    if (!part_extend(p, x + 1)) return false;
+    const int prev = part_byte(p, x - 1);
+    const int cur = part_byte(p, x);
+    bool start = prev == '\n' || (prev == '\r' && cur != '\n');
+    uint64_t q = x, lines = L;
+    for (;;) {
+        if (start && (lines & 3u) == 0) {
+            cut = q;
+            return true;
+        }
+        if (q >= p->total) {
+            cut = p->total;
+            return true;
+        }
+        if (q + 2 > p->dbase + p->data.size() && !part_extend(p, q + 2 + (1u << 16))) return false;
+        const int c = part_byte(p, q), nx = part_byte(p, q + 1);
+        start = false;
+        if (c == '\n' || (c == '\r' && nx != '\n')) {
+            ++lines;
+            start = true;
+        }
+        ++q;
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int fr_gz_part_open(const char* path, int part, int nparts, int threads, fr_gz_part** out, int* is_bgzf,
+                    uint64_t* lines, uint64_t* inflated) {
+    *out = nullptr;
+    *is_bgzf = 0;
+    if (!path || nparts < 1 || part < 0 || part >= nparts) return FR_ERR_INVALID;
+    FILE* fp = fopen(path, "rb");
+    if (!fp) return FR_ERR_IO;
+    struct stat sb;
+    std::vector<Member> ms;
+    if (fstat(fileno(fp), &sb) != 0 || !bgzf_table(fp, (uint64_t)sb.st_size, ms)) {
+        fclose(fp);
+        return FR_OK;  // not BGZF: the caller cuts with fr_gz_feed_part
+    }
+    fr_gz_part* p = nullptr;
+    try {
+        p = new fr_gz_part();
+        p->fp = fp;
+        p->ms = std::move(ms);
+        p->threads = std::max(threads, 1);
+        const Member& last = p->ms.back();
+        p->total = last.dst + last.isize;
+        auto target = [&](int j) -> uint64_t {
+            if (j <= 0) return 0;
+            if (j >= nparts) return p->total;
+            const uint64_t t = (uint64_t)((unsigned __int128)p->total * (unsigned)j / (unsigned)nparts);
+            const size_t k = member_at_or_after(p->ms, t);
+            return k < p->ms.size() ? p->ms[k].dst : p->total;
+        };
+        p->M0 = target(part);
+        p->M1 = std::max(target(part + 1), p->M0);
+        // decode from the member before M0 (the byte before the range) through the member at M1
+        size_t k0 = member_at_or_after(p->ms, p->M0);
+        while (k0 > 0 && part > 0 && (k0 >= p->ms.size() || p->ms[k0].dst >= p->M0)) --k0;  // holds byte M0 - 1
+        size_t k1 = member_at_or_after(p->ms, p->M1);
+        k1 = std::min(k1 + 1, p->ms.size());
+        if (k0 < p->ms.size()) {
+            p->dbase = p->ms[k0].dst;
+            if (!bgzf_decode_range(fp, p->ms, k0, std::max(k1, k0 + 1), p->threads, p->data)) {
+                delete p;
+                fclose(fp);
+                return FR_ERR_IO;
+            }
+            p->kn = std::max(k1, k0 + 1);
+        } else {
+            p->dbase = p->total;
+            p->kn = p->ms.size();
+        }
+        p->inflated = p->data.size();
+        // terminators with their terminating byte in [M0, M1): every '\n', and every '\r' not followed
+        // by '\n' (the byte after M1 - 1 is the first of the member at M1, decoded above)
+        uint64_t n = 0;
+        if (p->M1 > p->M0) {
+            const uint8_t* b = p->data.data() + (p->M0 - p->dbase);
+            const size_t len = p->M1 - p->M0;
+            n = (uint64_t)std::count(b, b + len, (uint8_t)'\n');
+            for (const uint8_t* r = (const uint8_t*)std::memchr(b, '\r', len); r;
+                 r = (const uint8_t*)std::memchr(r + 1, '\r', (size_t)(b + len - r - 1)))
+                if (part_byte(p, p->M0 + (uint64_t)(r - b) + 1) != '\n') ++n;
+        }
+        p->lines = n;
+    } catch (const std::bad_alloc&) {
+        if (p) {
+            p->fp = nullptr;
+            delete p;
+        }
+        fclose(fp);
+        return FR_ERR_IO;
+    }
+    *out = p;
+    *is_bgzf = 1;
+    if (lines) *lines = p->lines;
+    if (inflated) *inflated = p->inflated;
+    return FR_OK;
+}
+
+int fr_gz_part_data(fr_gz_part* p, uint64_t lines_before, const uint8_t** data, uint64_t* len, uint64_t* byte_base,
+                    uint64_t* inflated) {
+    *data = nullptr;
+    *len = 0;
+    uint64_t b0 = 0, b1 = 0;
+    try {
+        if (!part_cut(p, p->M0, lines_before, b0) || !part_cut(p, p->M1, lines_before + p->lines, b1)) {
+            p->err = "bgzf member failed to decode";
+            return FR_ERR_IO;
+        }
+        if (b1 < b0) b1 = b0;
+        if (!part_extend(p, b1)) {
+            p->err = "bgzf member failed to decode";
+            return FR_ERR_IO;
+        }
+    } catch (const std::bad_alloc&) {
+        p->err = "out of memory while inflating";
+        return FR_ERR_IO;
+    }
+    if (b1 > b0) {
+        *data = p->data.data() + (b0 - p->dbase);
+        *len = b1 - b0;
+    }
+    if (byte_base) *byte_base = b0;
+    if (inflated) *inflated = p->inflated;
+    return FR_OK;
+}
+
+int fr_gz_part_feed(fr_gz_part* p, fr_ctx* ctx, int64_t file_index, uint64_t lines_before, uint64_t* byte_base) {
+    const uint8_t* d = nullptr;
+    uint64_t n = 0, b0 = 0;
+    int rc = fr_gz_part_data(p, lines_before, &d, &n, &b0, nullptr);
+    if (rc != FR_OK) return rc;
+    if (byte_base) *byte_base = b0;
+    rc = fr_begin_file_at(ctx, file_index, b0, 0);
+    if (rc == FR_OK && n) rc = fr_feed(ctx, d, n);
+    if (rc != FR_OK) p->err = fr_last_error(ctx);
+    return rc;
+}
+
+const char* fr_gz_part_error(const fr_gz_part* p) { return p ? p->err.c_str() : "null part"; }
+
+void fr_gz_part_close(fr_gz_part* p) {
+    if (!p) return;
+    if (p->fp) fclose(p->fp);
+    delete p;
+}
+
+}  // extern "C"
+
 extern "C" {
 
 void fr_gz_close(fr_gz* g) {

@@ -1358,14 +1358,25 @@ __device__ __forceinline__ void parse_own_headers(ScanShared& sh, const ScanArgs
 // (in registers since the previous step) go to the wave's LDS copy first, so the registers take the
 // next tile's loads at once and those stay in flight through this tile's classify AND its parse;
 // the classify reads the lane's segment back from LDS.
-__device__ __forceinline__ u64 walk_wave(ScanShared& sh, const ScanArgs& a, u32 tb, u32 te, u64 L0, bool parse,
+__device__ __forceinline__ const ScanArgs* launder_args(const ScanArgs* p) {
+#ifdef FR_LAUNDER
+    asm volatile("" : "+s"(p));
+#endif
+    return p;
+}
+
+__device__ __forceinline__ u64 walk_wave(ScanShared& sh, const ScanArgs& a0, u32 tb, u32 te, u64 L0, bool parse,
                                          int lane, u32 wid) {
+    const ScanArgs& a = *launder_args(&a0);
     u64 lines = 0;
     u32 done = *(const volatile lds_u32*)&sh.rq_tail[wid];
     SegRegs r;
     if (tb < te) seg_load(a, tb, r, lane);
     lds_u32x4* mine = (lds_u32x4*)(&sh.raw[wid][0]) + lane * (SEG / 16);
     for (u32 t = tb; t < te; ++t) {
+#ifdef FR_LAUNDER
+        const ScanArgs& a = *launder_args(&a0);  // kernel arguments re-read per tile: no long-lived SGPR copies
+#endif
         // the previous tile's parse is done with the LDS copy (program order)
 #pragma unroll
         for (int k = 0; k < SEG / 16; ++k) {

@@ -385,7 +385,8 @@ def sharded_tally(dist, ctx, files, sample, cores):
     rank, world = dist.get_rank(), dist.get_world_size()
     wire = wire_of(dist, ctx)
     F = len(files)
-    mine = plan_shards(files, world, sample)[rank]
+    plan = plan_shards(files, world, sample)
+    mine = plan[rank]
     # Any failure on this rank is recorded, never raised before the collectives below (a rank that
     # left them would hang its peers): data errors by their file's flags, anything else (a device or
     # library error) as ERR_OTHER of its file, or of row F when it is tied to no file; the rank that
@@ -394,16 +395,45 @@ def sharded_tally(dist, ctx, files, sample, cores):
     flags = np.zeros((F + 1, 4), np.int64)
     other: dict = {}  # file index (F: none) -> this rank's exception
     pool = None
+    # Record parts of BGZF files decode on their own (fr_gz_part_open: no inflate of what precedes the
+    # part); their cuts need the line count before each part, so the ranks first count their parts'
+    # lines and exchange the counts (one all-reduce of an F x N matrix, run whenever the plan cuts a
+    # file, so every rank joins it).  Parts of other gzip streams inflate from the file's start
+    # (fr_gz_feed_part): a single deflate stream cannot be entered mid-way.
+    bgzf: dict = {}  # unit index -> GzPart
+    part_lines = np.zeros((F, world), np.int64)
+    for k, (fi, part, nparts) in enumerate(mine):
+        if nparts > 1:
+            try:
+                gp = _lib.GzPart.open(files[fi], part, nparts, threads=max(1, int(cores)))
+                if gp is not None:
+                    bgzf[k] = gp
+                    part_lines[fi, part] = gp.lines
+            except _lib.GzError:
+                flags[fi, ERR_GZ] = 1
+            except Exception as e:  # noqa: BLE001 - raised after the collectives
+                flags[fi, ERR_OTHER] = 1
+                other.setdefault(fi, e)
+    if F and any(u[2] > 1 for units in plan for u in units):
+        part_lines = reduce_sum(dist, wire, part_lines.reshape(-1)).reshape(F, world)
+    inflated = {}  # BGZF parts: decoded bytes produced, and the part's record bytes (diagnostics)
     try:
         ctx.reset()
-        pool = _lib.GzPool([files[fi] for fi, _, _ in mine], threads=max(1, int(cores)))
+        streamed = [k for k in range(len(mine)) if k not in bgzf and not (flags[mine[k][0]].any())]
+        pool = _lib.GzPool([files[mine[k][0]] for k in streamed], threads=max(1, int(cores)))
+        slot = {k: j for j, k in enumerate(streamed)}
         for k, (fi, part, nparts) in enumerate(mine):
+            if k not in bgzf and k not in slot:
+                continue  # failed before the collectives (flagged)
             try:
-                if nparts == 1:
+                if k in bgzf:
+                    ctx.feed_gz_part_counted(bgzf[k], fi, int(part_lines[fi, :part].sum()))
+                    inflated[fi] = (bgzf[k].inflated, bgzf[k].length)
+                elif nparts == 1:
                     ctx.begin_file(sample, file_index=fi)
-                    pool.feed(k, ctx)
+                    pool.feed(slot[k], ctx)
                 else:
-                    ctx.feed_gz_part(pool, k, fi, part, nparts, _lib.GzPool.size_hint(files[fi]))
+                    ctx.feed_gz_part(pool, slot[k], fi, part, nparts, _lib.GzPool.size_hint(files[fi]))
                 st = ctx.end_file()
                 records[fi] += int(st.records)
                 flags[fi, ERR_UTF8] |= 1 if st.utf8_bad else 0
@@ -424,6 +454,8 @@ def sharded_tally(dist, ctx, files, sample, cores):
     finally:
         if pool is not None:
             pool.close()
+        for gp in bgzf.values():
+            gp.close()
     # ---- the local table: rows, presence pairs, exotic codes ---------------------------------
     empty3 = np.zeros((0, 3), np.int64)
     try:
@@ -524,4 +556,5 @@ def sharded_tally(dist, ctx, files, sample, cores):
          "ecounts": ecounts, "efirst": efirst, "epc": epc, "epf": epf, "epn": epn}
     table = scan.build_table(t, names, [int(x) for x in records])
     table.group, table.wire = dist, wire
+    table.inflated = inflated
     return table

@@ -234,6 +234,25 @@ def write_fastq_gz(path: str, data: bytes, level: int = 1, members: int = 1) -> 
                 f.write(gzip.compress(data[a:b], compresslevel=level))
 
 
+def bgzf_bytes(data: bytes, block: int = 65280, level: int = 1) -> bytes:
+    """BGZF (the blocked gzip of htslib / bgzip): independent gzip members of <= 64 KiB of input, each
+    carrying its compressed size in a 'BC' extra subfield, then the empty EOF member.  Python's gzip
+    (and so the reference, frender.py:159) reads it as an ordinary multi-member gzip file."""
+    import struct
+    import zlib
+
+    out = []
+    for i in range(0, len(data), block):
+        chunk = data[i:i + block]
+        co = zlib.compressobj(level, zlib.DEFLATED, -15)
+        body = co.compress(chunk) + co.flush()
+        bsize = 12 + 6 + len(body) + 8
+        out.append(b"\x1f\x8b\x08\x04" + b"\x00" * 4 + b"\x00\xff" + struct.pack("<HBBHH", 6, 66, 67, 2, bsize - 1)
+                   + body + struct.pack("<II", zlib.crc32(chunk), len(chunk) & 0xFFFFFFFF))
+    out.append(bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000"))  # EOF member
+    return b"".join(out)
+
+
 def make_dataset(outdir: str, sheet: Sheet, n_reads: int, n_files: int = 1, R: int = 8, seed: int = 1,
                  rc_names=None, name_fmt: str = "syn_L{f:03d}_R1_001.fastq.gz", level: int = 1) -> list:
     """Split records [0, n_reads) into n_files gz files; return their paths."""

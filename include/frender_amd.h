@@ -146,6 +146,28 @@ int fr_gz_feed_part(fr_gz* g, int i, fr_ctx* ctx, int64_t file_index, int part, 
 /* The cuts fr_gz_feed_part makes: bounds[0..nparts] (b_0 = 0, b_nparts = the decoded size).  Host
  * only (no GPU context): FR_OK, or FR_ERR_IO when the file is not valid gzip. */
 int fr_gz_part_bounds(const char* path, int nparts, uint64_t hint, uint64_t* bounds);
+/* BGZF record parts without a prefix inflate (multi-GPU scans of fewer files than GPUs): a BGZF
+ * file's members give every member's decoded offset from the headers alone, so part `part` of
+ * `nparts` is decoded on its own.  Its member range is [M_part, M_part+1), M_j = the decoded offset of
+ * the first member starting at or after j * total / nparts (M_0 = 0, M_nparts = the decoded size).
+ * fr_gz_part_open decodes that range (threads: this thread plus helpers; libdeflate when present,
+ * else zlib) and returns the line terminators whose terminating byte lies in it (universal newlines,
+ * frender.py:159); *is_bgzf = 0 (and no handle) when the file is not BGZF: cut it with
+ * fr_gz_feed_part instead.  FR_ERR_IO: a member does not decode (the host replays the file through
+ * Python's gzip for the reference's exception).  With lines_before = the terminators before M_part
+ * (the other parts' counts, exchanged by the caller), the part's records are [b_part, b_part+1), b_j =
+ * the first record start at or after M_j: fr_gz_part_data hands them out (host bytes, valid until
+ * fr_gz_part_close), fr_gz_part_feed calls fr_begin_file_at(ctx, file_index, b_part, 0) and fr_feed
+ * with them (the caller then calls fr_end_file).  *inflated: decoded bytes produced for the part so far
+ * (the part plus at most the members around its ends). */
+typedef struct fr_gz_part fr_gz_part;
+int fr_gz_part_open(const char* path, int part, int nparts, int threads, fr_gz_part** out, int* is_bgzf,
+                    uint64_t* lines, uint64_t* inflated);
+int fr_gz_part_data(fr_gz_part* p, uint64_t lines_before, const uint8_t** data, uint64_t* len, uint64_t* byte_base,
+                    uint64_t* inflated);
+int fr_gz_part_feed(fr_gz_part* p, fr_ctx* ctx, int64_t file_index, uint64_t lines_before, uint64_t* byte_base);
+const char* fr_gz_part_error(const fr_gz_part* p);
+void fr_gz_part_close(fr_gz_part* p);
 /* The decoded size of a .gz file as far as its trailers tell (0 when unreadable): exact for BGZF (the
  * members' ISIZE fields) and for a single-member file of up to 4 GiB decoded; otherwise the last
  * member's ISIZE lifted toward 4x the compressed size.  A deterministic fr_gz_feed_part hint. */

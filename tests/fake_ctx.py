@@ -63,6 +63,12 @@ class FakeContext:
         self.feed(data[b[part]:b[part + 1]])
         return b[part]
 
+    def feed_gz_part_counted(self, part, file_index, lines_before) -> int:
+        data, base = part.data(lines_before)
+        self.begin_file(None, file_index=file_index, byte_base=base)
+        self.feed(data)
+        return base
+
     def end_file(self):
         data = bytes(self.buf)
         st = types.SimpleNamespace(records=0, new_keys=0, exotic=0, error=0, utf8_bad=0, lines=0)

@@ -214,3 +214,94 @@ def test_rank_failure_is_raised_not_hung(tmp_path):
         assert p.exitcode == 0
     assert got[1][1] == ("RuntimeError", "boom")
     assert got[0][1][0] == "PeerFailed"
+
+
+def _bgzf_file(d, name, text: bytes, block=4000):
+    p = os.path.join(d, name)
+    with open(p, "wb") as f:
+        f.write(synth.bgzf_bytes(text, block=block))
+    return p
+
+
+@pytest.mark.parametrize("nl", ["\n", "\r\n", "\r"])
+def test_bgzf_part_cuts(tmp_path, nl):
+    """fr_gz_part_open / fr_gz_part_data (host only): the parts of a BGZF file, each decoded on its
+    own with the line counts of the parts before it, are record-aligned and concatenate to the whole
+    decoded file; each part inflates little more than its own bytes (plus the members at its ends)."""
+    import re
+
+    from frender_amd import _lib
+    rng = random.Random(len(nl))
+    recs = [f"@r{i} 1:N:0:ACGT+TTTT\n{'A' * rng.randint(1, 90)}\n+\n" for i in range(6000)]
+    recs = [r + "F" * (len(r.split("\n")[1])) + "\n" for r in recs]
+    data = "".join(recs).replace("\n", nl).encode()
+    p = _bgzf_file(str(tmp_path), "x.fq.gz", data, block=3000)
+    ends = [m.end() for m in re.finditer(rb"\r\n|\r|\n", data)]
+    starts = set([0] + ends[3::4])
+    for k in (1, 2, 3, 7, 40):
+        gps = [_lib.GzPart.open(p, j, k, threads=2) for j in range(k)]
+        assert all(g is not None for g in gps)
+        before, got = 0, b""
+        for j, g in enumerate(gps):
+            chunk, base = g.data(before)
+            assert base == len(got) and (base in starts or base == len(data))
+            got += chunk
+            assert g.inflated <= len(chunk) + 3 * 3000 + 200, (k, j, g.inflated, len(chunk))
+            before += g.lines
+            g.close()
+        assert got == data
+    with open(os.path.join(str(tmp_path), "plain.fq.gz"), "wb") as f:
+        f.write(gzip.compress(data))
+    assert _lib.GzPart.open(os.path.join(str(tmp_path), "plain.fq.gz"), 0, 2) is None  # not BGZF
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_single_bgzf_file_record_shards(tmp_path, world):
+    """Fewer files than ranks, BGZF inputs: every rank decodes only its own part (fr_gz_part_open) and
+    the merged outputs are the single-rank ones (LF and CRLF)."""
+    files = _inputs(str(tmp_path), seed=13, n_files=1, dup=False)
+    with gzip.open(files[0], "rb") as g:
+        text = g.read()
+    for name, t in (("bg_R1.fq.gz", text), ("bgcr_R1.fq.gz", text.replace(b"\n", b"\r\n"))):
+        p = _bgzf_file(str(tmp_path), name, t)
+        one = _check(tmp_path, world, [p], {"rc": True})
+        assert one[1] is None
+
+
+def _inflated_rank(world, rank, path, port, q):
+    from fake_ctx import FakeContext
+
+    from frender_amd import dist as D
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    with contextlib.redirect_stdout(io.StringIO()):
+        t = D.sharded_tally(dist, FakeContext(), [path], None, 2)
+    q.put((rank, t.inflated))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bgzf_parts_inflate_only_their_part(tmp_path):
+    """Each rank's inflated bytes <= 1.1 x its part plus the members at its ends (no prefix inflate)."""
+    files = _inputs(str(tmp_path), seed=17, n_files=1, dup=False)
+    with gzip.open(files[0], "rb") as g:
+        text = g.read() * 4
+    p = _bgzf_file(str(tmp_path), "big_R1.fq.gz", text, block=8000)
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_inflated_rank, args=(world, r, p, port, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    got = dict(q.get(timeout=240) for _ in range(world))
+    for pr in procs:
+        pr.join(60)
+        assert pr.exitcode == 0
+    total = 0
+    for r in range(world):
+        (inflated, part_len), = got[r].values()
+        assert inflated <= 1.1 * part_len + 3 * 8000, (r, inflated, part_len)
+        total += part_len
+    assert total == len(text)

@@ -1081,3 +1081,47 @@ def test_stray_ablation_env_has_no_effect(lib, monkeypatch):
         finally:
             c.close()
         assert_same(got, oracle_tally([data]))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_cli_ranks_bgzf_single_file(tmp_path, world):
+    """`scan --gpus N` on ONE BGZF file: every rank decodes only its part (fr_gz_part_open, no prefix
+    inflate), and the CSVs equal the oracle's (LF and CRLF records, -rc)."""
+    import argparse
+    import contextlib
+    import io
+    import subprocess
+    import sys
+
+    from frender_amd import synth
+    from oracle import frender_oracle
+
+    sheet = synth.make_sheet(24, 8, 8, seed=5)
+    sheet.write_csv(str(tmp_path / "sheet.csv"))
+    raw = synth.generate_bytes(sheet, 0, 400000, R=8, seed=21, rc_names={sheet.ids[2]})
+    for name, data in (("bg_R1.fq.gz", raw), ("bgcr_R1.fq.gz", raw.replace(b"\n", b"\r\n"))):
+        p = tmp_path / name
+        p.write_bytes(synth.bgzf_bytes(data))
+        outs = {}
+        for label in ("gpu", "oracle"):
+            sub = tmp_path / f"{name}_{label}"
+            sub.mkdir()
+            if label == "gpu":
+                env = dict(os.environ, FRENDER_DIST_BACKEND="gloo",
+                           PYTHONPATH=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+                r = subprocess.run([sys.executable, "-m", "frender_amd", "scan", "-n", "1", "-rc", "-c", "4", "-o", "bg",
+                                    "-b", str(tmp_path / "sheet.csv"), "--gpus", str(world), str(p)], cwd=str(sub),
+                                   env=env, capture_output=True, text=True, timeout=240)
+                assert r.returncode == 0, r.stderr[-3000:]
+            else:
+                args = argparse.Namespace(n=1, rc=True, c=1.0, s=None, o="bg", p=None, b=str(tmp_path / "sheet.csv"),
+                                          files=[str(p)])
+                cwd = os.getcwd()
+                os.chdir(sub)
+                try:
+                    with contextlib.redirect_stdout(io.StringIO()):
+                        frender_oracle.scan(args)
+                finally:
+                    os.chdir(cwd)
+            outs[label] = {x: (sub / x).read_bytes() for x in sorted(os.listdir(sub))}
+        assert outs["gpu"] == outs["oracle"] and outs["gpu"]

@@ -114,16 +114,21 @@ def load_traffic(path, tree, per_launch_bytes, samples, index_len, combinatorial
                                             f"{tj.get('traffic_over_algorithmic')}x algorithmic"), tj.get("valu")
 
 
+VALU_PEAK_G = 1228.8  # MI355X_MICROARCH.md:53-54: 1024 SIMD-32s x 2.4 GHz / 2 cycles per wave64 VALU instruction
+VALU_MIX_G = 985.0     # measured: the tally's integer mix at 4 waves/SIMD, 0.401 inst/SIMD-cycle (profiles/r04b_ubench_valu.txt)
+
+
 def valu_roofline(valu, per_launch_ms):
     """The kernel's second bound: VALU issue.  SQ_INSTS_VALU per launch (the same PMC file, same tree)
-    over this run's measured launch time, against 1024 SIMDs x 2.4 GHz / 4 cycles per wave64 VALU
-    instruction.  None without a VALU pass for this tree."""
+    over this run's measured launch time, against the guide's 2-cycle wave64 issue (1229 G/s) and the
+    measured ceiling of the kernel's own instruction mix at its occupancy (scripts/ubench_valu.hip:
+    985 G/s at 4 waves per SIMD).  None without a VALU pass for this tree."""
     if not valu or not valu.get("insts_per_launch") or per_launch_ms <= 0:
         return None
     g = valu["insts_per_launch"] / (per_launch_ms / 1e3) / 1e9
-    peak = valu.get("peak_g_insts_per_s", 614.4)
-    return {"achieved": round(g, 1), "peak": peak, "unit": "G wave64 VALU inst/s", "frac": round(g / peak, 4),
-            "insts_per_record": valu.get("insts_per_record")}
+    return {"achieved": round(g, 1), "peak": VALU_PEAK_G, "unit": "G wave64 VALU inst/s",
+            "frac": round(g / VALU_PEAK_G, 4), "mix_ceiling_4waves": VALU_MIX_G,
+            "frac_of_mix_ceiling": round(g / VALU_MIX_G, 4), "insts_per_record": valu.get("insts_per_record")}
 
 
 def _gz(chunk: bytes) -> bytes:

@@ -220,10 +220,10 @@ constexpr u32 RARE_WAVE = RARE_RING / NW;    // rare-event ring entries per wave
 struct ScanShared {
     u32 raw[NW][TILE / 4];   // each wave's current wave-tile (the parse reads code bytes here)
     LSlot ls[NS];            // LDS hash table of this workgroup's chunk
-    u64 bsp[NW][SEGS + 1];   // per wave, per 64-B segment of its staged tile: ' ' | line-end bitmap
-    u64 bcol[NW][SEGS + 1];  //                                              ':' bitmap
-    u64 beol[NW][SEGS + 1];  //                                              '\r' | '\n' bitmap
-                             // entry SEGS of each stays zero: the window's second segment past the tile
+    u64 bsp[NW][SEGS + 2];   // per wave, per 64-B segment of its staged tile: ' ' | line-end bitmap
+    u64 bcol[NW][SEGS + 2];  //                                              ':' bitmap
+    u64 beol[NW][SEGS + 2];  //                                              '\r' | '\n' bitmap
+                             // entries SEGS, SEGS + 1 stay zero: window words past the tile
     u64 wcount[NW];          // pass 0: line terminators of each wave's part of the chunk
     int wphase[NW];          // pass 0: the phase each wave parsed with (mod 4), -1 count only
     u32 rq_tail[NW];         // rare-event ring: events pushed by each wave (monotonic)
@@ -1222,6 +1222,35 @@ __device__ __forceinline__ u64 window64(u64 x0, u64 x1, u32 b) { return (x0 >> b
 // and the last ':' before it.  0: code at [start, start + n) (tile offsets); 1: no ' '; 2: word-scan
 // fallback (the first ' ' or the token end lies 64 or more bytes on, or the token starts past the
 // staged bytes).
+#ifdef FR_LOC1
+// One LDS round trip: the words of the two windows (w, w+1 of the line-end bitmap; w .. w+2 of the
+// token-end and ':' bitmaps, since the token starts at most 64 bytes past p) are read together.
+__device__ __forceinline__ int locate_code(const ScanShared& sh, u32 wid, u32 p, u32 bl, u32& start, u32& n) {
+    if (p >= bl) return 2;
+    const u32 w = p >> 6, b = p & 63u;
+    const u64 x0 = sh.bsp[wid][w], x1 = sh.bsp[wid][w + 1], x2 = sh.bsp[wid][w + 2];
+    const u64 c0 = sh.bcol[wid][w], c1 = sh.bcol[wid][w + 1], c2 = sh.bcol[wid][w + 2];
+    const u64 e0 = sh.beol[wid][w], e1 = sh.beol[wid][w + 1];
+    const u64 se = window64(x0, x1, b);
+    const u64 eo = window64(e0, e1, b);
+    const u32 f1 = ctz64x(se);
+    const u32 q = p + f1 + 1u;
+    if (f1 >= 64u) return 2;
+    if (ctz64x(eo) == f1) return 1;
+    if (q >= bl) return 2;
+    const bool nxt = (q >> 6) != w;  // the token's window starts in word w + 1
+    const u32 b2 = q & 63u;
+    const u64 se2 = window64(nxt ? x1 : x0, nxt ? x2 : x1, b2);
+    const u64 co2 = window64(nxt ? c1 : c0, nxt ? c2 : c1, b2);
+    const u32 f2 = ctz64x(se2);
+    if (f2 >= 64u) return 2;
+    const int hc = hsb64x(co2 & ((1ull << f2) - 1ull));  // the last ':' of the token, < 0 none
+    const u32 cs = (u32)max(hc + 1, 0);
+    start = q + cs;
+    n = f2 - cs;
+    return 0;
+}
+#else
 __device__ __forceinline__ int locate_code(const ScanShared& sh, u32 wid, u32 p, u32 bl, u32& start, u32& n) {
     if (p >= bl) return 2;
     const u32 w = p >> 6, b = p & 63u;
@@ -1243,6 +1272,7 @@ __device__ __forceinline__ int locate_code(const ScanShared& sh, u32 wid, u32 p,
     n = f2 - cs;
     return 0;
 }
+#endif
 
 // code bytes [start, start + n) from the wave's LDS copy -> fast key, n wave-uniform (nu): the
 // per-word byte masks are scalars and only the words the code reaches are packed
@@ -1499,9 +1529,9 @@ __global__ __launch_bounds__(WG, FR_OCC) void chunk_kernel(ScanArgs args) {
     const u32 wid = wave_id();  // wave-uniform: LDS addresses by wave stay scalar
     for (int i = tid; i < NS; i += WG) sh.ls[i] = LSlot{0, 0, 0xFFFFFFFFu};
     if (lane == 0) {
-        sh.bsp[wid][SEGS] = 0;
-        sh.bcol[wid][SEGS] = 0;
-        sh.beol[wid][SEGS] = 0;
+        sh.bsp[wid][SEGS] = sh.bsp[wid][SEGS + 1] = 0;
+        sh.bcol[wid][SEGS] = sh.bcol[wid][SEGS + 1] = 0;
+        sh.beol[wid][SEGS] = sh.beol[wid][SEGS + 1] = 0;
         sh.rq_tail[wid] = 0;
     }
     if (tid == 0) {

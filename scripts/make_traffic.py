@@ -23,7 +23,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNEL = "fr::chunk_kernel"
-VALU_PEAK_G = 256 * 4 * 2.4 / 4  # G wave64 VALU instructions per second (MI355X: 16-lane SIMDs)
+VALU_PEAK_G = 1228.8  # MI355X_MICROARCH.md:53-54: SIMD-32, one wave64 VALU instruction per 2 cycles per SIMD
 
 
 def rows(pattern):
@@ -78,7 +78,10 @@ def main():
         valu_d = {"insts_per_launch": int(vi), "insts_per_record": round(vi / (reads / launches), 3),
                   "active_quad_cycles_per_launch": int(sum(vact.values()) / len(vact)) if vact else None,
                   "peak_g_insts_per_s": VALU_PEAK_G,
-                  "peak_note": "256 CUs x 4 SIMDs x 2.4 GHz / 4 cycles per wave64 VALU instruction"}
+                  "peak_note": "256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction (MI355X_MICROARCH.md:53-54); "
+                                "measured for the tally's own integer mix at 4 waves/SIMD: 0.401 instructions per SIMD-cycle "
+                                "= 985 G/s (profiles/r04b_ubench_valu.txt, scripts/ubench_valu.hip)",
+                  "mix_ceiling_g_insts_per_s": 985.0}
     out = {
         "round": int(os.environ.get("ROUND", "3")),
         "tree_hash": source_tree_hash(),

@@ -623,7 +623,17 @@ struct SegClass {
     bool hi;                  // a byte >= 0x80 among the own bytes (UTF-8 check, kind 4)
 };
 
+template <class Src>
+__device__ __forceinline__ SegClass seg_classify_src(const ScanArgs& a, u32 t, const Src& src, int lane);
+
 __device__ __forceinline__ SegClass seg_classify(const ScanArgs& a, u32 t, const SegRegs& r, int lane) {
+    return seg_classify_src(a, t, [&](int k) { return r.v[k]; }, lane);
+}
+
+// src(k): the segment's k-th 16 bytes (registers, or a read of the wave's LDS copy: then only one
+// quarter of the segment is live at a time)
+template <class Src>
+__device__ __forceinline__ SegClass seg_classify_src(const ScanArgs& a, u32 t, const Src& src, int lane) {
     const u64 tile0 = (u64)t * TSTEP;
     const u32 tlen = (u32)min((u64)TSTEP, a.len - tile0);
     const u32 bl = (u32)min((u64)TILE, a.avail - tile0);
@@ -637,7 +647,7 @@ __device__ __forceinline__ SegClass seg_classify(const ScanArgs& a, u32 t, const
         u32 acc = 0;
 #pragma unroll
         for (int qv = 0; qv < SEG / 16; ++qv) {  // class words live one quarter at a time
-            const uint4 v = r.v[qv];
+            const uint4 v = src(qv);
             const u32 c0 = classify4(v.x), c1 = classify4(v.y), c2 = classify4(v.z), c3 = classify4(v.w);
             eol16[qv] = gather16<0>(c0, c1, c2, c3);
             sp16[qv] = gather16<2>(c0, c1, c2, c3);
@@ -1415,6 +1425,13 @@ __device__ __forceinline__ u64 walk_wave(ScanShared& sh, const ScanArgs& a0, u32
             mine[k] = v;
         }
         if (t + 1 < te) seg_load(a, t + 1, r, lane);
+#ifdef FR_QREAD
+        // volatile: a real LDS read, one quarter of the segment at a time inside the classify
+        const SegClass sc = seg_classify_src(a, t, [&](int k) {
+            const u32x4 v = *(const volatile lds_u32x4*)&mine[k];
+            return make_uint4(v.x, v.y, v.z, v.w);
+        }, lane);
+#else
         SegRegs q;
 #pragma unroll
         for (int k = 0; k < SEG / 16; ++k) {
@@ -1425,6 +1442,7 @@ __device__ __forceinline__ u64 walk_wave(ScanShared& sh, const ScanArgs& a0, u32
         }
         q.nx = 0;
         const SegClass sc = seg_classify(a, t, q, lane);
+#endif
         if (sc.hi) rare_push(sh, a, (u32)((u64)t * TSTEP) + lane * SEG, 4u,
                              min((u32)min((u64)TSTEP, a.len - (u64)t * TSTEP) - lane * SEG, (u32)SEG), 0u);
         const u32 tail = *(const volatile lds_u32*)&sh.rq_tail[wid];

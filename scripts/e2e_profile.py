@@ -1,4 +1,5 @@
-"""cProfile of one `scan` over 4 x 2M-read .fastq.gz files (where the end-to-end time goes)."""
+"""cProfile of one `scan` over F .fastq.gz files (where the end-to-end time goes).
+usage: e2e_profile.py [reads] [files]  (default 24M reads in 8 files: the bench cpu_baseline / e2e shape)"""
 import cProfile
 import os
 import pstats
@@ -12,7 +13,8 @@ sys.path.insert(0, ROOT)
 from frender_amd import synth  # noqa: E402
 from frender_amd.scan import frender_scan  # noqa: E402
 
-n, files = int(sys.argv[1]) if len(sys.argv) > 1 else 8_000_000, 4
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 24_000_000
+files = int(sys.argv[2]) if len(sys.argv) > 2 else 8
 sheet = synth.make_sheet(96, 8, 8)
 with tempfile.TemporaryDirectory() as d:
     paths = synth.make_dataset(d, sheet, n, n_files=files, R=8, seed=1, level=1)
@@ -26,4 +28,5 @@ with tempfile.TemporaryDirectory() as d:
     frender_scan(args)
     pr.disable()
     print("scan s", round(time.perf_counter() - t0, 3))
-    pstats.Stats(pr).sort_stats("cumulative").print_stats(25)
+    pstats.Stats(pr).sort_stats("cumulative").print_stats(30)
+    pstats.Stats(pr).sort_stats("tottime").print_stats(20)

@@ -4,9 +4,14 @@
 // Each lane runs ITERS iterations of 8 independent dependency chains of one instruction kind
 // (inline asm, so the instruction and its count are exact), at 1, 2, 4 and 8 waves per SIMD (one
 // workgroup of 256 x W lanes per CU; W = 8 as two workgroups of 1024).  Each wave stamps
-// s_memtime (shader clock) around its loop.  Reported per kind and waves/SIMD:
+// s_memtime (shader clock) and s_memrealtime (100 MHz) around its loop.  Each configuration runs
+// back to back for >= 2 s first (MI355X_MICROARCH.md, DVFS give-back item 6).  Reported per kind
+// and waves/SIMD:
 //   cyc/inst/wave  = the wave's loop cycles / its instructions (one wave's issue interval)
 //   SIMD issue     = waves per SIMD / cyc/inst/wave  (wave64 instructions per SIMD per cycle)
+//   clock          = median over waves of d(s_memtime) / d(s_memrealtime) x 100 MHz
+//   overlap        = sum of the waves' loop durations (real time) / (span x 1024 SIMDs): the mean
+//                    number of waves per SIMD actually running together
 //   chip G inst/s  = every wave's instructions / kernel wall time (HIP events)
 // The kinds are the tally loop's: v_and_b32, v_perm_b32 (the 8-entry classify lookups),
 // v_dot4_u32_u8 (bitmap gathers), v_add_u32 with DPP row_shr (line-count scan), v_ffbl_b32 /
@@ -17,6 +22,7 @@
 #include <cstdio>
 #include <cstdint>
 #include <cstdlib>
+#include <algorithm>
 #include <vector>
 
 typedef uint32_t u32;
@@ -68,7 +74,7 @@ __device__ __forceinline__ void step(u32 (&x)[8], u64 (&y)[8], u32 a, u32 b) {
 }
 
 template <int K>
-__global__ void valu_kernel(u32* out, u64* cyc, int iters, u32 a, u32 b) {
+__global__ void valu_kernel(u32* out, u64* cyc, int iters, u32 a, u32 b) {  // cyc: 4 u64 per wave
     u32 x[8];
     u64 y[8];
 #pragma unroll
@@ -77,14 +83,22 @@ __global__ void valu_kernel(u32* out, u64* cyc, int iters, u32 a, u32 b) {
         y[i] = ((u64)x[i] << 32) | x[i];
     }
     __syncthreads();
+    const u64 r0 = __builtin_amdgcn_s_memrealtime();
     const u64 t0 = __builtin_amdgcn_s_memtime();
     for (int it = 0; it < iters; ++it) step<K>(x, y, a, b);
     const u64 t1 = __builtin_amdgcn_s_memtime();
+    const u64 r1 = __builtin_amdgcn_s_memrealtime();
     u32 acc = 0;
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc ^= x[i] ^ (u32)y[i] ^ (u32)(y[i] >> 32);
     out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
-    if ((threadIdx.x & 63) == 0) cyc[(blockIdx.x * blockDim.x + threadIdx.x) >> 6] = t1 - t0;
+    if ((threadIdx.x & 63) == 0) {
+        u64* c = cyc + 4 * ((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+        c[0] = t1 - t0;
+        c[1] = r0;
+        c[2] = r1;
+        c[3] = 0;
+    }
 }
 
 template <int K>
@@ -95,28 +109,55 @@ static void run(int wps, int ncu, int iters) {
     u32* out;
     u64* cyc;
     CK(hipMalloc(&out, threads * 4));
-    CK(hipMalloc(&cyc, waves * 8));
+    CK(hipMalloc(&cyc, waves * 32));
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    hipLaunchKernelGGL(valu_kernel<K>, dim3(grid), dim3(per_wg), 0, 0, out, cyc, iters / 10, 0x08040201u, 0x80402010u);
-    CK(hipDeviceSynchronize());
+    {  // >= 2 s of back-to-back launches first: the clock the chip holds under this load
+        hipEvent_t w0, w1;
+        CK(hipEventCreate(&w0));
+        CK(hipEventCreate(&w1));
+        float tot = 0;
+        while (tot < 2000.f) {
+            CK(hipEventRecord(w0));
+            for (int r = 0; r < 20; ++r)
+                hipLaunchKernelGGL(valu_kernel<K>, dim3(grid), dim3(per_wg), 0, 0, out, cyc, iters, 0x08040201u, 0x80402010u);
+            CK(hipEventRecord(w1));
+            CK(hipEventSynchronize(w1));
+            float m = 0;
+            CK(hipEventElapsedTime(&m, w0, w1));
+            tot += m;
+        }
+    }
     CK(hipEventRecord(e0));
     hipLaunchKernelGGL(valu_kernel<K>, dim3(grid), dim3(per_wg), 0, 0, out, cyc, iters, 0x08040201u, 0x80402010u);
     CK(hipEventRecord(e1));
     CK(hipEventSynchronize(e1));
     float ms = 0;
     CK(hipEventElapsedTime(&ms, e0, e1));
-    std::vector<u64> c(waves);
-    CK(hipMemcpy(c.data(), cyc, waves * 8, hipMemcpyDeviceToHost));
-    double mean = 0;
-    for (u64 v : c) mean += (double)v;
+    std::vector<u64> c(4 * (size_t)waves);
+    CK(hipMemcpy(c.data(), cyc, waves * 32, hipMemcpyDeviceToHost));
+    double mean = 0, busy = 0;
+    u64 rmin = ~0ull, rmax = 0;
+    std::vector<double> clk(waves);
+    for (int w = 0; w < waves; ++w) {
+        mean += (double)c[4 * w];
+        const u64 r0 = c[4 * w + 1], r1 = c[4 * w + 2];
+        rmin = std::min(rmin, r0);
+        rmax = std::max(rmax, r1);
+        busy += (double)(r1 - r0);
+        clk[w] = r1 > r0 ? (double)c[4 * w] / (double)(r1 - r0) * 0.1 : 0.0;  // GHz
+    }
     mean /= waves;
+    std::sort(clk.begin(), clk.end());
+    const double ghz = clk[waves / 2];
+    const double overlap = busy / ((double)(rmax - rmin) * 4.0 * ncu);
     const double inst_wave = (double)iters * 8 * INSTS[K];
     const double cpi = mean / inst_wave;
     const double chip = inst_wave * waves / (ms * 1e-3) / 1e9;
-    printf("%-24s waves/SIMD %d  cyc/inst/wave %6.2f  SIMD issue %5.3f inst/cyc  chip %7.1f G inst/s  (%.3f ms)\n",
-           NAMES[K], wps, cpi, wps / cpi, chip, ms);
+    printf("%-24s waves/SIMD %d  cyc/inst/wave %6.2f  SIMD issue %5.3f inst/cyc  clock %.2f GHz  overlap %.2f  "
+           "chip %7.1f G inst/s  (%.3f ms; span %.3f ms)\n",
+           NAMES[K], wps, cpi, wps / cpi, ghz, overlap, chip, ms, (rmax - rmin) * 1e-5);
     CK(hipFree(out));
     CK(hipFree(cyc));
 }

@@ -71,7 +71,9 @@ def test_bench_refuses_traffic_of_another_tree(tmp_path):
         t, note, v = bench.load_traffic(p, tree, 3.7e9, 96, 8, False)
         assert (t == 4000000000) == ok and (note.startswith("refused") != ok), note
         assert (v == valu) == ok  # the VALU figures travel with the traffic file, under the same checks
-    r = bench.valu_roofline(valu, 1.45)  # 6.82e8 instructions in 1.45 ms against 614.4 G/s
-    assert r["unit"] == "G wave64 VALU inst/s" and abs(r["frac"] - 6.82e8 / 1.45e-3 / 1e9 / 614.4) < 1e-3
+    r = bench.valu_roofline(valu, 1.45)  # 6.82e8 instructions in 1.45 ms against the bench's peaks
+    g = 6.82e8 / 1.45e-3 / 1e9
+    assert r["unit"] == "G wave64 VALU inst/s" and abs(r["frac"] - g / bench.VALU_PEAK_G) < 1e-3
+    assert abs(r["frac_of_mix_ceiling"] - g / bench.VALU_MIX_G) < 1e-3
     assert bench.valu_roofline(None, 1.45) is None
     assert bench.load_traffic(str(tmp_path / "absent.json"), tree, 3.7e9, 96, 8, False)[0] is None

@@ -41,6 +41,7 @@ def source_tree_hash() -> str:
     return h.hexdigest()[:16]
 
 FR_OK = 0
+FR_ERR_INVALID = 1
 FR_SAMPLE_DONE = 5
 FR_ERR_IO = 6
 FR_SCAN_OK, FR_SCAN_NO_SPACE, FR_SCAN_UTF8 = 0, 1, 2
@@ -107,6 +108,8 @@ _SIGS = {
     "fr_gz_next": (C.c_int, [P, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]),
     "fr_gz_feed_part": (C.c_int, [P, C.c_int, P, C.c_int64, C.c_int, C.c_int, C.c_uint64, C.POINTER(C.c_uint64)]),
     "fr_gz_size_hint": (C.c_uint64, [C.c_char_p]),
+    "fr_write_scan_csv": (C.c_int, [C.c_char_p, C.c_char_p, C.c_uint64, P, P, P, P, P, P, P, C.c_char_p, P, P,
+                                    C.c_uint64, P, C.c_char_p, P]),
     "fr_gz_part_bounds": (C.c_int, [C.c_char_p, C.c_int, C.c_uint64, C.POINTER(C.c_uint64)]),
     "fr_gz_error": (C.c_char_p, [P]),
     "fr_gz_part_open": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_int),

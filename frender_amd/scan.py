@@ -21,8 +21,11 @@ from __future__ import annotations
 
 import csv
 import gzip
+import io
+import operator
 import os
 import re
+from collections.abc import Sequence
 from itertools import islice
 from datetime import datetime, timezone
 from pathlib import Path
@@ -157,19 +160,54 @@ def local_table(ctx) -> dict:
             "ecodes": ecodes, "ecounts": ecounts, "efirst": efirst, "epc": epc, "epf": epf, "epn": epn}
 
 
+class Codes(Sequence):
+    """UniqueTable.codes: the code strings in merged order, decoded from the packed keys only when
+    someone reads them (the CSV writer works from the keys: a config-2 scan has ~10^6 codes, and
+    decoding them all to Python strings cost more host time than the GPU's whole tally).  Exotic
+    codes are held as text at their merged positions."""
+
+    def __init__(self, key_of, exo_pos, exo_codes):
+        self._keys = np.asarray(key_of, dtype=np.uint64)
+        self._exo = dict(zip(np.asarray(exo_pos, dtype=np.int64).tolist(), exo_codes))
+        self._list = None
+
+    def __len__(self):
+        return int(self._keys.size)
+
+    def _all(self) -> list:
+        if self._list is None:
+            out = _lib.decode_keys(self._keys)
+            for j, c in self._exo.items():
+                out[j] = c
+            self._list = out
+        return self._list
+
+    def __getitem__(self, j):
+        if self._list is not None or isinstance(j, slice):
+            return self._all()[j]
+        j = operator.index(j)
+        n = len(self)
+        if j < 0:
+            j += n
+        if not 0 <= j < n:
+            raise IndexError("list index out of range")
+        c = self._exo.get(j)
+        return c if c is not None else _lib.decode_keys(self._keys[j:j + 1])[0]
+
+    def __iter__(self):
+        return iter(self._all())
+
+
 def build_table(t: dict, names, records) -> UniqueTable:
     """barcode_counter["total"] (frender.py:199-203) from a finalized tally: keyed and exotic codes
     interleaved in (file, first occurrence) order."""
     keys, counts, first = t["keys"], t["counts"], t["first"]
-    fast_codes = _lib.decode_keys(keys)
     exo_codes = [c.decode("utf-8") for c in t["ecodes"]]
     exo_counts = np.asarray(t["ecounts"], dtype=np.uint64)
     exo_first = np.asarray(t["efirst"], dtype=np.uint64)
     all_first = np.concatenate([first, exo_first])
     order = np.argsort(all_first, kind="stable")
-    nf = len(fast_codes)
-    all_codes = fast_codes + exo_codes
-    codes = [all_codes[i] for i in order.tolist()]
+    nf = len(keys)
     pos = np.empty(order.size, dtype=np.int64)
     pos[order] = np.arange(order.size)
     fast_idx = np.where(order < nf, order, -1)
@@ -180,6 +218,7 @@ def build_table(t: dict, names, records) -> UniqueTable:
     pres_f = np.concatenate([pf, epf])
     pres_n = np.concatenate([np.asarray(t["pn"], dtype=np.uint64), np.asarray(t["epn"], dtype=np.uint64)])
     key_of = np.concatenate([np.asarray(keys, dtype=np.uint64), np.zeros(len(exo_codes), np.uint64)])[order]
+    codes = Codes(key_of, pos[nf:], exo_codes)
     return UniqueTable(codes, np.concatenate([counts, exo_counts])[order], all_first[order], fast_idx, exo_idx,
                        pres_u, pres_f, list(names), list(records), key_of, pres_n)
 
@@ -446,7 +485,8 @@ def call_barcodes_correctly_distributed(table: UniqueTable, results: Results, pr
 def _gather_partitions(table: UniqueTable, results: Results, demux_ok):
     """Multi-GPU: every partition's classified rows on rank 0, in first-occurrence order (int64 rows
     over RCCL: first, key, count, m1, m2, class, row, demux_ok; exotic codes are rank 0's already).
-    Returns (codes, counts, m1, m2, cls, row, demux_ok) lists on rank 0, None elsewhere."""
+    Returns (keys, exotic positions, exotic codes, counts, m1, m2, cls, row, demux_ok) arrays on
+    rank 0 (key 0 at an exotic code's position), None elsewhere."""
     from .dist import gather_rows
 
     import torch
@@ -463,35 +503,86 @@ def _gather_partitions(table: UniqueTable, results: Results, demux_ok):
     allr = np.concatenate(got, 0)
     exo = np.nonzero(table.exo_idx >= 0)[0]
     first = np.concatenate([allr[:, 0].view(np.uint64), table.first[exo]])
-    codes = _lib.decode_keys(allr[:, 1].view(np.uint64)) + [table.codes[j] for j in exo.tolist()]
-    counts = np.concatenate([allr[:, 2], table.counts[exo].view(np.int64)])
+    keys = np.concatenate([allr[:, 1].view(np.uint64), np.zeros(exo.size, np.uint64)])
+    counts = np.concatenate([allr[:, 2].view(np.uint64), table.counts[exo]])
     rest = [np.concatenate([allr[:, 3 + i], np.asarray(c, np.int64)[exo]])
             for i, c in enumerate((results.m1, results.m2, results.cls, results.row, dok))]
     o = np.argsort(first, kind="stable")
-    return ([codes[i] for i in o.tolist()], counts[o].tolist(), *[r[o].tolist() for r in rest[:4]],
-            [bool(x) for x in rest[4][o].tolist()])
+    pos = np.empty(o.size, np.int64)
+    pos[o] = np.arange(o.size)
+    exo_pos = pos[allr.shape[0]:]
+    return (keys[o], exo_pos, [table.codes[j] for j in exo.tolist()], counts[o], rest[0][o].astype(np.int16),
+            rest[1][o].astype(np.int16), rest[2][o].astype(np.uint8), rest[3][o].astype(np.int16),
+            rest[4][o].astype(bool))
+
+
+def _csv_fields(*fields) -> str:
+    """The fields as Python's csv module (excel dialect) writes them inside a row, joined by ','."""
+    buf = io.StringIO()
+    csv.writer(buf).writerow([*fields, "x"])
+    return buf.getvalue()[:-len(",x\r\n")]
+
+
+def _write_csv_native(path, header, keys, exo_pos, exo_codes, counts, m1, m2, cls, row, dok, idx1, idx2, ids) -> bool:
+    """fr_write_scan_csv (fr_csv.cpp): the rows formatted from the packed keys and the classification
+    arrays.  False, with nothing written, when some code does not split on '+' (the caller's row
+    loop then raises the reference's IndexError where the reference does)."""
+    texts = []
+    for c in exo_codes:
+        parts = c.split("+")
+        if len(parts) < 2:
+            return False
+        texts.append(_csv_fields(parts[0], parts[1]).encode("utf-8", "surrogateescape"))
+    ents = [_csv_fields(x).encode("utf-8", "surrogateescape") for x in (*idx1, *idx2, *ids, *CLASS_NAMES)]
+    dict_off = np.concatenate([[0], np.cumsum([len(e) for e in ents])]).astype(np.uint64)
+    dict_n = np.array([len(idx1), len(idx2), len(ids), len(CLASS_NAMES)], np.uint32)
+    eo = np.argsort(np.asarray(exo_pos, np.int64), kind="stable")
+    exo_rows = np.ascontiguousarray(np.asarray(exo_pos, np.uint64)[eo])
+    exo_text = b"".join(texts[i] for i in eo.tolist())
+    exo_off = np.concatenate([[0], np.cumsum([len(texts[i]) for i in eo.tolist()])]).astype(np.uint64)
+    arr = [np.ascontiguousarray(keys, np.uint64), np.ascontiguousarray(counts, np.uint64),
+           np.ascontiguousarray(m1, np.int16), np.ascontiguousarray(m2, np.int16), np.ascontiguousarray(cls, np.uint8),
+           np.ascontiguousarray(row, np.int16)]
+    d = None if dok is None else np.ascontiguousarray(dok, np.uint8)
+    rc = _lib.lib.fr_write_scan_csv(os.fsencode(path), header.encode(), len(arr[0]), *[_lib._ptr(a) for a in arr],
+                                    _lib._ptr(d), b"".join(ents), _lib._ptr(dict_off), _lib._ptr(dict_n),
+                                    len(exo_rows), _lib._ptr(exo_rows), exo_text, _lib._ptr(exo_off))
+    if rc == _lib.FR_ERR_INVALID:
+        return False
+    if rc != 0:
+        raise OSError(f"fr_write_scan_csv failed ({rc}) writing {path}")
+    return True
 
 
 def report_analysis(table: UniqueTable, results: Results, demux_ok, out_csv_name: str) -> None:
     """frender.py:482-501: the scan CSV (excel dialect, columns in the code's order).  On a key
-    partition (multi-GPU) rank 0 gathers every partition's rows and writes the file."""
+    partition (multi-GPU) rank 0 gathers every partition's rows and writes the file.  The rows are
+    formatted natively from the packed keys (fr_write_scan_csv); the row loop below is kept for the
+    codes that do not split on '+', where it raises the reference's IndexError at the same row."""
     if table.group is not None:
         got = _gather_partitions(table, results, demux_ok)
         if got is None:
             return
-        codes, counts, m1, m2, cls, row, dok_all = got
+        keys, exo_pos, exo_codes, counts, m1, m2, cls, row, dok = got
+        dok = dok if demux_ok is not None else None
     else:
-        codes, counts = table.codes, table.counts.tolist()
-        m1, m2, cls, row = results.m1.tolist(), results.m2.tolist(), results.cls.tolist(), results.row.tolist()
-        dok_all = demux_ok.tolist() if demux_ok is not None else None
+        keys, counts = table.key_of, table.counts
+        exo_pos = np.nonzero(table.exo_idx >= 0)[0]
+        exo_codes = [table.codes[j] for j in exo_pos.tolist()]
+        m1, m2, cls, row, dok = results.m1, results.m2, results.cls, results.row, demux_ok
     print(f"Analysis complete! Writing results to {out_csv_name}")
-    if len(codes) == 0:
+    if len(keys) == 0:
         raise IndexError("list index out of range")  # results[0].keys() on an empty scan (:497)
     idx1, idx2, ids = results.idx1, results.idx2, results.ids
     header = ["idx1", "idx2", "matched_idx1", "matched_idx2", "read_type", "sample_name", "reads"]
-    dok = dok_all if demux_ok is not None else None
     if dok is not None:
         header.append("demux_ok")
+    if _write_csv_native(out_csv_name, _csv_fields(*header) + "\r\n", keys, exo_pos, exo_codes, counts, m1, m2, cls,
+                         row, dok, idx1, idx2, ids):
+        return
+    codes = Codes(keys, exo_pos, exo_codes)
+    m1, m2, cls, row, counts = m1.tolist(), m2.tolist(), cls.tolist(), row.tolist(), counts.tolist()
+    dok = None if dok is None else dok.tolist()
 
     def rows():
         for j, code in enumerate(codes):

@@ -172,6 +172,22 @@ void fr_gz_part_close(fr_gz_part* p);
  * members' ISIZE fields) and for a single-member file of up to 4 GiB decoded; otherwise the last
  * member's ISIZE lifted toward 4x the compressed size.  A deterministic fr_gz_feed_part hint. */
 uint64_t fr_gz_size_hint(const char* path);
+
+/* ---- scan CSV (row a9; replaces report_analysis' csv.DictWriter, frender.py:482-501) ------------
+ * Writes header, then one excel-dialect row per unique code: parts[0], parts[1] of code.split("+"),
+ * matched_idx1, matched_idx2, read_type, sample_name, reads[, demux_ok].  keys[j] is row j's packed
+ * key (fr_get_unique form, fast or wide); rows listed in exo_rows (increasing) take their first two
+ * fields from exo_text[exo_off[e], exo_off[e+1]) instead ("p0,p1", already CSV-quoted).  dict holds
+ * the CSV-quoted strings the other fields index: dict_n[0] idx1 entries (m1), dict_n[1] idx2
+ * entries (m2), dict_n[2] sample names (row), dict_n[3] class names (cls); entry i is
+ * dict[dict_off[i], dict_off[i+1]).  Negative m1/m2/row write an empty field; demux_ok NULL omits the
+ * column.  FR_ERR_INVALID (nothing written) when a keyed code has no '+' or an index is out of
+ * range; FR_ERR_IO when the file cannot be written. */
+int fr_write_scan_csv(const char* path, const char* header, uint64_t n_rows, const uint64_t* keys,
+                      const uint64_t* counts, const int16_t* m1, const int16_t* m2, const uint8_t* cls,
+                      const int16_t* row, const uint8_t* demux_ok, const char* dict, const uint64_t* dict_off,
+                      const uint32_t* dict_n, uint64_t n_exotic, const uint64_t* exo_rows, const char* exo_text,
+                      const uint64_t* exo_off);
 const char* fr_gz_error(const fr_gz* g);
 void fr_gz_close(fr_gz* g);
 

@@ -114,15 +114,20 @@ def load_traffic(path, tree, per_launch_bytes, samples, index_len, combinatorial
                                             f"{tj.get('traffic_over_algorithmic')}x algorithmic"), tj.get("valu")
 
 
-VALU_PEAK_G = 1228.8  # MI355X_MICROARCH.md:53-54: 1024 SIMD-32s x 2.4 GHz / 2 cycles per wave64 VALU instruction
-VALU_MIX_G = 985.0     # measured: the tally's integer mix at 4 waves/SIMD, 0.401 inst/SIMD-cycle (profiles/r04b_ubench_valu.txt)
+# The chip's wave64 VALU issue ceiling, measured (scripts/ubench_valu.hip, profiles/r04c_ubench_valu.txt: wall-clock
+# chip rate, in-kernel clock 2.35-2.39 GHz by s_memtime/s_memrealtime): independent v_and_b32 chains top out at
+# 640-647 G inst/s at 2, 4 and 8 waves per SIMD, one wave64 instruction per SIMD every ~3.7 cycles.  The guide's
+# "2 cycles per wave64 instruction" (MI355X_MICROARCH.md:54, 1229 G/s) is the SIMD-32's two passes, not an issue
+# rate this chip sustains for these instructions.
+VALU_PEAK_G = 646.9   # v_and_b32, 4 waves/SIMD (the kernel's occupancy)
+VALU_MIX_G = 626.9    # the tally's classify mix (v_perm, v_dot4, masks), 4 waves/SIMD
 
 
 def valu_roofline(valu, per_launch_ms):
     """The kernel's second bound: VALU issue.  SQ_INSTS_VALU per launch (the same PMC file, same tree)
-    over this run's measured launch time, against the guide's 2-cycle wave64 issue (1229 G/s) and the
-    measured ceiling of the kernel's own instruction mix at its occupancy (scripts/ubench_valu.hip:
-    985 G/s at 4 waves per SIMD).  None without a VALU pass for this tree."""
+    over this run's measured launch time, against the measured chip issue ceiling (647 G/s) and the
+    measured ceiling of the kernel's own instruction mix at its occupancy (627 G/s at 4 waves per SIMD,
+    scripts/ubench_valu.hip).  None without a VALU pass for this tree."""
     if not valu or not valu.get("insts_per_launch") or per_launch_ms <= 0:
         return None
     g = valu["insts_per_launch"] / (per_launch_ms / 1e3) / 1e9

@@ -44,11 +44,74 @@
 
 #include "../../include/frender_amd.h"
 
+// Byte buffers whose resize() does not zero-fill: every byte of a decode buffer is written by the
+// decoder before anything reads it, and zeroing 1-2 GB per scan cost as much as the copies.
+template <class T>
+struct DefaultInit : std::allocator<T> {
+    template <class U>
+    struct rebind {
+        using other = DefaultInit<U>;
+    };
+    DefaultInit() = default;
+    template <class U>
+    DefaultInit(const DefaultInit<U>&) {}
+    template <class U, class... A>
+    void construct(U* p, A&&... a) {
+        if constexpr (sizeof...(A) == 0) ::new ((void*)p) U;
+        else ::new ((void*)p) U(std::forward<A>(a)...);
+    }
+};
+using Bytes = std::vector<uint8_t, DefaultInit<uint8_t>>;
+
 namespace {
+
+// Decode buffers outlive the pool that used them.  A scan inflates GBs into buffers of hundreds of
+// MB; giving them back to the OS at fr_gz_close (munmap) and faulting fresh pages in at the next
+// scan's decode cost ~0.1 s per GB each way.  Released buffers of >= 1 MiB stay here (up to
+// CACHE_MAX bytes of capacity, process-wide) and the next take() of at most their size reuses one.
+class BufCache {
+    static constexpr size_t CACHE_MAX = 4ull << 30;
+    std::mutex m_;
+    std::vector<Bytes> v_;
+    size_t bytes_ = 0;
+
+  public:
+    Bytes take(size_t n) {
+        Bytes b;
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            size_t best = v_.size();
+            for (size_t i = 0; i < v_.size(); ++i)
+                if (v_[i].capacity() >= n && (best == v_.size() || v_[i].capacity() < v_[best].capacity())) best = i;
+            if (best < v_.size()) {
+                b = std::move(v_[best]);
+                v_[best] = std::move(v_.back());
+                v_.pop_back();
+                bytes_ -= b.capacity();
+            }
+        }
+        b.resize(n);
+        return b;
+    }
+    void give(Bytes&& b) {
+        Bytes drop = std::move(b);  // freed outside the lock when it does not stay
+        if (drop.capacity() < (1u << 20)) return;
+        std::lock_guard<std::mutex> lk(m_);
+        if (bytes_ + drop.capacity() > CACHE_MAX) return;
+        bytes_ += drop.capacity();
+        drop.clear();
+        v_.push_back(std::move(drop));
+    }
+};
+
+BufCache& buf_cache() {
+    static BufCache* c = new BufCache();  // never destroyed: no teardown-order questions at exit
+    return *c;
+}
 
 struct GzFile {
     std::string path;
-    std::deque<std::vector<uint8_t>> q;
+    std::deque<Bytes> q;
     bool done = false;
     bool cancel = false;
     std::string err;
@@ -66,12 +129,18 @@ struct fr_gz {
     std::mutex m;
     std::condition_variable cv;
     std::vector<std::thread> workers;
-    std::vector<std::vector<uint8_t>> spare;  // consumed blocks for reuse (no page faults per block)
-    std::vector<uint8_t> held;                // the block fr_gz_next handed out last
+    std::vector<Bytes> spare;  // consumed blocks for reuse (no page faults per block)
+    Bytes held;                // the block fr_gz_next handed out last
     int next = 0;     // next file a worker starts
     int consume = 0;  // file the consumer reads (workers stay within [consume, consume + threads))
     bool stop = false;
     std::string err;
+    ~fr_gz() {  // the buffers stay in the process-wide cache
+        for (auto& f : files)
+            for (auto& b : f.q) buf_cache().give(std::move(b));
+        for (auto& b : spare) buf_cache().give(std::move(b));
+        buf_cache().give(std::move(held));
+    }
 };
 
 namespace {
@@ -116,7 +185,7 @@ inline uint32_t le32(const uint8_t* p) { return le16(p) | (le16(p + 2) << 16); }
 // and its decoded length in the trailer, so the members of one file are found by walking headers
 // alone and decode independently.  True with the member list when the whole file is such members
 // (NUL padding at the end allowed); anything else is not BGZF.
-bool bgzf_members(const std::vector<uint8_t>& in, std::vector<Member>& ms) {
+bool bgzf_members(const Bytes& in, std::vector<Member>& ms) {
     const size_t n = in.size();
     size_t pos = 0, dst = 0;
     ms.clear();
@@ -162,7 +231,7 @@ void give_threads(fr_gz* g, int k) {
 
 // decode BGZF members [k0, k1) in parallel into out (member m lands at m.dst - base): this thread
 // plus the pool's idle threads, each with its own decompressor
-bool bgzf_decode(fr_gz* g, const Libdeflate* ld, const std::vector<uint8_t>& in, const std::vector<Member>& ms,
+bool bgzf_decode(fr_gz* g, const Libdeflate* ld, const Bytes& in, const std::vector<Member>& ms,
                  size_t k0, size_t k1, size_t base, uint8_t* out) {
     std::atomic<size_t> next{k0};
     std::atomic<bool> ok{true};
@@ -215,7 +284,11 @@ bool inflate_whole(fr_gz* g, GzFile& f) {
         size_t b;
         ~Hold() { give_budget(g, b); }
     } hold{g, n};
-    std::vector<uint8_t> in(n);
+    struct In {  // the compressed bytes, back to the cache on every path
+        Bytes b;
+        ~In() { buf_cache().give(std::move(b)); }
+    } hin{buf_cache().take(n)};
+    Bytes& in = hin.b;
     FILE* fp = fopen(f.path.c_str(), "rb");
     if (!fp) return false;
     const size_t got = n ? fread(in.data(), 1, n, fp) : 0;
@@ -229,7 +302,7 @@ bool inflate_whole(fr_gz* g, GzFile& f) {
             while (k1 < ms.size() && ms[k1].dst + ms[k1].isize - ms[k0].dst <= BGZF_WINDOW) ++k1;
             if (k1 == k0) ++k1;
             const size_t base = ms[k0].dst, len = ms[k1 - 1].dst + ms[k1 - 1].isize - base;
-            std::vector<uint8_t> out;
+            Bytes out;
             {  // wait for room in the file's queue (bounded memory), then decode the window
                 std::unique_lock<std::mutex> lk(g->m);
                 g->cv.wait(lk, [&] { return f.q.size() < g->depth || f.cancel || g->stop; });
@@ -239,6 +312,7 @@ bool inflate_whole(fr_gz* g, GzFile& f) {
                     g->spare.pop_back();
                 }
             }
+            if (out.capacity() < len) out = buf_cache().take(len);
             out.resize(len);
             if (!bgzf_decode(g, ld, in, ms, k0, k1, base, out.data())) {
                 if (k0 == 0) return false;  // nothing queued yet: the zlib stream redoes the file
@@ -263,7 +337,11 @@ bool inflate_whole(fr_gz* g, GzFile& f) {
     Hold hold_out{g, cap};
     void* d = ld->alloc();
     if (!d) return false;
-    std::vector<uint8_t> out(cap);
+    struct Out {  // unless queued, back to the cache
+        Bytes b;
+        ~Out() { buf_cache().give(std::move(b)); }
+    } hout{buf_cache().take(cap)};
+    Bytes& out = hout.b;
     size_t len = 0, pos = 0;
     bool ok = true;
     while (ok) {
@@ -312,7 +390,7 @@ std::string inflate_stream(fr_gz* g, int i) {
     }
     FILE* fp = fopen(f.path.c_str(), "rb");
     if (!fp) return "cannot open " + f.path;
-    std::vector<uint8_t> in(4u << 20);
+    Bytes in(4u << 20);
     z_stream zs;
     std::memset(&zs, 0, sizeof(zs));
     if (inflateInit2(&zs, 16 + MAX_WBITS) != Z_OK) {
@@ -321,13 +399,13 @@ std::string inflate_stream(fr_gz* g, int i) {
     }
     auto fresh = [&]() {
         std::lock_guard<std::mutex> lk(g->m);
-        if (g->spare.empty()) return std::vector<uint8_t>(g->block);
-        std::vector<uint8_t> v = std::move(g->spare.back());
+        if (g->spare.empty()) return buf_cache().take(g->block);
+        Bytes v = std::move(g->spare.back());
         g->spare.pop_back();
         v.resize(g->block);
         return v;
     };
-    std::vector<uint8_t> out = fresh();
+    Bytes out = fresh();
     size_t have = 0;  // bytes of `out` filled
     std::string err;
     bool in_member = false;  // a member has started and not ended
@@ -471,7 +549,7 @@ int fr_gz_feed(fr_gz* g, int i, fr_ctx* ctx) {
         g->cv.notify_all();
     }
     for (;;) {
-        std::vector<uint8_t> b;
+        Bytes b;
         {
             std::unique_lock<std::mutex> lk(g->m);
             g->cv.wait(lk, [&] { return !f.q.empty() || f.done; });
@@ -491,6 +569,7 @@ int fr_gz_feed(fr_gz* g, int i, fr_ctx* ctx) {
             std::lock_guard<std::mutex> lk(g->m);
             if (g->spare.size() < (size_t)g->threads * g->depth) g->spare.push_back(std::move(b));
         }
+        if (b.capacity()) buf_cache().give(std::move(b));
         if (rc != FR_OK) {  // the -s sample is complete, or a feed error: this file is finished
             std::lock_guard<std::mutex> lk(g->m);
             f.cancel = true;
@@ -513,7 +592,7 @@ int fr_gz_next(fr_gz* g, int i, const uint8_t** data, uint64_t* len) {
     std::unique_lock<std::mutex> lk(g->m);
     if (g->held.capacity()) {  // the block handed out last is the caller's no longer
         if (g->spare.size() < (size_t)g->threads * g->depth) g->spare.push_back(std::move(g->held));
-        g->held = std::vector<uint8_t>();
+        g->held = Bytes();
     }
     // readers of several files at once (demux: R1 and R2 in lockstep) keep the furthest one
     g->consume = std::max(g->consume, i);
@@ -673,7 +752,7 @@ int fr_gz_part_bounds(const char* path, int nparts, uint64_t hint, uint64_t* bou
         g->cv.notify_all();
     }
     for (;;) {
-        std::vector<uint8_t> b;
+        Bytes b;
         {
             std::unique_lock<std::mutex> lk(g->m);
             g->cv.wait(lk, [&] { return !f.q.empty() || f.done; });
@@ -731,7 +810,7 @@ int fr_gz_feed_part(fr_gz* g, int i, fr_ctx* ctx, int64_t file_index, int part, 
         g->cv.notify_all();
     };
     for (;;) {
-        std::vector<uint8_t> b;
+        Bytes b;
         bool end = false;
         {
             std::unique_lock<std::mutex> lk(g->m);
@@ -809,7 +888,7 @@ bool bgzf_table(FILE* fp, uint64_t csize, std::vector<Member>& ms) {
     while (pos < csize) {
         if (fseek(fp, (long)pos, SEEK_SET) != 0 || fread(h, 1, 1, fp) != 1) return false;
         if (h[0] == 0) {  // trailing NUL padding only
-            std::vector<uint8_t> rest(csize - pos - 1);
+            Bytes rest(csize - pos - 1);
             if (!rest.empty() && fread(rest.data(), 1, rest.size(), fp) != rest.size()) return false;
             for (uint8_t c : rest)
                 if (c) return false;
@@ -837,11 +916,11 @@ bool bgzf_table(FILE* fp, uint64_t csize, std::vector<Member>& ms) {
 // compressed bytes of the range are read once, then libdeflate (this thread plus up to threads - 1
 // helpers) or zlib per member
 bool bgzf_decode_range(FILE* fp, const std::vector<Member>& ms, size_t k0, size_t k1, int threads,
-                       std::vector<uint8_t>& out) {
+                       Bytes& out) {
     out.clear();
     if (k0 >= k1) return true;
     const size_t c0 = ms[k0].off, c1 = ms[k1 - 1].off + ms[k1 - 1].len;
-    std::vector<uint8_t> in(c1 - c0);
+    Bytes in(c1 - c0);
     if (fseek(fp, (long)c0, SEEK_SET) != 0 || fread(in.data(), 1, in.size(), fp) != in.size()) return false;
     const size_t base = ms[k0].dst;
     out.resize(ms[k1 - 1].dst + ms[k1 - 1].isize - base);
@@ -908,7 +987,7 @@ struct fr_gz_part {
     uint64_t M0 = 0, M1 = 0;    // the part's member range [M0, M1) (decoded offsets)
     size_t kn = 0;              // first member not decoded yet (past data's end)
     uint64_t dbase = 0;         // decoded offset of data[0]
-    std::vector<uint8_t> data;  // decoded bytes [dbase, dbase + data.size())
+    Bytes data;  // decoded bytes [dbase, dbase + data.size())
     uint64_t lines = 0;         // terminators whose terminating byte lies in [M0, M1)
     uint64_t inflated = 0;      // decoded bytes produced for this part
     int threads = 1;
@@ -922,7 +1001,7 @@ bool part_extend(fr_gz_part* p, uint64_t want) {
     while (p->dbase + p->data.size() < std::min(want, p->total) && p->kn < p->ms.size()) {
         size_t k1 = p->kn + 1;
         while (k1 < p->ms.size() && k1 - p->kn < 16) ++k1;  // a few members at a time
-        std::vector<uint8_t> more;
+        Bytes more;
         if (!bgzf_decode_range(p->fp, p->ms, p->kn, k1, p->threads, more)) return false;
         p->inflated += more.size();
         p->data.insert(p->data.end(), more.begin(), more.end());

@@ -1232,35 +1232,6 @@ __device__ __forceinline__ u64 window64(u64 x0, u64 x1, u32 b) { return (x0 >> b
 // and the last ':' before it.  0: code at [start, start + n) (tile offsets); 1: no ' '; 2: word-scan
 // fallback (the first ' ' or the token end lies 64 or more bytes on, or the token starts past the
 // staged bytes).
-#ifdef FR_LOC1
-// One LDS round trip: the words of the two windows (w, w+1 of the line-end bitmap; w .. w+2 of the
-// token-end and ':' bitmaps, since the token starts at most 64 bytes past p) are read together.
-__device__ __forceinline__ int locate_code(const ScanShared& sh, u32 wid, u32 p, u32 bl, u32& start, u32& n) {
-    if (p >= bl) return 2;
-    const u32 w = p >> 6, b = p & 63u;
-    const u64 x0 = sh.bsp[wid][w], x1 = sh.bsp[wid][w + 1], x2 = sh.bsp[wid][w + 2];
-    const u64 c0 = sh.bcol[wid][w], c1 = sh.bcol[wid][w + 1], c2 = sh.bcol[wid][w + 2];
-    const u64 e0 = sh.beol[wid][w], e1 = sh.beol[wid][w + 1];
-    const u64 se = window64(x0, x1, b);
-    const u64 eo = window64(e0, e1, b);
-    const u32 f1 = ctz64x(se);
-    const u32 q = p + f1 + 1u;
-    if (f1 >= 64u) return 2;
-    if (ctz64x(eo) == f1) return 1;
-    if (q >= bl) return 2;
-    const bool nxt = (q >> 6) != w;  // the token's window starts in word w + 1
-    const u32 b2 = q & 63u;
-    const u64 se2 = window64(nxt ? x1 : x0, nxt ? x2 : x1, b2);
-    const u64 co2 = window64(nxt ? c1 : c0, nxt ? c2 : c1, b2);
-    const u32 f2 = ctz64x(se2);
-    if (f2 >= 64u) return 2;
-    const int hc = hsb64x(co2 & ((1ull << f2) - 1ull));  // the last ':' of the token, < 0 none
-    const u32 cs = (u32)max(hc + 1, 0);
-    start = q + cs;
-    n = f2 - cs;
-    return 0;
-}
-#else
 __device__ __forceinline__ int locate_code(const ScanShared& sh, u32 wid, u32 p, u32 bl, u32& start, u32& n) {
     if (p >= bl) return 2;
     const u32 w = p >> 6, b = p & 63u;
@@ -1282,7 +1253,6 @@ __device__ __forceinline__ int locate_code(const ScanShared& sh, u32 wid, u32 p,
     n = f2 - cs;
     return 0;
 }
-#endif
 
 // code bytes [start, start + n) from the wave's LDS copy -> fast key, n wave-uniform (nu): the
 // per-word byte masks are scalars and only the words the code reaches are packed
@@ -1398,25 +1368,15 @@ __device__ __forceinline__ void parse_own_headers(ScanShared& sh, const ScanArgs
 // (in registers since the previous step) go to the wave's LDS copy first, so the registers take the
 // next tile's loads at once and those stay in flight through this tile's classify AND its parse;
 // the classify reads the lane's segment back from LDS.
-__device__ __forceinline__ const ScanArgs* launder_args(const ScanArgs* p) {
-#ifdef FR_LAUNDER
-    asm volatile("" : "+s"(p));
-#endif
-    return p;
-}
-
 __device__ __forceinline__ u64 walk_wave(ScanShared& sh, const ScanArgs& a0, u32 tb, u32 te, u64 L0, bool parse,
                                          int lane, u32 wid) {
-    const ScanArgs& a = *launder_args(&a0);
+    const ScanArgs& a = a0;
     u64 lines = 0;
     u32 done = *(const volatile lds_u32*)&sh.rq_tail[wid];
     SegRegs r;
     if (tb < te) seg_load(a, tb, r, lane);
     lds_u32x4* mine = (lds_u32x4*)(&sh.raw[wid][0]) + lane * (SEG / 16);
     for (u32 t = tb; t < te; ++t) {
-#ifdef FR_LAUNDER
-        const ScanArgs& a = *launder_args(&a0);  // kernel arguments re-read per tile: no long-lived SGPR copies
-#endif
         // the previous tile's parse is done with the LDS copy (program order)
 #pragma unroll
         for (int k = 0; k < SEG / 16; ++k) {
@@ -1425,24 +1385,11 @@ __device__ __forceinline__ u64 walk_wave(ScanShared& sh, const ScanArgs& a0, u32
             mine[k] = v;
         }
         if (t + 1 < te) seg_load(a, t + 1, r, lane);
-#ifdef FR_QREAD
         // volatile: a real LDS read, one quarter of the segment at a time inside the classify
         const SegClass sc = seg_classify_src(a, t, [&](int k) {
             const u32x4 v = *(const volatile lds_u32x4*)&mine[k];
             return make_uint4(v.x, v.y, v.z, v.w);
         }, lane);
-#else
-        SegRegs q;
-#pragma unroll
-        for (int k = 0; k < SEG / 16; ++k) {
-            // volatile: a real LDS read.  Forwarded from the stores, the tile would stay in 16 more
-            // VGPRs (copied by 16 v_mov per tile) while the next tile's loads fill r
-            const u32x4 v = *(const volatile lds_u32x4*)&mine[k];
-            q.v[k] = make_uint4(v.x, v.y, v.z, v.w);
-        }
-        q.nx = 0;
-        const SegClass sc = seg_classify(a, t, q, lane);
-#endif
         if (sc.hi) rare_push(sh, a, (u32)((u64)t * TSTEP) + lane * SEG, 4u,
                              min((u32)min((u64)TSTEP, a.len - (u64)t * TSTEP) - lane * SEG, (u32)SEG), 0u);
         const u32 tail = *(const volatile lds_u32*)&sh.rq_tail[wid];

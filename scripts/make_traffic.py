@@ -23,7 +23,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNEL = "fr::chunk_kernel"
-VALU_PEAK_G = 1228.8  # MI355X_MICROARCH.md:53-54: SIMD-32, one wave64 VALU instruction per 2 cycles per SIMD
+VALU_PEAK_G = 646.9  # measured chip issue ceiling (profiles/r04c_ubench_valu.txt: v_and_b32, 4 waves/SIMD, wall clock)
 
 
 def rows(pattern):

@@ -579,7 +579,11 @@ __device__ __forceinline__ void seg_fetch(const ScanArgs& a, u32 t, SegRegs& r, 
                                                         0x00020000);
 #pragma unroll
     for (int k = 0; k < SEG / 16; ++k) {
+#ifdef FR_NT
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, lane * SEG, k * 16, 2);  // nt: streamed once
+#else
         const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, lane * SEG, k * 16, 0);
+#endif
         r.v[k] = make_uint4(v[0], v[1], v[2], v[3]);
     }
     r.nx = with_nx ? __builtin_amdgcn_raw_buffer_load_b32(rsrc, lane * SEG + SEG, 0, 0) : 0u;  // '\r' path only
@@ -675,6 +679,10 @@ __device__ __forceinline__ SegClass seg_classify_src(const ScanArgs& a, u32 t, c
             const u64 nxt = (q.nx & 0xFFu) == (u32)'\n' ? 1ull : 0ull;
             tm = eol & ~(cr & ((nl >> 1) | (nxt << 63)));
         }
+#ifdef FR_EDGE_UNIFORM
+        // interior wave-tiles (every segment whole and owned): no per-lane edge masks at all
+        if (__builtin_amdgcn_readfirstlane(__ballot(bl - s0 < SEG || s0 >= tlen || tlen - s0 < SEG) != 0)) {
+#endif
         const u32 bvalid = bl - s0;
         if (bvalid < SEG) {
             const u64 vm = (1ull << bvalid) - 1ull;
@@ -682,12 +690,19 @@ __device__ __forceinline__ SegClass seg_classify_src(const ScanArgs& a, u32 t, c
             col &= vm;
             eol &= vm;
         }
+        if (s0 < tlen) {
+            const u32 valid = tlen - s0;
+            if (valid < SEG) tm &= (1ull << valid) - 1ull;
+        } else {
+            tm = 0;
+        }
+#ifdef FR_EDGE_UNIFORM
+        }
+#endif
         sc.sp = sp;
         sc.col = col;
         sc.eol = eol;
         if (s0 < tlen) {
-            const u32 valid = tlen - s0;
-            if (valid < SEG) tm &= (1ull << valid) - 1ull;
             sc.tmask = tm;
             sc.hi = (acc & 0x10101010u) != 0;  // exact own-byte test in drain_rare (kind 4)
         }
@@ -749,47 +764,45 @@ __device__ __forceinline__ void seg_marks(const SegRegs& r, u64& at, u64& plus) 
 // Guess P = (lines before the wave-tile) mod 4 from its first PHASE_LINES complete lines: with lines
 // indexed P+k+1 after the k-th terminator, a FASTQ record has a header ('@') at phase 0, '+' at
 // phase 2 and equal seq/qual lengths at phases 1/3.  Exactly one consistent P -> the guess;
-// otherwise -1 (unsure).  One lane.  Bitmaps (staged by the caller, the wave's area): bsp = line
-// terminators, bcol = '@', beol = '+'.  Line lengths include a '\r' of "\r\n" (equal on both
-// lines of a consistently terminated record).
-__device__ __forceinline__ int infer_phase(const ScanShared& sh, u32 wid) {
-    bool ok[4] = {true, true, true, true};
-    int seqlen[4] = {-1, -1, -1, -1};
-    int prev = -1, k = 0;
-    for (int w = 0; w < SEGS && k < PHASE_LINES; ++w) {
-        u64 m = sh.bsp[wid][w];
-        while (m && k < PHASE_LINES) {
-            const int e = w * SEG + (__ffsll((long long)m) - 1);
-            m &= m - 1;
-            if (prev >= 0) {  // the line [prev+1, e)
-                const int st = prev + 1;
-                const int len = e - st;
-                const bool is_at = len > 0 && ((sh.bcol[wid][st >> 6] >> (st & 63)) & 1ull);
-                const bool is_plus = len > 0 && ((sh.beol[wid][st >> 6] >> (st & 63)) & 1ull);
-#pragma unroll
-                for (int P = 0; P < 4; ++P) {
-                    const int ph = (P + k + 1) & 3;
-                    if (ph == 0) ok[P] &= is_at;
-                    else if (ph == 2) ok[P] &= is_plus;
-                    else if (ph == 1) seqlen[P] = len;
-                    else {
-                        if (seqlen[P] >= 0) ok[P] &= seqlen[P] == len;
-                        seqlen[P] = -1;
-                    }
-                }
-                ++k;
-            }
-            prev = e;
-        }
+// otherwise -1 (unsure).  Bitmaps (staged by the caller, the wave's area): bcol = '@', beol = '+'.
+// Line lengths include a '\r' of "\r\n" (equal on both lines of a consistently terminated record).
+// All lanes at once (round 4; it was one lane walking the lines while the wave waited): the
+// terminators e_0 .. e_PHASE_LINES of the tile go to LDS by their index in the tile (each lane writes
+// its own, from the wave's terminator scan), then lane k checks line k = (e_k, e_{k+1}) against the
+// four candidate phases and ballots decide.
+__device__ __forceinline__ int infer_phase(ScanShared& sh, const SegClass& sc, int lane, u32 wid) {
+    lds_u32* E = (lds_u32*)&sh.raw[wid][0];  // the wave's tile copy is free until its walk starts
+    u32 i = sc.x - sc.c;                      // this lane's first terminator's index in the tile
+    u64 m = sc.tmask;
+    while (m && i <= (u32)PHASE_LINES) {
+        E[i] = (u32)lane * SEG + (u32)__builtin_ctzll(m);
+        m &= m - 1ull;
+        ++i;
     }
-    if (k < 8) return -1;
+    lds_fence();
+    const u32 tot = __builtin_amdgcn_readlane(sc.x, 63);  // terminators in the tile
+    const int K = (int)min(tot, (u32)PHASE_LINES + 1u) - 1;  // complete lines looked at
+    if (K < 8) return -1;
+    const bool valid = lane < K;
+    int len = 0;
+    bool is_at = false, is_plus = false;
+    if (valid) {
+        const u32 st = E[lane] + 1u;
+        len = (int)E[lane + 1] - (int)st;
+        is_at = len > 0 && ((sh.bcol[wid][st >> 6] >> (st & 63u)) & 1ull);
+        is_plus = len > 0 && ((sh.beol[wid][st >> 6] >> (st & 63u)) & 1ull);
+    }
+    const int len2 = __shfl(len, lane - 2, 64);  // line k - 2: the phase-1 line before a phase-3 line
     int found = -1, nfound = 0;
 #pragma unroll
-    for (int P = 0; P < 4; ++P)
-        if (ok[P]) {
+    for (int P = 0; P < 4; ++P) {
+        const int ph = (P + lane + 1) & 3;
+        const bool bad = valid && ((ph == 0 && !is_at) || (ph == 2 && !is_plus) || (ph == 3 && lane >= 2 && len != len2));
+        if (__ballot(bad) == 0) {
             found = P;
             ++nfound;
         }
+    }
     return nfound == 1 ? found : -1;
 }
 
@@ -800,13 +813,10 @@ __device__ __attribute__((noinline)) int guess_phase(ScanShared& sh, const ScanA
     const SegClass sc = seg_classify(a, t, r, lane);
     u64 at, plus;
     seg_marks(r, at, plus);
-    sh.bsp[wid][lane] = sc.tmask;  // infer_phase: terminators, '@', '+'
-    sh.bcol[wid][lane] = at;
+    sh.bcol[wid][lane] = at;  // infer_phase: '@', '+'
     sh.beol[wid][lane] = plus;
     lds_fence();
-    int P = 0;
-    if (lane == 0) P = infer_phase(sh, wid);
-    return __shfl(P, 0, 64);
+    return infer_phase(sh, sc, lane, wid);
 }
 
 // Commit: resolve first, update last.  A wait for a load or CAS return also waits for every
@@ -1242,6 +1252,20 @@ __device__ __forceinline__ int locate_code(const ScanShared& sh, u32 wid, u32 p,
     if (f1 >= 64u) return 2;
     if (ctz64x(eo) == f1) return 1;
     if (q >= bl) return 2;
+#ifdef FR_LOC_ONE
+    {  // the token ends inside the same window (headers shorter than 64 B): no second window
+        const u64 after = se & ~((2ull << f1) - 1ull);  // token ends past the first ' '
+        if (after) {
+            const u32 f2 = ctz64x(after);  // relative to p
+            const u64 co = window64(sh.bcol[wid][w], sh.bcol[wid][w + 1], b);
+            const int hc = hsb64x(co & ((1ull << f2) - 1ull) & ~((2ull << f1) - 1ull));  // last ':' in (f1, f2)
+            const u32 cs = hc >= 0 ? (u32)hc + 1u : f1 + 1u;
+            start = p + cs;
+            n = f2 - cs;
+            return 0;
+        }
+    }
+#endif
     const u32 w2 = q >> 6, b2 = q & 63u;
     const u64 se2 = window64(sh.bsp[wid][w2], sh.bsp[wid][w2 + 1], b2);
     const u64 co2 = window64(sh.bcol[wid][w2], sh.bcol[wid][w2 + 1], b2);
@@ -1328,7 +1352,11 @@ __device__ __forceinline__ void parse_own_headers(ScanShared& sh, const ScanArgs
         const u64 d = m & (m - 1ull);
         m = q < skip ? d : m;
     }
+#ifdef FR_NOLIMIT
+    const bool limited = false;
+#else
     const bool limited = a.max_records > 0;  // -s: uniform
+#endif
     u64 rec = 0;
     if (limited) rec = (L0 + (sc.x - sc.c) + skip + 1u) >> 2;
     const bool own0 = t == 0 && lane == 0 && a.own_start && (L0 & 3ull) == 0 && a.avail > 0 &&

@@ -579,11 +579,7 @@ __device__ __forceinline__ void seg_fetch(const ScanArgs& a, u32 t, SegRegs& r, 
                                                         0x00020000);
 #pragma unroll
     for (int k = 0; k < SEG / 16; ++k) {
-#ifdef FR_NT
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, lane * SEG, k * 16, 2);  // nt: streamed once
-#else
         const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, lane * SEG, k * 16, 0);
-#endif
         r.v[k] = make_uint4(v[0], v[1], v[2], v[3]);
     }
     r.nx = with_nx ? __builtin_amdgcn_raw_buffer_load_b32(rsrc, lane * SEG + SEG, 0, 0) : 0u;  // '\r' path only
@@ -679,10 +675,6 @@ __device__ __forceinline__ SegClass seg_classify_src(const ScanArgs& a, u32 t, c
             const u64 nxt = (q.nx & 0xFFu) == (u32)'\n' ? 1ull : 0ull;
             tm = eol & ~(cr & ((nl >> 1) | (nxt << 63)));
         }
-#ifdef FR_EDGE_UNIFORM
-        // interior wave-tiles (every segment whole and owned): no per-lane edge masks at all
-        if (__builtin_amdgcn_readfirstlane(__ballot(bl - s0 < SEG || s0 >= tlen || tlen - s0 < SEG) != 0)) {
-#endif
         const u32 bvalid = bl - s0;
         if (bvalid < SEG) {
             const u64 vm = (1ull << bvalid) - 1ull;
@@ -696,9 +688,6 @@ __device__ __forceinline__ SegClass seg_classify_src(const ScanArgs& a, u32 t, c
         } else {
             tm = 0;
         }
-#ifdef FR_EDGE_UNIFORM
-        }
-#endif
         sc.sp = sp;
         sc.col = col;
         sc.eol = eol;
@@ -1252,20 +1241,6 @@ __device__ __forceinline__ int locate_code(const ScanShared& sh, u32 wid, u32 p,
     if (f1 >= 64u) return 2;
     if (ctz64x(eo) == f1) return 1;
     if (q >= bl) return 2;
-#ifdef FR_LOC_ONE
-    {  // the token ends inside the same window (headers shorter than 64 B): no second window
-        const u64 after = se & ~((2ull << f1) - 1ull);  // token ends past the first ' '
-        if (after) {
-            const u32 f2 = ctz64x(after);  // relative to p
-            const u64 co = window64(sh.bcol[wid][w], sh.bcol[wid][w + 1], b);
-            const int hc = hsb64x(co & ((1ull << f2) - 1ull) & ~((2ull << f1) - 1ull));  // last ':' in (f1, f2)
-            const u32 cs = hc >= 0 ? (u32)hc + 1u : f1 + 1u;
-            start = p + cs;
-            n = f2 - cs;
-            return 0;
-        }
-    }
-#endif
     const u32 w2 = q >> 6, b2 = q & 63u;
     const u64 se2 = window64(sh.bsp[wid][w2], sh.bsp[wid][w2 + 1], b2);
     const u64 co2 = window64(sh.bcol[wid][w2], sh.bcol[wid][w2 + 1], b2);

@@ -26,3 +26,7 @@ if [[ ${E2E:-0} == 1 ]]; then
   timeout -k 10 400 python -u scripts/e2e_profile.py > gpurun_out/${TAG}_e2e_profile.txt 2>&1 || { tail -5 gpurun_out/${TAG}_e2e_profile.txt; exit 1; }
   grep "scan s" gpurun_out/${TAG}_e2e_profile.txt
 fi
+if [[ ${TRACE:-0} == 1 ]]; then
+  PMC=${PMC:-0} bash scripts/gpu_profile.sh > gpurun_out/${TAG}_prof.log 2>&1 || { tail -5 gpurun_out/${TAG}_prof.log; exit 1; }
+  tail -12 gpurun_out/${TAG}_prof.log | cut -c1-250
+fi

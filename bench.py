@@ -60,6 +60,12 @@ def parse():
     ap.add_argument("--pin-json", default=os.path.join(ROOT, "tests", "golden", "cfg2_pin.json"),
                     help="the reference's own rows for BASELINE config 2 (tests/golden/make_golden_cfg2.py): at N=1 "
                          "on that exact shape the classified table must reproduce them (checked after timing)")
+    ap.add_argument("--cfg5", action="store_true",
+                    help="instead of the headline metric: BASELINE config 5's shape end to end (paired .fastq.gz, "
+                         "R=150 -> scan + demux CLIs) beside the reference's CPU path (oracle port) on a bounded sample")
+    ap.add_argument("--cfg5-pairs", type=int, default=2_000_000)
+    ap.add_argument("--cfg5-files", type=int, default=4, help="file pairs")
+    ap.add_argument("--cfg5-cpu-pairs", type=int, default=100_000)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r03.json"),
                     help="per-launch HBM bytes of the tally kernel from rocprofv3 PMC (scripts/make_traffic.py); "
                          "used only when taken on this source tree and this launch shape, else traffic is null")
@@ -246,6 +252,101 @@ def cpu_baseline(args, ctx, sheet, reclen):
                       f"files (level 1), {cores} workers: {dt:.2f} s{cal}"}
 
 
+def _cfg5_write(job):
+    from frender_amd import synth
+
+    path, r0, n, mate = job
+    t = synth.generate_bytes(synth.make_sheet(96, 8, 8), r0, n, R=150, seed=5)
+    if mate == 2:
+        t = t.replace(b" 1:N:0:", b" 2:N:0:")
+    synth.write_fastq_gz(path, t, level=1)
+    return os.path.getsize(path)
+
+
+def cfg5(args):
+    """--cfg5: BASELINE config 5's shape (96 samples, 8+8 bp, n=1, paired-end R=150 per mate) end to end
+    on this box -- not the headline metric (config 5 is quoted on 8 GPUs over 500M pairs).  Product: the
+    scan and demux command lines (`python -m frender_amd`, each paying its Python start and GPU
+    context) over --cfg5-files level-1 .fastq.gz file pairs, demux writing the reference's level-9
+    gzip.  CPU baseline: the reference's scan + demux as restated by the oracle (scan: Pool of 8 over
+    files; demux: one process, gzip.open writers, one write per line, frender.py:667-676, :726-814), on
+    the first --cfg5-cpu-pairs pairs.  One JSON line."""
+    import contextlib
+    import io
+    import subprocess
+    import tempfile
+    from concurrent.futures import ProcessPoolExecutor
+
+    from frender_amd import synth
+    from oracle import demux_oracle as D
+    from oracle import frender_oracle as O
+
+    n, fp = args.cfg5_pairs, args.cfg5_files
+    per = n // fp
+    cpu_n = min(args.cfg5_cpu_pairs, per)
+    with tempfile.TemporaryDirectory() as d:
+        sheet = synth.make_sheet(96, 8, 8)
+        csv_path = os.path.join(d, "sheet.csv")
+        sheet.write_csv(csv_path)
+        os.mkdir(os.path.join(d, "in"))
+        os.mkdir(os.path.join(d, "cpu_in"))
+        jobs = [(os.path.join(d, "in", f"syn_L{p + 1:03d}_R{m}_001.fastq.gz"), p * per, per, m)
+                for p in range(fp) for m in (1, 2)]
+        jobs += [(os.path.join(d, "cpu_in", f"syn_L001_R{m}_001.fastq.gz"), 0, cpu_n, m) for m in (1, 2)]
+        with ProcessPoolExecutor(8) as ex:
+            in_bytes = sum(ex.map(_cfg5_write, jobs))
+        r1 = sorted(os.path.join(d, "in", x) for x in os.listdir(os.path.join(d, "in")) if "_R1_" in x)
+        allf = sorted(os.path.join(d, "in", x) for x in os.listdir(os.path.join(d, "in")))
+        work = os.path.join(d, "gpu")
+        os.mkdir(work)
+        env = dict(os.environ, PYTHONPATH=ROOT)
+        t0 = time.perf_counter()
+        sp = subprocess.run([sys.executable, "-m", "frender_amd", "scan", "-n", "1", "-c", "8", "-o", "cfg5", "-b",
+                             csv_path, *r1], cwd=work, env=env, capture_output=True, text=True)
+        t1 = time.perf_counter()
+        if sp.returncode:
+            raise SystemExit(f"cfg5 scan failed: {sp.stderr[-2000:]}")
+        res = [os.path.join(work, x) for x in os.listdir(work) if x.endswith(".csv")]
+        dm = subprocess.run([sys.executable, "-m", "frender_amd", "demux", "-r", res[0], "-d",
+                             os.path.join(work, "out"), *allf], cwd=work, env=env, capture_output=True, text=True)
+        t2 = time.perf_counter()
+        if dm.returncode:
+            raise SystemExit(f"cfg5 demux failed: {dm.stderr[-2000:]}")
+        # the CPU baseline on the first cpu_n pairs (one file pair)
+        cwork = os.path.join(d, "cpu")
+        os.mkdir(cwork)
+        c1 = os.path.join(d, "cpu_in", "syn_L001_R1_001.fastq.gz")
+        c2 = os.path.join(d, "cpu_in", "syn_L001_R2_001.fastq.gz")
+        cwd = os.getcwd()
+        os.chdir(cwork)
+        try:
+            with contextlib.redirect_stdout(io.StringIO()):
+                u0 = time.perf_counter()
+                O.scan(argparse.Namespace(n=1, rc=False, c=8.0, s=None, o="cpu", p=None, b=csv_path, files=[c1]))
+                u1 = time.perf_counter()
+                cres = [x for x in os.listdir(cwork) if x.endswith(".csv")][0]
+                D.demux(argparse.Namespace(r=cres, d=os.path.join(cwork, "out"), o=None, no_index_hop=False,
+                                           no_ambiguous=False, no_undeter=False, no_samples=False, strict_header=False,
+                                           files=[c1, c2]), write_files=True)
+                u2 = time.perf_counter()
+        finally:
+            os.chdir(cwd)
+    return {"metric": "M read pairs/s scan+demux (BASELINE config 5 shape: 96 samples, 8+8bp, n=1, paired R=150)",
+            "value": round(n / (t2 - t0) / 1e6, 4), "unit": "M read pairs/s", "n_gpus": 1,
+            "higher_is_better": True, "data": "synthetic (SYN-v1, R=150 per mate, level-1 .fastq.gz inputs)",
+            "config": {"workload": f"{n} read pairs in {fp} file pairs; scan -n 1 -c 8, then demux (gzip level 9 "
+                                   f"writers, the reference's)", "in_gz_bytes": in_bytes},
+            "scan_s": round(t1 - t0, 3), "demux_s": round(t2 - t1, 3),
+            "demux_M_pairs_per_s": round(n / (t2 - t1) / 1e6, 4),
+            "cpu_baseline": {"value": round(cpu_n / (u2 - u0) / 1e6, 5), "unit": "M read pairs/s", "cores": 8,
+                             "kind": "port", "scan_s": round(u1 - u0, 3), "demux_s": round(u2 - u1, 3),
+                             "demux_M_pairs_per_s": round(cpu_n / (u2 - u1) / 1e6, 5),
+                             "sample": f"oracle.frender_oracle.scan (Pool of 8 over the files) + oracle.demux_oracle."
+                                       f"demux(write_files=True) (one process: the reference's demux loop has no "
+                                       f"Pool) on the first {cpu_n} pairs (one file pair)"},
+            "note": "two CLI processes for the product (each pays its Python/torch start and GPU context)"}
+
+
 def pin_check(args, ctx, sheet, idx2rc, nid, names):
     """BASELINE config 2 at N=1: the benchmarked table (the last timed step's), classified, must equal
     the reference's own tally_barcodes + process rows on the same records (tests/golden/cfg2_pin.json:
@@ -297,6 +398,9 @@ def main():
         return 2
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.cfg5:
+        print(json.dumps(cfg5(args)), flush=True)
+        return 0
     if args.rank_check:
         return rank_check(world) if world > 1 else (print(json.dumps({"rank_check": True, "world": 1,
                                                                       "ranks_joined": 1})) or 0)

@@ -105,9 +105,11 @@ def out_name(d: str, name: str, infix, read: str) -> str:
     return f"{d}{name}_frender-demux_{infix + '_' if infix else ''}{read}.fq.gz"
 
 
-def demux(args) -> dict:
+def demux(args, write_files: bool = False) -> dict:
     """frender.py:733-814.  Returns {output file path: decoded bytes written} (all writers,
-    including empty ones); raises like the reference does."""
+    including empty ones); raises like the reference does.  write_files: also write every output
+    the way the reference does (gzip.open(..., "wb") writers at gzip's default level 9, one write per
+    line, open_files / write_reads :667-676, :726-730) -- the CPU baseline timing of bench.py --cfg5."""
     want_hop = not args.no_index_hop
     want_amb = not args.no_ambiguous
     want_und = not args.no_undeter
@@ -122,10 +124,16 @@ def demux(args) -> dict:
     os.mkdir(args.d)
     out: dict = {}
 
+    import gzip
+
+    gz: dict = {}
+
     def writers(name):
         pair = (out_name(args.d, name, args.o, "R1"), out_name(args.d, name, args.o, "R2"))
         for p in pair:
             out[p] = bytearray()
+            if write_files:
+                gz[p] = gzip.open(p, "wb")
         return pair
 
     sample_w = {sid: writers(sid) for sid in ids} if want_samples else None
@@ -165,5 +173,10 @@ def demux(args) -> dict:
                 raise SystemExit("Unrecognized read type found in supplied frender result file!")
             for lines, p in zip((g1, g2), w):
                 for line in lines:
-                    out[p] += line.encode("utf-8")
+                    if write_files:
+                        gz[p].write(str(line).encode("utf-8"))
+                    else:
+                        out[p] += line.encode("utf-8")
+    for f in gz.values():
+        f.close()
     return {p: bytes(b) for p, b in out.items()}

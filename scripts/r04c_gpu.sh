@@ -30,3 +30,7 @@ if [[ ${TRACE:-0} == 1 ]]; then
   PMC=${PMC:-0} bash scripts/gpu_profile.sh > gpurun_out/${TAG}_prof.log 2>&1 || { tail -5 gpurun_out/${TAG}_prof.log; exit 1; }
   tail -12 gpurun_out/${TAG}_prof.log | cut -c1-250
 fi
+if [[ ${CFG5:-0} == 1 ]]; then
+  timeout -k 10 600 python -u bench.py --cfg5 > gpurun_out/${TAG}_cfg5.log 2>&1 || { tail -5 gpurun_out/${TAG}_cfg5.log; exit 1; }
+  tail -1 gpurun_out/${TAG}_cfg5.log | cut -c1-400
+fi

@@ -24,3 +24,16 @@ def test_demux_oracle_matches_reference(name):
 
 def test_demux_cases_present():
     assert len(case_names()) >= 15
+
+
+def _oracle_demux_files(args):
+    """The timing port (bench.py --cfg5): the oracle writes the outputs itself, through gzip.open
+    writers line by line as the reference does."""
+    from oracle import demux_oracle
+    demux_oracle.demux(args, write_files=True)
+
+
+@pytest.mark.parametrize("name", case_names())
+def test_demux_oracle_file_writers_match_reference(name):
+    diffs = run_case(name, _oracle_demux_files)
+    assert not diffs, "\n".join(diffs)

@@ -73,17 +73,27 @@ def main():
     valu, _ = per_dispatch(rows(src + "/prof_valu/**/*counter_collection.csv"), "SQ_INSTS_VALU")
     vact, _ = per_dispatch(rows(src + "/prof_valu/**/*counter_collection.csv"), "SQ_ACTIVE_INST_VALU")
     valu_d = None
-    if valu:  # VALU issue: wave64 instructions; one SIMD issues one per 4 cycles (16 lanes)
+    if valu:  # VALU issue: wave64 instructions against the measured chip ceiling
         vi = sum(valu.values()) / len(valu)
         valu_d = {"insts_per_launch": int(vi), "insts_per_record": round(vi / (reads / launches), 3),
                   "active_quad_cycles_per_launch": int(sum(vact.values()) / len(vact)) if vact else None,
                   "peak_g_insts_per_s": VALU_PEAK_G,
-                  "peak_note": "256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction (MI355X_MICROARCH.md:53-54); "
-                                "measured for the tally's own integer mix at 4 waves/SIMD: 0.401 instructions per SIMD-cycle "
-                                "= 985 G/s (profiles/r04b_ubench_valu.txt, scripts/ubench_valu.hip)",
-                  "mix_ceiling_g_insts_per_s": 985.0}
+                  "peak_note": "measured chip issue ceiling: independent v_and_b32 chains at 4 waves/SIMD, wall clock, "
+                                "in-kernel clock 2.37 GHz (profiles/r04c_ubench_valu.txt, scripts/ubench_valu.hip); the "
+                                "guide's 2-cycle figure (1229 G/s) is not sustained",
+                  "mix_ceiling_g_insts_per_s": 626.9}
+    # A lower reading of the same counters: the table probes beyond the stream (random 32-B slot reads)
+    # are one 64-B FETCH unit each (profiles/r04h_table_pmc/summary.json); x2 assumes each is a 128-B
+    # line tallied at 64 B like the streaming loads, x1 that it is a 64-B fill.  Needs the stream-only pass.
+    lower = None
+    if calib:
+        extra_kb = max(fkb - calib["fetch_size_kb_avg"], 0.0)
+        lb = 2 * calib["fetch_size_kb_avg"] * 1024 + extra_kb * 1024 + wkb * 1024
+        lower = {"hbm_bytes_per_launch": int(lb), "traffic_over_algorithmic": round(lb / alg, 4),
+                 "note": "stream fetch x2 (16-B/lane loads, calibrated) + the rest of FETCH_SIZE x1 (table probes "
+                         "counted at one 64-B unit each, profiles/r04h_table_pmc) + WRITE_SIZE"}
     out = {
-        "round": int(os.environ.get("ROUND", "3")),
+        "round": int(os.environ.get("ROUND", "4")),
         "tree_hash": source_tree_hash(),
         "samples": int(os.environ.get("SAMPLES", "96")),
         "index_len": int(os.environ.get("INDEX_LEN", "8")),
@@ -101,6 +111,7 @@ def main():
         "traffic_over_algorithmic": round((2 * fkb * 1024 + wkb * 1024) / alg, 4),
         "fetch_over_algorithmic": round(2 * fkb * 1024 / alg, 4),
         "stream_only_calibration": calib,
+        "lower_reading": lower,
         "valu": valu_d,
         "source": f"profiles/{tag}_pmc_chunk_kernel.csv (rocprofv3 --pmc FETCH_SIZE, then --pmc WRITE_SIZE, "
                   f"separate runs of bench.py {os.environ.get('PROF_ARGS', '--steps 5 --warmup 1 --no-cpu')})",

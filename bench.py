@@ -66,7 +66,7 @@ def parse():
     ap.add_argument("--cfg5-pairs", type=int, default=2_000_000)
     ap.add_argument("--cfg5-files", type=int, default=4, help="file pairs")
     ap.add_argument("--cfg5-cpu-pairs", type=int, default=100_000)
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r03.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r04.json"),
                     help="per-launch HBM bytes of the tally kernel from rocprofv3 PMC (scripts/make_traffic.py); "
                          "used only when taken on this source tree and this launch shape, else traffic is null")
     return ap.parse_args()

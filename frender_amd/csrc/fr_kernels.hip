@@ -97,6 +97,18 @@ __device__ __forceinline__ u32 classify4(u32 w) {
     return lo3 & mid3 & top2;
 }
 
+// The same classes from two lookups (round 4): bits [2:0] and bits [6:3] of the byte.  The 16-entry
+// lookup leans on v_perm's fixed selectors (8-11: the sign bits of table bytes 1, 3, 5, 7, all 0 here;
+// 12: 0x00; 13-15: 0xFF), so bytes 0x68-0x7F would read "every class" from it: the lo-table entries
+// that carry a class also carry bit 7, and a class word with bit 7 set (the ASCII bytes h j m p r u x
+// z }) sends the wave-tile to classify4.  Bit 7 of the byte is not looked at: a byte >= 0x80 sends the
+// wave-tile there too.  Every other ASCII byte gets exactly classify4's bits 0-3 (checked for all 128).
+__device__ __forceinline__ u32 classify4_fast(u32 w) {
+    const u32 lo3 = __builtin_amdgcn_perm(0x00008300u, 0x00890084u, w & 0x07070707u);
+    const u32 hi4 = __builtin_amdgcn_perm(0x08000004u, 0x00000300u, (w >> 3) & 0x0F0F0F0Fu);
+    return lo3 & hi4;
+}
+
 // Class K of 16 bytes (four class words, byte i of word j = position 4j + i) -> a 16-bit mask.
 // v_dot4_u32_u8 gathers the flag bytes at full rate: weights 1,2,4,8 place word 0's bytes at
 // bits 0-3, weights 16..128 word 1's at bits 4-7 (every product is scaled by 2^K, undone at
@@ -626,6 +638,29 @@ struct SegClass {
 template <class Src>
 __device__ __forceinline__ SegClass seg_classify_src(const ScanArgs& a, u32 t, const Src& src, int lane);
 
+struct Cls16 {  // a segment's class bitmaps in 16-bit quarters, and the OR of its class words
+    u32 eol[4], sp[4], col[4], acc;
+};
+
+// classify4 over the lane's segment, re-read from memory: the exact path of seg_classify_src
+__device__ __attribute__((noinline)) Cls16 classes_exact(const ScanArgs& a, u32 t, int lane) {
+    SegRegs q;
+    if (seg_in_range(a, t)) seg_fetch(a, t, q, lane);
+    else q = seg_load_tail(a, t, lane);
+    Cls16 r;
+    r.acc = 0;
+#pragma unroll
+    for (int qv = 0; qv < SEG / 16; ++qv) {
+        const u32 c0 = classify4(q.v[qv].x), c1 = classify4(q.v[qv].y), c2 = classify4(q.v[qv].z),
+                  c3 = classify4(q.v[qv].w);
+        r.eol[qv] = gather16<0>(c0, c1, c2, c3);
+        r.sp[qv] = gather16<2>(c0, c1, c2, c3);
+        r.col[qv] = gather16<3>(c0, c1, c2, c3);
+        r.acc |= c0 | c1 | c2 | c3;
+    }
+    return r;
+}
+
 __device__ __forceinline__ SegClass seg_classify(const ScanArgs& a, u32 t, const SegRegs& r, int lane) {
     return seg_classify_src(a, t, [&](int k) { return r.v[k]; }, lane);
 }
@@ -644,15 +679,29 @@ __device__ __forceinline__ SegClass seg_classify_src(const ScanArgs& a, u32 t, c
     sc.hi = false;
     if (s0 < bl) {
         u32 eol16[4], sp16[4], col16[4];
-        u32 acc = 0;
+        u32 acc = 0, raw = 0;
 #pragma unroll
         for (int qv = 0; qv < SEG / 16; ++qv) {  // class words live one quarter at a time
             const uint4 v = src(qv);
-            const u32 c0 = classify4(v.x), c1 = classify4(v.y), c2 = classify4(v.z), c3 = classify4(v.w);
+            const u32 c0 = classify4_fast(v.x), c1 = classify4_fast(v.y), c2 = classify4_fast(v.z),
+                      c3 = classify4_fast(v.w);
             eol16[qv] = gather16<0>(c0, c1, c2, c3);
             sp16[qv] = gather16<2>(c0, c1, c2, c3);
             col16[qv] = gather16<3>(c0, c1, c2, c3);
             acc |= c0 | c1 | c2 | c3;
+            raw |= v.x | v.y | v.z | v.w;
+        }
+        if (__builtin_amdgcn_readfirstlane(__ballot(((acc | raw) & 0x80808080u) != 0) != 0)) {
+            // a byte >= 0x80 or a fast-table sentinel somewhere in the wave-tile: the exact classifier,
+            // out of line on the segment re-read from L2 (no register of the common path is held for it)
+            const Cls16 e = classes_exact(a, t, lane);
+#pragma unroll
+            for (int qv = 0; qv < SEG / 16; ++qv) {
+                eol16[qv] = e.eol[qv];
+                sp16[qv] = e.sp[qv];
+                col16[qv] = e.col[qv];
+            }
+            acc = e.acc;
         }
         auto join = [](const u32 (&g)[4]) {
             return ((u64)(g[2] | (g[3] << 16)) << 32) | (u64)(g[0] | (g[1] << 16));

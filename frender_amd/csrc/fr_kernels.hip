@@ -691,7 +691,7 @@ __device__ __forceinline__ SegClass seg_classify_src(const ScanArgs& a, u32 t, c
             acc |= c0 | c1 | c2 | c3;
             raw |= v.x | v.y | v.z | v.w;
         }
-        if (__builtin_amdgcn_readfirstlane(__ballot(((acc | raw) & 0x80808080u) != 0) != 0)) {
+        if (__ballot(((acc | raw) & 0x80808080u) != 0) != 0) {  // a wave-uniform SGPR value: a scalar branch
             // a byte >= 0x80 or a fast-table sentinel somewhere in the wave-tile: the exact classifier,
             // out of line on the segment re-read from L2 (no register of the common path is held for it)
             const Cls16 e = classes_exact(a, t, lane);
@@ -708,7 +708,7 @@ __device__ __forceinline__ SegClass seg_classify_src(const ScanArgs& a, u32 t, c
         };
         u64 eol = join(eol16), sp = join(sp16), col = join(col16);
         u64 tm = eol;
-        if (__builtin_amdgcn_readfirstlane(__ballot((acc & 0x02020202u) != 0) != 0)) {
+        if (__ballot((acc & 0x02020202u) != 0) != 0) {
             // '\r' somewhere in the wave (CRLF / CR files): a '\r' right before a '\n' ends no line.
             // The segment (and the byte after it) is re-read from L2 here, so no class word has to
             // stay live through the common path.
@@ -1453,7 +1453,10 @@ __device__ __forceinline__ u64 walk_wave(ScanShared& sh, const ScanArgs& a0, u32
         sh.bcol[wid][lane] = sc.col;
         sh.beol[wid][lane] = sc.eol;
         lds_fence();
-        if (parse && !uniform_flag(sh.spec_bad) && !(ABLATE & 1u)) parse_own_headers(sh, a, t, sc, L0 + lines, lane, wid);
+        // (a speculation buffer that overflowed mid-walk, sh.spec_bad, is not checked per tile: the chunk is
+        // redone exactly and everything its walk buffered is discarded, so parsing on is harmless; the check
+        // was an LDS round trip per tile)
+        if (parse && !(ABLATE & 1u)) parse_own_headers(sh, a, t, sc, L0 + lines, lane, wid);
         lines += sc.wtot;
     }
     lds_fence();

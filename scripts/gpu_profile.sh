@@ -20,7 +20,7 @@ fi
 if [[ ${STREAM:-0} == 1 ]]; then  # calibration: FETCH_SIZE of the stream-only ablation (no parse, no table):
   # the experiment build scripts/build_exp.sh stream "-DFR_ABLATE=1" (ablations are compile-time only)
   FRENDER_HIP_LIB="$R/frender_amd/libfrender_hip_exp_stream.so" timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$R/gpurun_out/prof_fetch_stream" -o run \
-      -- python3 "$R/bench.py" $ARGS > "$R/gpurun_out/prof_fetch_stream.log" 2>&1 || { echo "pmc stream fetch failed"; exit 1; }
+      -- python3 "$R/bench.py" $ARGS --pin-json "$R/no-pin-for-the-ablation.json" > "$R/gpurun_out/prof_fetch_stream.log" 2>&1 || { echo "pmc stream fetch failed"; exit 1; }
 fi
 cd "$R"
 find gpurun_out/prof_trace -name "*kernel_stats.csv" | head -1 | xargs cat | head -20

@@ -116,6 +116,10 @@ struct fr_ctx {
     bool file_open = false;
     u32 file_tag = 0;         // current (last) file's tag = file index + 1; increases within a scan
     u32 first_tag = 0;        // the first file's tag since fr_reset (0: none yet)
+    // the first file's presence scan, deferred by fr_end_file (0: none pending): its pairs are every live
+    // key.  A second file runs the scan before it tallies (flush_presence); a scan of that one file ends
+    // with fr_finalize writing its pairs straight from the finalized table (launch_presence_one_file)
+    u32 pres_defer_tag = 0;
     u64 file_base = 0;        // file offset of the current file's first fed byte (fr_begin_file_at)
     bool merged = false;  // the table holds ordinals merged from other contexts (any file tag)
     u64 max_file_bytes = 0;  // bytes of the longest file tallied since fr_reset (ordinal offsets are below it)
@@ -306,6 +310,19 @@ static int ensure_presence_cap(fr_ctx* ctx) {
     ctx->tab.pres = np;
     ctx->tab.pres_cap = ncap;
     return FR_OK;
+}
+
+// the deferred presence scan of the first file (see fr_ctx::pres_defer_tag), before anything else
+// changes the table's last tags
+static int flush_presence(fr_ctx* ctx) {
+    if (!ctx->pres_defer_tag) return FR_OK;
+    int rc = ensure_presence_cap(ctx);
+    if (rc) return rc;
+    ctx->st_fresh = false;
+    CK(launch_presence_scan(ctx->tab.slots, ctx->nslots, ctx->pres_defer_tag, ctx->tab.pres, ctx->tab.pres_cap,
+                            ctx->st, ctx->stream));
+    ctx->pres_defer_tag = 0;
+    return read_state(ctx);
 }
 
 // called before each tally launch: act on the latest asynchronous snapshot, if ready
@@ -867,6 +884,7 @@ int fr_reset(fr_ctx* ctx) {
     ctx->file_open = false;
     ctx->file_tag = 0;
     ctx->first_tag = 0;
+    ctx->pres_defer_tag = 0;
     ctx->merged = false;
     ctx->max_file_bytes = 0;
     ctx->par = 0;
@@ -898,7 +916,9 @@ int fr_begin_file_at(fr_ctx* ctx, int64_t file_index, uint64_t byte_base, int64_
     if ((u32)file_index + 1u <= ctx->file_tag)
         return fail(ctx, FR_ERR_INVALID, "fr_begin_file_at: file indices must increase within a scan");
     if (byte_base >= (1ull << ORD_SHIFT)) return fail(ctx, FR_ERR_INVALID, "fr_begin_file_at: byte base too large");
-    int rc = read_state(ctx);
+    int rc = flush_presence(ctx);  // the first file's pairs, before this file changes any last tag
+    if (rc) return rc;
+    rc = read_state(ctx);
     if (rc) return rc;
     ctx->pres_before = ctx->h_st->n_presence;
     ctx->exo_new_file = 0;
@@ -1100,11 +1120,17 @@ int fr_end_file(fr_ctx* ctx, fr_file_stats* out) {
     ctx->last_valid = false;
     rc = grow_table(ctx, false);  // re-inserts any overflow; exact state afterwards
     if (rc) return rc;
-    rc = ensure_presence_cap(ctx);
-    if (rc) return rc;
-    ctx->st_fresh = false;
-    CK(launch_presence_scan(ctx->tab.slots, ctx->nslots, ctx->file_tag, ctx->tab.pres, ctx->tab.pres_cap, ctx->st,
-                            ctx->stream));
+    // the first file since the reset: every live key is its (it made them all), so its presence scan waits
+    // until a second file begins (flush_presence) -- a one-file scan never runs it (fr_finalize)
+    const bool defer = ctx->file_tag == ctx->first_tag && !ctx->merged && ctx->pres_before == 0 &&
+                       ctx->h_st->n_presence == 0;
+    if (!defer) {
+        rc = ensure_presence_cap(ctx);
+        if (rc) return rc;
+        ctx->st_fresh = false;
+        CK(launch_presence_scan(ctx->tab.slots, ctx->nslots, ctx->file_tag, ctx->tab.pres, ctx->tab.pres_cap,
+                                ctx->st, ctx->stream));
+    }
     rc = read_state(ctx);
     if (rc) return rc;
     const DevState& s = *ctx->h_st;
@@ -1118,7 +1144,8 @@ int fr_end_file(fr_ctx* ctx, fr_file_stats* out) {
     std::memset(out, 0, sizeof(*out));
     out->records = records;
     out->lines = lines;
-    out->new_keys = s.n_presence - ctx->pres_before + ctx->exo_new_file;
+    out->new_keys = (defer ? s.n_keys : s.n_presence - ctx->pres_before) + ctx->exo_new_file;
+    if (defer) ctx->pres_defer_tag = ctx->file_tag;
     out->exotic = ctx->exo_records_file;
     out->error = FR_SCAN_OK;
     if (s.utf8_bad) {
@@ -1251,7 +1278,7 @@ int fr_finalize(fr_ctx* ctx, uint64_t* n_unique, uint64_t* n_presence, uint64_t*
                          ctx->stream));
         CK(launch_set_uidx(ctx->tab.slots, ctx->tab.mask, ctx->d_keys_s, nk, ctx->d_rank, ctx->stream));
     }
-    const u64 np = std::min<u64>(ctx->h_st->n_presence, ctx->tab.pres_cap);
+    const u64 np = ctx->pres_defer_tag ? nk : std::min<u64>(ctx->h_st->n_presence, ctx->tab.pres_cap);
     if (np > ctx->pmap_cap) {
         if (ctx->d_pres_u) CK(hipFree(ctx->d_pres_u));
         if (ctx->d_pres_f) CK(hipFree(ctx->d_pres_f));
@@ -1261,8 +1288,12 @@ int fr_finalize(fr_ctx* ctx, uint64_t* n_unique, uint64_t* n_presence, uint64_t*
         CK(dalloc(&ctx->d_pres_c, np));
         ctx->pmap_cap = np;
     }
-    CK(launch_presence_map(ctx->tab.slots, ctx->tab.mask, ctx->tab.pres, np, ctx->d_pres_u, ctx->d_pres_f,
-                           ctx->d_pres_c, ctx->stream));
+    if (ctx->pres_defer_tag)  // one file: its pairs are the finalized table itself
+        CK(launch_presence_one_file(ctx->d_counts_s, np, ctx->pres_defer_tag, ctx->d_pres_u, ctx->d_pres_f,
+                                    ctx->d_pres_c, ctx->stream));
+    else
+        CK(launch_presence_map(ctx->tab.slots, ctx->tab.mask, ctx->tab.pres, np, ctx->d_pres_u, ctx->d_pres_f,
+                               ctx->d_pres_c, ctx->stream));
     *ctx->h_fin = 0;
     if (nbins)  // the scan's last entry: every live slot counted once
         CK(hipMemcpyAsync(ctx->h_fin, ctx->d_binbase + nbins, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
@@ -1540,8 +1571,10 @@ int fr_merge_unique_device(fr_ctx* ctx, const void* dev_keys, const void* dev_co
                            uint64_t n) {
     if (int src = settle_finalize(ctx)) return src;
     if (ctx->file_open) return fail(ctx, FR_ERR_INVALID, "fr_merge_unique_device: a file is open");
+    int rc = flush_presence(ctx);  // this context's own file, before merged rows change the table
+    if (rc) return rc;
     ctx->merged = true;
-    int rc = read_state(ctx);
+    rc = read_state(ctx);
     if (rc) return rc;
     if ((ctx->h_st->n_keys + n) * 2 > ctx->nslots) {
         rc = grow_table(ctx, true);

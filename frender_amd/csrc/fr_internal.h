@@ -275,6 +275,8 @@ hipError_t launch_order(const u64* first_in, const u32* pos_in, u64 n, u64* firs
                         void* temp, size_t* temp_bytes, int begin_bit, int end_bit, hipStream_t s);
 hipError_t launch_gather(const u32* perm, u64 n, const u64* keys, const u64* counts, u64* keys_o,
                          u64* counts_o, u32* rank, hipStream_t s);
+hipError_t launch_presence_one_file(const u64* counts, u64 n, u32 tag, u32* uidx, u32* file_idx, u64* snap,
+                                    hipStream_t s);
 hipError_t launch_presence_map(const GSlot* slots, u64 mask, const Presence* pres, u64 n, u32* uidx,
                                u32* file_idx, u64* snap, hipStream_t s);
 // first-occurrence order by binning (fr_finalize without merged rows)

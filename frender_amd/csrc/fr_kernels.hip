@@ -2241,6 +2241,25 @@ __global__ void presence_map_kernel(const GSlot* slots, u64 mask, const Presence
     }
 }
 
+// The presence pairs of a scan of one file (fr_finalize when fr_end_file deferred that file's scan):
+// every finalized code, in final order, present in that file with its whole count -- what
+// presence_scan_kernel + presence_map_kernel would give, without the two passes over the table.
+__global__ void presence_one_file_kernel(const u64* counts, u64 n, u32 tag, u32* uidx, u32* file_idx, u64* snap) {
+    for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
+        uidx[i] = (u32)i;
+        file_idx[i] = tag - 1u;
+        snap[i] = counts[i] & ((1ull << (64 - PRES_TAG_BITS)) - 1ull);
+    }
+}
+
+hipError_t launch_presence_one_file(const u64* counts, u64 n, u32 tag, u32* uidx, u32* file_idx, u64* snap,
+                                    hipStream_t s) {
+    if (!n) return hipSuccess;
+    const int grid = (int)std::min<u64>((n + 255) / 256, 8192);
+    hipLaunchKernelGGL(presence_one_file_kernel, dim3(grid), dim3(256), 0, s, counts, n, tag, uidx, file_idx, snap);
+    return hipGetLastError();
+}
+
 hipError_t launch_presence_map(const GSlot* slots, u64 mask, const Presence* pres, u64 n, u32* uidx,
                                u32* file_idx, u64* snap, hipStream_t s) {
     if (!n) return hipSuccess;

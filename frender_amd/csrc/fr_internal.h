@@ -171,6 +171,8 @@ struct ScanArgs {
                          // last ramp_g shrink linearly (chunk_bounds), so workgroups finish their chunks
                          // (look-back, HBM commit) at staggered times and all run out of work together
     u32 mid_chunks;      // full chunks between the two ramps
+    u32 ramp_up_s;       // the smallest chunk of the ramp-up / ramp-down (tiles, >= 1; FR_RAMP_UP_S,
+    u32 ramp_down_s;     // FR_RAMP_DOWN_S)
     u32 chunk_tiles_h;   // the heavy geometry of the same ramped launch (num_chunks_h = 0: none; the
     u32 mid_chunks_h;    // kernel picks it when DevState::heavy[par] is set)
     u32 num_chunks_h;
@@ -193,6 +195,11 @@ struct ScanArgs {
     Table tabv;          // the table by value: read from the kernarg segment where used (scalar loads,
                          // no dependent global load before a commit's first slot load)
 };
+
+// tiles before ramp chunk j of a ramp of G chunks growing from s to C tiles (chunk_bounds)
+__host__ __device__ inline u64 ramp_tiles_before(u64 C, u64 G, u64 s, u64 j) {
+    return s * j + ((C - s) * j * (j + 1)) / (2ull * G);
+}
 
 struct SheetArgs {
     int S;

@@ -1115,6 +1115,29 @@ __device__ __attribute__((noinline)) void commit_buffers(ScanShared& sh, const S
             ck[b] = cv[b] ? cl[2 * i] : 0;
             co[b] = cv[b] ? cl[2 * i + 1] : 0;
         }
+        Resolved rc[CL];
+#if defined(FR_COMMIT_JOINT)  // the LDS slots and the first cold batch resolved in one set of rounds
+        {
+            u64 jk[2 * CL];
+            bool jv[2 * CL];
+            Resolved jr[2 * CL];
+#pragma unroll
+            for (int b = 0; b < CL; ++b) {
+                jk[b] = sh.ls[tid + b * WG].key;
+                jv[b] = jk[b] != 0;
+                jk[CL + b] = ck[b];
+                jv[CL + b] = cv[b];
+            }
+            made += resolve_batch<2 * CL>(a, jk, jv, jr);
+#pragma unroll
+            for (int b = 0; b < CL; ++b) {
+                park[tid + b * WG] = jr[b];
+                rc[b] = jr[CL + b];
+            }
+        }
+        FR_CSTAMP(1);
+        FR_CSTAMP(2);
+#else
         {
             u64 lk[CL];
             bool lv[CL];
@@ -1129,9 +1152,9 @@ __device__ __attribute__((noinline)) void commit_buffers(ScanShared& sh, const S
             for (int b = 0; b < CL; ++b) park[tid + b * WG] = rs[b];
         }
         FR_CSTAMP(1);
-        Resolved rc[CL];
         made += resolve_batch<CL>(a, ck, cv, rc);
         FR_CSTAMP(2);
+#endif
         // every slot is known: the updates, none waited for
 #pragma unroll
         for (int b = 0; b < CL; ++b) {
@@ -1465,13 +1488,14 @@ __device__ __forceinline__ u64 walk_wave(ScanShared& sh, const ScanArgs& a0, u32
     return lines;
 }
 
-// Tiles [tb, te) of chunk c.  Uniform: chunk_tiles each.  Ramped (ramp_g = G > 0, C = chunk_tiles):
-// R(j) = j + floor((C-1) j (j+1) / 2G) tiles precede ramp-up chunk j, so chunk j holds
-// 1 + ~(C-1)(j+1)/G tiles and the G first chunks, all taken at once, finish in ticket order;
-// mid_chunks full chunks follow; the last G chunks mirror the ramp-up, so every workgroup runs
-// out of work at about the same time.  fr_api only ramps ranges of >= 2 R(G) + C tiles.
-__device__ __forceinline__ u64 ramp_prefix(const ScanArgs& a, const Geom& g, u64 j) {
-    return j + ((u64)(g.chunk_tiles - 1u) * j * (j + 1)) / (2ull * a.ramp_g);
+// Tiles [tb, te) of chunk c.  Uniform: chunk_tiles each.  Ramped (ramp_g = G > 0, C = chunk_tiles,
+// s = the ramp's smallest chunk): R_s(j) = s j + floor((C-s) j (j+1) / 2G) tiles precede ramp-up
+// chunk j, so chunk j holds s + ~(C-s)(j+1)/G tiles and the G first chunks, all taken at once, finish
+// in ticket order; mid_chunks full chunks follow; the last G chunks mirror the ramp-up (smallest
+// chunk ramp_down_s), so every workgroup runs out of work at about the same time.  fr_api only ramps
+// ranges of >= R_up(G) + R_down(G) + C tiles (ramp_prefix in fr_internal.h, shared with the host).
+__device__ __forceinline__ u64 ramp_prefix(const ScanArgs& a, const Geom& g, u64 j, u32 s0) {
+    return ramp_tiles_before(g.chunk_tiles, a.ramp_g, s0, j);
 }
 
 // Run by the workgroup that finishes the launch's last chunk: the exact line prefix of every chunk
@@ -1519,20 +1543,44 @@ __device__ __forceinline__ void chunk_bounds(const ScanArgs& a, const Geom& g, u
         te = min(tb + g.chunk_tiles, a.num_tiles);
         return;
     }
-    const u64 G = a.ramp_g, rg = ramp_prefix(a, g, G), mid_end = (u64)a.num_tiles - rg;
+    const u32 su = min(a.ramp_up_s, g.chunk_tiles), sd = min(a.ramp_down_s, g.chunk_tiles);
+    const u64 G = a.ramp_g, rg = ramp_prefix(a, g, G, su), mid_end = (u64)a.num_tiles - ramp_prefix(a, g, G, sd);
     if (c < G) {
-        tb = (u32)ramp_prefix(a, g, c);
-        te = (u32)ramp_prefix(a, g, c + 1);
+        tb = (u32)ramp_prefix(a, g, c, su);
+        te = (u32)ramp_prefix(a, g, c + 1, su);
     } else if (c < G + g.mid_chunks) {
         const u64 b = rg + (u64)(c - G) * g.chunk_tiles;
         tb = (u32)b;
         te = (u32)min(b + g.chunk_tiles, mid_end);
     } else {
         const u64 j = c - G - g.mid_chunks;  // 0 .. G-1: shrinking
-        tb = (u32)((u64)a.num_tiles - ramp_prefix(a, g, G - j));
-        te = (u32)((u64)a.num_tiles - ramp_prefix(a, g, G - j - 1));
+        tb = (u32)((u64)a.num_tiles - ramp_prefix(a, g, G - j, sd));
+        te = (u32)((u64)a.num_tiles - ramp_prefix(a, g, G - j - 1, sd));
     }
 }
+
+#if defined(FR_STAMPS) && FR_STAMPS == 3  // diagnostic builds only: a timeline of every chunk and workgroup
+constexpr u32 TRACE_CHUNKS = 1u << 14;  // per launch parity
+constexpr u32 TRACE_WGS = 4096;
+__device__ u64 g_chunk_trace[2 * TRACE_CHUNKS * 4];  // per ticket: {wg | xcc << 16 | tiles << 32, ticket, walked, committed}
+__device__ u64 g_wg_trace[2 * TRACE_WGS * 2];        // per workgroup: {entry, exit} (s_memrealtime, 100 MHz)
+__device__ __forceinline__ u32 xcc_id() {
+    u32 x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    return x & 0xFu;
+}
+extern "C" int fr_trace_read(u64* chunks, u64* wgs) {
+    if (hipMemcpyFromSymbol(chunks, HIP_SYMBOL(g_chunk_trace), sizeof(g_chunk_trace)) != hipSuccess) return 1;
+    if (hipMemcpyFromSymbol(wgs, HIP_SYMBOL(g_wg_trace), sizeof(g_wg_trace)) != hipSuccess) return 1;
+    return 0;
+}
+extern "C" int fr_trace_clear() {
+    static u64 zero[2 * TRACE_CHUNKS * 4];
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_chunk_trace), zero, sizeof(g_chunk_trace)) != hipSuccess) return 1;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_wg_trace), zero, sizeof(g_wg_trace)) != hipSuccess) return 1;
+    return 0;
+}
+#endif
 
 #ifndef FR_OCC
 #define FR_OCC 4  // workgroups (= waves per SIMD) per CU: ~39 KB of LDS per workgroup (the wave-tile copies
@@ -1564,6 +1612,10 @@ __global__ __launch_bounds__(WG, FR_OCC) void chunk_kernel(ScanArgs args) {
         sh.nexo = 0;
         sh.err_off = 0xFFFFFFFFu;
     }
+#if defined(FR_STAMPS) && FR_STAMPS == 3
+    if (tid == 0 && blockIdx.x < TRACE_WGS) g_wg_trace[(a.par * TRACE_WGS + blockIdx.x) * 2] = __builtin_amdgcn_s_memrealtime();
+    u64 tl_t0 = 0;
+#endif
     const u64 base_lines = a.st->lines[a.par];
     // the geometry: heavy when the previous launch said so (ramped launches that have a heavy set)
     const bool hv = a.num_chunks_h != 0 &&
@@ -1576,9 +1628,16 @@ __global__ __launch_bounds__(WG, FR_OCC) void chunk_kernel(ScanArgs args) {
     const u64 k0_ = __builtin_amdgcn_s_memtime();
 #endif
     FR_STAMP_DECL
-    for (;;) {
+    for (bool first = true;; first = false) {
         if (tid == 0) {
+#ifndef FR_TICKET_ALL
+            // the first chunk is the workgroup's own index, the rest go by ticket after the grid's first
+            // chunks: 1024 workgroups no longer queue on one counter at the launch start (serialised
+            // same-address atomics: ~12 us before the last workgroup had its first chunk)
+            sh.chunk = first ? blockIdx.x : gridDim.x + atomicAdd(&a.st->ticket, 1u);
+#else
             sh.chunk = atomicAdd(&a.st->ticket, 1u);
+#endif
             sh.spec = 1u;  // pass 0 runs on guessed phases: side effects are buffered
         }
         __syncthreads();
@@ -1587,6 +1646,9 @@ __global__ __launch_bounds__(WG, FR_OCC) void chunk_kernel(ScanArgs args) {
         if (c >= g.num_chunks) break;
         u32 tb, te;
         chunk_bounds(a, g, c, tb, te);
+#if defined(FR_STAMPS) && FR_STAMPS == 3
+        if (tid == 0) tl_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
         const u32 per = (te - tb + NW - 1) / NW;  // this wave's part of the chunk: [wb, we)
         const u32 wb = min(tb + wid * per, te), we = min(wb + per, te);
         // ---- pass 0: chunk 0's first wave starts at the range's exact line count; every other
@@ -1690,7 +1752,19 @@ __global__ __launch_bounds__(WG, FR_OCC) void chunk_kernel(ScanArgs args) {
         }
         FR_TRACE("w%d commit\n", (int)wid);
         FR_STAMP(3);
+#if defined(FR_STAMPS) && FR_STAMPS == 3
+        const u64 tl_t1 = __builtin_amdgcn_s_memrealtime();
+#endif
         commit_buffers(sh, a, tid, g, hv);  // starts and ends with a barrier: sh.last is visible
+#if defined(FR_STAMPS) && FR_STAMPS == 3
+        if (tid == 0 && c < TRACE_CHUNKS) {
+            u64* e = &g_chunk_trace[(a.par * TRACE_CHUNKS + c) * 4];
+            e[0] = (u64)blockIdx.x | ((u64)xcc_id() << 16) | ((u64)(te - tb) << 32);
+            e[1] = tl_t0;
+            e[2] = tl_t1;
+            e[3] = __builtin_amdgcn_s_memrealtime();
+        }
+#endif
         FR_TRACE("w%d committed last %u\n", (int)wid, sh.last);
         if (sh.last) {  // once per launch: the acquire is cheap here (chunk_info is read with sc1 loads anyway)
             __atomic_thread_fence(__ATOMIC_ACQUIRE);
@@ -1700,6 +1774,9 @@ __global__ __launch_bounds__(WG, FR_OCC) void chunk_kernel(ScanArgs args) {
     }
 #if defined(FR_STAMPS) && FR_STAMPS == 1
     FR_STAMP_FLUSH(k0_);
+#endif
+#if defined(FR_STAMPS) && FR_STAMPS == 3
+    if (tid == 0 && blockIdx.x < TRACE_WGS) g_wg_trace[(a.par * TRACE_WGS + blockIdx.x) * 2 + 1] = __builtin_amdgcn_s_memrealtime();
 #endif
     __syncthreads();
     if (tid == 0) {

@@ -188,11 +188,7 @@ struct fr_ctx {
     u32* d_arr = nullptr;  // per table slot: arrival index in its bin
     u64 arr_cap = 0;
     FinRow* d_rows = nullptr;  // live slots grouped by bin
-    FinRow* d_rows2 = nullptr;  // ... by coarse bucket, then (d_rows) by bin
     u64 rows_cap = 0;
-    u32* d_cbase = nullptr;  // coarse-bucket starts per (bucket, workgroup) (fin_count's scan)
-    u64 cbase_cap = 0;
-    bool fin_old = true;     // fin_hist / fin_scatter (a global atomic per code); FR_FIN_OLD=0: coarse buckets
     u64 n_pres = 0;
     u64 pmap_cap = 0;
     u32 *d_pres_u = nullptr, *d_pres_f = nullptr;
@@ -633,7 +629,6 @@ fr_ctx* fr_create(int device, uint64_t chunk_bytes, uint64_t table_slots) {
     ctx->grid = prop.multiProcessorCount * per_cu;
     if (const char* g = getenv("FR_GRID")) ctx->grid = std::max(1, atoi(g));
     if (const char* f = getenv("FR_FLUSH_AT")) ctx->flush_at = (u32)atoi(f);
-    if (const char* f = getenv("FR_FIN_OLD")) ctx->fin_old = atoi(f) != 0;
     if (const char* f = getenv("FR_NBR")) ctx->nbr_enabled = atoi(f) != 0;
     if (const char* f = getenv("FR_COLD_CAP")) ctx->cold_cap = (u32)std::max(1024, atoi(f));
     if ((e = dalloc(&ctx->cold, 2ull * ctx->cold_cap * (u64)ctx->grid)) != hipSuccess) return bad("cold lists", e);
@@ -723,7 +718,7 @@ void fr_destroy(fr_ctx* ctx) {
     void* dev[] = {ctx->st, ctx->d_tab, ctx->tiles, ctx->tab.slots, ctx->tab.ovf, ctx->tab.pres, ctx->tab.exo_ord,
                    ctx->tab.exo_off, ctx->tab.exo_len, ctx->tab.exo_pool, ctx->dbuf[0], ctx->dbuf[1], ctx->d_sheet,
                    ctx->d_keys, ctx->d_counts, ctx->d_first, ctx->d_keys_s, ctx->d_counts_s,
-                   ctx->d_first_s, ctx->d_pos, ctx->d_perm, ctx->d_rank, ctx->d_counter, ctx->d_temp, ctx->d_bins, ctx->d_binbase, ctx->d_arr, ctx->d_rows, ctx->d_rows2, ctx->d_cbase, ctx->d_pres_u,
+                   ctx->d_first_s, ctx->d_pos, ctx->d_perm, ctx->d_rank, ctx->d_counter, ctx->d_temp, ctx->d_bins, ctx->d_binbase, ctx->d_arr, ctx->d_rows, ctx->d_pres_u,
                    ctx->d_pres_f, ctx->d_pres_c, ctx->d_m1, ctx->d_m2, ctx->d_row, ctx->d_rm2, ctx->d_rrow, ctx->d_cls, ctx->d_rcls,
                    ctx->d_errw, ctx->d_errf, ctx->d_nbr, ctx->cold, ctx->rare, ctx->chunk_info, ctx->log, ctx->log_sub, ctx->log_temp};
     for (void* p : dev)
@@ -1222,7 +1217,7 @@ int fr_finalize(fr_ctx* ctx, uint64_t* n_unique, uint64_t* n_presence, uint64_t*
     if (nbins) {
         bm.nbins = nbins;
         bm.cap = ctx->ucap;
-        if (ctx->fin_old && ctx->nslots > ctx->arr_cap) {
+        if (ctx->nslots > ctx->arr_cap) {
             if (ctx->d_arr) CK(hipFree(ctx->d_arr));
             ctx->d_arr = nullptr;
             CK(hipMalloc(&ctx->d_arr, ctx->nslots * sizeof(u32)));
@@ -1230,32 +1225,21 @@ int fr_finalize(fr_ctx* ctx, uint64_t* n_unique, uint64_t* n_presence, uint64_t*
         }
         if (ctx->ucap > ctx->rows_cap) {
             if (ctx->d_rows) CK(hipFree(ctx->d_rows));
-            if (ctx->d_rows2) CK(hipFree(ctx->d_rows2));
-            ctx->d_rows = ctx->d_rows2 = nullptr;
+            ctx->d_rows = nullptr;
             CK(hipMalloc(&ctx->d_rows, ctx->ucap * sizeof(FinRow)));
-            CK(hipMalloc(&ctx->d_rows2, ctx->ucap * sizeof(FinRow)));
             ctx->rows_cap = ctx->ucap;
         }
-        const FinBuckets fb = fin_buckets(ctx->nslots, nbins);
-        const u64 nh = (u64)fb.nc * fb.groups + 1;  // fin_count's counts and the scan's total
-        if (!ctx->fin_old && nh > ctx->cbase_cap) {
-            if (ctx->d_cbase) CK(hipFree(ctx->d_cbase));
-            ctx->d_cbase = nullptr;
-            CK(hipMalloc(&ctx->d_cbase, nh * sizeof(u32)));
-            ctx->cbase_cap = nh;
-        }
-        if (std::max<u64>(nbins + 1, nh) > ctx->bins_cap) {
+        if (nbins + 1 > ctx->bins_cap) {
             if (ctx->d_bins) CK(hipFree(ctx->d_bins));
             if (ctx->d_binbase) CK(hipFree(ctx->d_binbase));
             ctx->d_bins = ctx->d_binbase = nullptr;
-            const u64 cap = std::max<u64>(std::max<u64>(nbins + 1, nh), 1u << 16);
+            const u64 cap = std::max<u64>(nbins + 1, 1u << 16);
             CK(hipMalloc(&ctx->d_bins, cap * sizeof(u32)));
             CK(hipMalloc(&ctx->d_binbase, cap * sizeof(u32)));
             ctx->bins_cap = cap;
         }
-        const u64 nscan = ctx->fin_old ? nbins + 1 : nh;
         size_t need = 0;
-        CK(launch_fin_scan(ctx->d_bins, ctx->d_binbase, nscan, nullptr, &need, ctx->stream));
+        CK(launch_fin_scan(ctx->d_bins, ctx->d_binbase, nbins + 1, nullptr, &need, ctx->stream));
         if (need > ctx->temp_bytes) {
             if (ctx->d_temp) CK(hipFree(ctx->d_temp));
             CK(hipMalloc(&ctx->d_temp, need));
@@ -1264,17 +1248,10 @@ int fr_finalize(fr_ctx* ctx, uint64_t* n_unique, uint64_t* n_presence, uint64_t*
         size_t tb = ctx->temp_bytes;
         // the slots' uidx is read only by presence_map_kernel: a one-file scan (deferred presence) skips it
         const bool set_uidx = ctx->pres_defer_tag == 0;
-        if (ctx->fin_old) {
-            CK(hipMemsetAsync(ctx->d_bins, 0, (nbins + 1) * sizeof(u32), ctx->stream));
-            CK(launch_fin_hist(ctx->tab.slots, ctx->nslots, bm, ctx->d_bins, ctx->d_arr, ctx->stream));
-            CK(launch_fin_scan(ctx->d_bins, ctx->d_binbase, nbins + 1, ctx->d_temp, &tb, ctx->stream));
-            CK(launch_fin_scatter(ctx->tab.slots, ctx->nslots, bm, ctx->d_binbase, ctx->d_arr, ctx->d_rows, ctx->stream));
-        } else {
-            CK(launch_fin_count(ctx->tab.slots, ctx->nslots, bm, fb, ctx->d_bins, ctx->stream));
-            CK(launch_fin_scan(ctx->d_bins, ctx->d_cbase, nh, ctx->d_temp, &tb, ctx->stream));
-            CK(launch_fin_bucket(ctx->tab.slots, ctx->nslots, bm, fb, ctx->d_cbase, ctx->d_rows2, ctx->stream));
-            CK(launch_fin_fine(ctx->d_rows2, bm, fb, ctx->d_cbase, ctx->d_binbase, ctx->d_rows, ctx->stream));
-        }
+        CK(hipMemsetAsync(ctx->d_bins, 0, (nbins + 1) * sizeof(u32), ctx->stream));
+        CK(launch_fin_hist(ctx->tab.slots, ctx->nslots, bm, ctx->d_bins, ctx->d_arr, ctx->stream));
+        CK(launch_fin_scan(ctx->d_bins, ctx->d_binbase, nbins + 1, ctx->d_temp, &tb, ctx->stream));
+        CK(launch_fin_scatter(ctx->tab.slots, ctx->nslots, bm, ctx->d_binbase, ctx->d_arr, ctx->d_rows, ctx->stream));
         CK(launch_fin_rank(ctx->tab.slots, nk, bm, ctx->d_binbase, ctx->d_rows, ctx->d_keys_s, ctx->d_counts_s,
                            ctx->d_first_s, set_uidx, ctx->stream));
     } else {

@@ -304,21 +304,6 @@ hipError_t launch_fin_scatter(const GSlot* slots, u64 nslots, const BinMap& m, c
                               FinRow* rows, hipStream_t s);
 hipError_t launch_fin_rank(GSlot* slots, u64 nk, const BinMap& m, const u32* base, const FinRow* rows, u64* keys_o,
                            u64* counts_o, u64* first_o, bool set_uidx, hipStream_t s);
-// the bins grouped into coarse buckets counted in LDS (no global atomic per code): fin_count ->
-// exclusive scan of its nc x groups + 1 counts -> fin_bucket -> fin_fine (fine-bin bases and rows by
-// fine bin) -> fin_rank
-struct FinBuckets {
-    u32 cshift;  // bucket = bin >> cshift
-    u32 nc;      // buckets
-    u32 groups;  // workgroups of fin_count / fin_bucket (FIN_SPW slots each)
-};
-FinBuckets fin_buckets(u64 nslots, u64 nbins);
-hipError_t launch_fin_count(const GSlot* slots, u64 nslots, const BinMap& m, const FinBuckets& b, u32* hist,
-                            hipStream_t s);
-hipError_t launch_fin_bucket(const GSlot* slots, u64 nslots, const BinMap& m, const FinBuckets& b, const u32* cbase,
-                             FinRow* rows, hipStream_t s);
-hipError_t launch_fin_fine(const FinRow* rows, const BinMap& m, const FinBuckets& b, const u32* cbase, u32* binbase,
-                           FinRow* rows2, hipStream_t s);
 hipError_t launch_classify(const u64* keys, const u64* counts, u64 n, SheetArgs sh, int nsubs, int rc,
                            ClassOut o, const NbrMap& nm, hipStream_t s);
 // neighbourhood codes of one sheet row: sum over d <= nsubs of C(L, d) 5^d (every query symbol)

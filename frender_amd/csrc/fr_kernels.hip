@@ -2389,109 +2389,6 @@ __global__ __launch_bounds__(256) void fin_scatter_kernel(const GSlot* slots, u6
     }
 }
 
-// ---- the same bins without a global atomic per code (round 4) --------------------------------
-// fin_hist's returning atomic per live slot on ~1M random bin counters runs at the memory-side atomic
-// rate (~22 G/s: 63 us for the bench's 1.38M codes).  Instead the bins are grouped into <= FIN_NC
-// coarse buckets (bin >> cshift) and counted in LDS:
-//   fin_count   a workgroup per FIN_SPW slots: LDS counts per coarse bucket, written bucket-major
-//               (hist[c G + w]), so one exclusive scan gives every (bucket, workgroup) its start;
-//   fin_bucket  the workgroup reads its slots again and places each live slot's row in its bucket's run
-//               (LDS cursors from the scan);
-//   fin_fine    a workgroup per bucket: LDS counts per fine bin, an LDS scan, the bucket's fine-bin bases
-//               (the old scan's output) and its rows regrouped by fine bin -- what fin_rank reads.
-constexpr int FIN_NC = 1024;     // coarse buckets at most (fine bins per bucket: <= 2^21 / 1024)
-constexpr int FIN_MAXF = 2048;   // fine bins per bucket at most
-constexpr u32 FIN_SPW = 16384;   // slots per workgroup of fin_count / fin_bucket
-constexpr int FIN_WG = 1024;
-
-__global__ __launch_bounds__(FIN_WG) void fin_count_kernel(const GSlot* slots, u64 n, BinMap m, u32 cshift, u32 nc,
-                                                           u32 G, u32* hist) {
-    __shared__ u32 h[FIN_NC];
-    for (u32 c = threadIdx.x; c < nc; c += FIN_WG) h[c] = 0;
-    __syncthreads();
-    const u64 lo = (u64)blockIdx.x * FIN_SPW, hi = min(n, lo + FIN_SPW);
-    for (u64 i = lo + threadIdx.x; i < hi; i += FIN_WG) {
-        const uint4 w0 = *(const uint4*)&slots[i];
-        const uint4 w1 = *((const uint4*)&slots[i] + 1);
-        if ((w0.x | w0.y) != 0u) atomicAdd(&h[(u32)(ord_bin(m, ((u64)w1.y << 32) | w1.x) >> cshift)], 1u);
-    }
-    __syncthreads();
-    for (u32 c = threadIdx.x; c < nc; c += FIN_WG) hist[(u64)c * G + blockIdx.x] = h[c];
-    if (blockIdx.x == 0 && threadIdx.x == 0) hist[(u64)nc * G] = 0;  // the scan's total
-}
-
-__global__ __launch_bounds__(FIN_WG) void fin_bucket_kernel(const GSlot* slots, u64 n, BinMap m, u32 cshift, u32 nc,
-                                                            u32 G, const u32* cbase, FinRow* rows) {
-    __shared__ u32 cur[FIN_NC];
-    for (u32 c = threadIdx.x; c < nc; c += FIN_WG) cur[c] = cbase[(u64)c * G + blockIdx.x];
-    __syncthreads();
-    const u64 lo = (u64)blockIdx.x * FIN_SPW, hi = min(n, lo + FIN_SPW);
-    for (u64 i = lo + threadIdx.x; i < hi; i += FIN_WG) {
-        const uint4 w0 = *(const uint4*)&slots[i];
-        const uint4 w1 = *((const uint4*)&slots[i] + 1);
-        if ((w0.x | w0.y) == 0u) continue;
-        const u64 first = ((u64)w1.y << 32) | w1.x;
-        const u32 q = atomicAdd(&cur[(u32)(ord_bin(m, first) >> cshift)], 1u);
-        if (q < m.cap) {
-            typedef u32 u32x4 __attribute__((ext_vector_type(4)));
-            u32x4* d = (u32x4*)&rows[q];
-            d[0] = u32x4{w1.x, w1.y, w0.x, w0.y};
-            d[1] = u32x4{w0.z, w0.w, (u32)i, 0u};
-        }
-    }
-}
-
-constexpr int FINF_WG = 512;
-__global__ __launch_bounds__(FINF_WG) void fin_fine_kernel(const FinRow* rows, BinMap m, u32 cshift, u32 G,
-                                                           const u32* cbase, u32* binbase, FinRow* rows2) {
-    __shared__ u32 fh[FIN_MAXF];
-    __shared__ u32 part[FINF_WG / 64];
-    const u32 c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const u32 start = cbase[(u64)c * G], end = min(cbase[(u64)(c + 1) * G], (u32)m.cap);
-    const u64 b0 = (u64)c << cshift;
-    const u32 nf = (u32)min((u64)1 << cshift, m.nbins - b0);  // this bucket's fine bins
-    for (u32 i = tid; i < nf; i += FINF_WG) fh[i] = 0;
-    __syncthreads();
-    for (u32 j = start + tid; j < end; j += FINF_WG) atomicAdd(&fh[(u32)(ord_bin(m, rows[j].first) - b0)], 1u);
-    __syncthreads();
-    // exclusive scan of fh[0, nf): FIN_MAXF / FINF_WG consecutive entries per thread, then the threads' sums
-    constexpr u32 PER = FIN_MAXF / FINF_WG;
-    u32 v[PER], s = 0;
-#pragma unroll
-    for (u32 k = 0; k < PER; ++k) {
-        const u32 i = tid * PER + k;
-        v[k] = i < nf ? fh[i] : 0u;
-        s += v[k];
-    }
-    u32 x = s;  // inclusive wave scan
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const u32 y = __shfl_up(x, d, 64);
-        if (lane >= (u32)d) x += y;
-    }
-    if (lane == 63) part[wv] = x;
-    __syncthreads();
-    u32 wbase = 0;
-    for (u32 k = 0; k < wv; ++k) wbase += part[k];
-    u32 run = start + wbase + x - s;
-#pragma unroll
-    for (u32 k = 0; k < PER; ++k) {
-        const u32 i = tid * PER + k;
-        if (i < nf) {
-            fh[i] = run;
-            binbase[b0 + i] = run;
-        }
-        run += v[k];
-    }
-    if (b0 + nf == m.nbins && tid == 0) binbase[m.nbins] = end;  // the last bucket: every live row counted
-    __syncthreads();
-    for (u32 j = start + tid; j < end; j += FINF_WG) {
-        const FinRow r = rows[j];
-        const u32 q = atomicAdd(&fh[(u32)(ord_bin(m, r.first) - b0)], 1u);
-        rows2[q] = r;
-    }
-}
-
 // final index = the bin's base + the codes of the bin with a smaller ordinal (ties: slot index,
 // never met for one context's ordinals); the row goes there and the slot's uidx becomes that index
 __global__ __launch_bounds__(256) void fin_rank_kernel(GSlot* slots, u64 nk, BinMap m, const u32* base,
@@ -2538,36 +2435,6 @@ hipError_t launch_fin_rank(GSlot* slots, u64 nk, const BinMap& m, const u32* bas
     if (!nk) return hipSuccess;
     hipLaunchKernelGGL(fin_rank_kernel, dim3(lane_grid(nk)), dim3(256), 0, s, slots, nk, m, base, rows, keys_o,
                        counts_o, first_o, set_uidx ? 1 : 0);
-    return hipGetLastError();
-}
-
-FinBuckets fin_buckets(u64 nslots, u64 nbins) {
-    FinBuckets b;
-    b.cshift = 0;
-    while (((nbins - 1) >> b.cshift) >= (u64)FIN_NC) ++b.cshift;
-    b.nc = (u32)(((nbins - 1) >> b.cshift) + 1);
-    b.groups = (u32)std::max<u64>(1, (nslots + FIN_SPW - 1) / FIN_SPW);
-    return b;
-}
-
-hipError_t launch_fin_count(const GSlot* slots, u64 nslots, const BinMap& m, const FinBuckets& b, u32* hist,
-                            hipStream_t s) {
-    hipLaunchKernelGGL(fin_count_kernel, dim3(b.groups), dim3(FIN_WG), 0, s, slots, nslots, m, b.cshift, b.nc, b.groups,
-                       hist);
-    return hipGetLastError();
-}
-
-hipError_t launch_fin_bucket(const GSlot* slots, u64 nslots, const BinMap& m, const FinBuckets& b, const u32* cbase,
-                             FinRow* rows, hipStream_t s) {
-    hipLaunchKernelGGL(fin_bucket_kernel, dim3(b.groups), dim3(FIN_WG), 0, s, slots, nslots, m, b.cshift, b.nc,
-                       b.groups, cbase, rows);
-    return hipGetLastError();
-}
-
-hipError_t launch_fin_fine(const FinRow* rows, const BinMap& m, const FinBuckets& b, const u32* cbase, u32* binbase,
-                           FinRow* rows2, hipStream_t s) {
-    hipLaunchKernelGGL(fin_fine_kernel, dim3(b.nc), dim3(FINF_WG), 0, s, rows, m, b.cshift, b.groups, cbase, binbase,
-                       rows2);
     return hipGetLastError();
 }
 

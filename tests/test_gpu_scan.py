@@ -906,15 +906,12 @@ def test_bgzf_scan_matches_oracle(tmp_path, corrupt):
 # ---------------------------------------------------------------------------------------
 # first-occurrence order by binning (fr_finalize, fin_* kernels)
 # ---------------------------------------------------------------------------------------
-@pytest.mark.parametrize("fin_old", ["1", "0"])
 @pytest.mark.parametrize("mode", ["host", "device"])
-def test_first_occurrence_bins(lib, mode, fin_old, monkeypatch):
+def test_first_occurrence_bins(lib, mode):
     """Dense bins: ~22-B records whose codes are nearly all new, so every 8-KiB bin holds hundreds of
     codes ranked inside the bin; files at non-consecutive indices and one at a large byte base (the
     bins span every file's bytes); codes repeated across files keep their first file's ordinal.
-    Order, counts and records equal the oracle's.  Both finalize pipelines: a global atomic per code
-    (FR_FIN_OLD=1) and coarse buckets counted in LDS (0: a few buckets of tens of thousands of rows)."""
-    monkeypatch.setenv("FR_FIN_OLD", fin_old)
+    Order, counts and records equal the oracle's."""
     rng = np.random.default_rng(17)
     alpha = np.array(list("ACGT"))
     pool = ["".join(rng.choice(alpha, 8)) + "+" + "".join(rng.choice(alpha, 8)) for _ in range(60000)]
@@ -976,8 +973,7 @@ def test_timing_events_off_same_table(lib):
     assert out[0] == out[1]
 
 
-@pytest.mark.parametrize("fin_old", ["1", "0"])
-def test_bench_geometry_pinned_to_reference(lib, fin_old, monkeypatch):
+def test_bench_geometry_pinned_to_reference(lib):
     """bench.py's exact workload and launch geometry (BASELINE config 2: 100M SYN-v1 records in HBM,
     one device feed cut into two 3.7 GB launches of the 1024-workgroup ramped grid, 4 Mi initial
     slots, speculative commits, heavy-chunk switch) against the REFERENCE's own tally_barcodes +
@@ -990,7 +986,6 @@ def test_bench_geometry_pinned_to_reference(lib, fin_old, monkeypatch):
     from frender_amd.host import reverse_complement
     from frender_amd.scan import _sheet_names
 
-    monkeypatch.setenv("FR_FIN_OLD", fin_old)  # both finalize pipelines
     with open(os.path.join(os.path.dirname(__file__), "golden", "cfg2_pin.json")) as f:
         pin = json.load(f)
     n = pin["reads"]

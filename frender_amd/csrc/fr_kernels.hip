@@ -1491,11 +1491,11 @@ __device__ __forceinline__ u64 walk_wave(ScanShared& sh, const ScanArgs& a0, u32
 // Tiles [tb, te) of chunk c.  Uniform: chunk_tiles each.  Ramped (ramp_g = G > 0, C = chunk_tiles,
 // s = the ramp's smallest chunk): R_s(j) = s j + floor((C-s) j (j+1) / 2G) tiles precede ramp-up
 // chunk j, so chunk j holds s + ~(C-s)(j+1)/G tiles and the G first chunks, all taken at once, finish
-// in ticket order; mid_chunks full chunks follow; the last G chunks mirror the ramp-up (smallest
-// chunk ramp_down_s), so every workgroup runs out of work at about the same time.  fr_api only ramps
+// in ticket order; mid_chunks full chunks follow; the last Gd = ramp_down_g chunks shrink the same way
+// (over Gd chunks, smallest ramp_down_s), so every workgroup runs out of work at about the same time.  fr_api only ramps
 // ranges of >= R_up(G) + R_down(G) + C tiles (ramp_prefix in fr_internal.h, shared with the host).
-__device__ __forceinline__ u64 ramp_prefix(const ScanArgs& a, const Geom& g, u64 j, u32 s0) {
-    return ramp_tiles_before(g.chunk_tiles, a.ramp_g, s0, j);
+__device__ __forceinline__ u64 ramp_prefix(const Geom& g, u64 G, u64 j, u32 s0) {
+    return ramp_tiles_before(g.chunk_tiles, G, s0, j);
 }
 
 // Run by the workgroup that finishes the launch's last chunk: the exact line prefix of every chunk
@@ -1544,18 +1544,19 @@ __device__ __forceinline__ void chunk_bounds(const ScanArgs& a, const Geom& g, u
         return;
     }
     const u32 su = min(a.ramp_up_s, g.chunk_tiles), sd = min(a.ramp_down_s, g.chunk_tiles);
-    const u64 G = a.ramp_g, rg = ramp_prefix(a, g, G, su), mid_end = (u64)a.num_tiles - ramp_prefix(a, g, G, sd);
+    const u64 G = a.ramp_g, Gd = a.ramp_down_g;
+    const u64 rg = ramp_prefix(g, G, G, su), mid_end = (u64)a.num_tiles - ramp_prefix(g, Gd, Gd, sd);
     if (c < G) {
-        tb = (u32)ramp_prefix(a, g, c, su);
-        te = (u32)ramp_prefix(a, g, c + 1, su);
+        tb = (u32)ramp_prefix(g, G, c, su);
+        te = (u32)ramp_prefix(g, G, c + 1, su);
     } else if (c < G + g.mid_chunks) {
         const u64 b = rg + (u64)(c - G) * g.chunk_tiles;
         tb = (u32)b;
         te = (u32)min(b + g.chunk_tiles, mid_end);
     } else {
-        const u64 j = c - G - g.mid_chunks;  // 0 .. G-1: shrinking
-        tb = (u32)((u64)a.num_tiles - ramp_prefix(a, g, G - j, sd));
-        te = (u32)((u64)a.num_tiles - ramp_prefix(a, g, G - j - 1, sd));
+        const u64 j = c - G - g.mid_chunks;  // 0 .. Gd-1: shrinking
+        tb = (u32)((u64)a.num_tiles - ramp_prefix(g, Gd, Gd - j, sd));
+        te = (u32)((u64)a.num_tiles - ramp_prefix(g, Gd, Gd - j - 1, sd));
     }
 }
 

@@ -103,7 +103,8 @@ struct fr_ctx {
     // fr_kernels.hip); fr_reset clears it.
     u32 chunk_tiles_heavy = 448;
     u32 ramp_up_s = 1, ramp_down_s = 1;  // the ramps' smallest chunks (tiles)
-    u32 ramp_down_pct = 100;              // ramp-down chunks, % of the grid (FR_RAMP_DOWN_PCT)
+    u32 ramp_down_pct = 100;              // ramp-down chunks, % of the grid (FR_RAMP_DOWN_PCT; the heavy
+    u32 ramp_down_pct_h = 70;             // geometry's: FR_RAMP_DOWN_PCT_H, config-3 shape 3.39 -> 3.29 ms)
     bool ramp = true;      // FR_RAMP=0: one uniform chunk per workgroup
     u8* pin[2] = {nullptr, nullptr};
     u8* dbuf[2] = {nullptr, nullptr};
@@ -557,15 +558,18 @@ static int launch_range(fr_ctx* ctx, const u8* dptr, u64 len, u64 avail, int own
     // chunk, else one uniform chunk per workgroup.  A ramped launch also carries the heavy geometry
     // when the range fits it; the kernel picks one (DevState::heavy)
     const u64 G = (u64)ctx->grid, C = ctx->chunk_tiles, Ch = ctx->chunk_tiles_heavy;
-    const u64 Gd = std::max<u64>(1, G * ctx->ramp_down_pct / 100);
+    // the ramp-down's chunk count: a workgroup's last chunk ends with a commit of roughly fixed length,
+    // so the shrinking chunks are spread over fewer tickets than the grid where commits are long
+    const u64 Gd = std::max<u64>(1, G * ctx->ramp_down_pct / 100), Gdh = std::max<u64>(1, G * ctx->ramp_down_pct_h / 100);
     a.ramp_up_s = ctx->ramp_up_s;
     a.ramp_down_s = ctx->ramp_down_s;
     a.ramp_down_g = (u32)Gd;
-    auto ramps = [&](u64 c) {  // R_up(G) + R_down(Gd) at chunk size c (chunk_bounds)
+    a.ramp_down_g_h = (u32)Gdh;
+    auto ramps = [&](u64 c, u64 gd) {  // R_up(G) + R_down(gd) at chunk size c (chunk_bounds)
         return ramp_tiles_before(c, G, std::min<u64>(ctx->ramp_up_s, c), G) +
-               ramp_tiles_before(c, Gd, std::min<u64>(ctx->ramp_down_s, c), Gd);
+               ramp_tiles_before(c, gd, std::min<u64>(ctx->ramp_down_s, c), gd);
     };
-    const u64 rg = ramps(C), rgh = ramps(Ch);
+    const u64 rg = ramps(C, Gd), rgh = ramps(Ch, Gdh);
     if (ctx->ramp && (u64)a.num_tiles >= rg + C) {
         a.ramp_g = (u32)G;
         a.chunk_tiles = (u32)C;
@@ -574,7 +578,7 @@ static int launch_range(fr_ctx* ctx, const u8* dptr, u64 len, u64 avail, int own
         if (Ch != C && (u64)a.num_tiles >= rgh + Ch) {
             a.chunk_tiles_h = (u32)Ch;
             a.mid_chunks_h = (u32)(((u64)a.num_tiles - rgh + Ch - 1) / Ch);
-            a.num_chunks_h = (u32)(G + Gd) + a.mid_chunks_h;
+            a.num_chunks_h = (u32)(G + Gdh) + a.mid_chunks_h;
         }
     } else {
         a.ramp_g = 0;
@@ -663,6 +667,7 @@ fr_ctx* fr_create(int device, uint64_t chunk_bytes, uint64_t table_slots) {
     if (const char* f = getenv("FR_RAMP_UP_S")) ctx->ramp_up_s = (u32)std::max(1, atoi(f));
     if (const char* f = getenv("FR_RAMP_DOWN_S")) ctx->ramp_down_s = (u32)std::max(1, atoi(f));
     if (const char* f = getenv("FR_RAMP_DOWN_PCT")) ctx->ramp_down_pct = (u32)std::min(100, std::max(1, atoi(f)));
+    if (const char* f = getenv("FR_RAMP_DOWN_PCT_H")) ctx->ramp_down_pct_h = (u32)std::min(100, std::max(1, atoi(f)));
     ctx->tiles_cap = RANGE_MAX / TSTEP + 2;
     ctx->nslots = pow2_at_least(std::max<u64>(table_slots, 1024));
     if ((e = hipMalloc((void**)&ctx->st, sizeof(DevState))) != hipSuccess) return bad("state", e);

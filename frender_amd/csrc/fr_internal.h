@@ -173,7 +173,8 @@ struct ScanArgs {
     u32 mid_chunks;      // full chunks between the two ramps
     u32 ramp_up_s;       // the smallest chunk of the ramp-up / ramp-down (tiles, >= 1; FR_RAMP_UP_S,
     u32 ramp_down_s;     // FR_RAMP_DOWN_S)
-    u32 ramp_down_g;     // chunks of the ramp-down (ramp_g of them grow; FR_RAMP_DOWN_PCT of ramp_g shrink)
+    u32 ramp_down_g;     // chunks of the ramp-down (ramp_g of them grow; FR_RAMP_DOWN_PCT of ramp_g shrink),
+    u32 ramp_down_g_h;   // and of the heavy geometry's (FR_RAMP_DOWN_PCT_H: its commits take longer)
     u32 chunk_tiles_h;   // the heavy geometry of the same ramped launch (num_chunks_h = 0: none; the
     u32 mid_chunks_h;    // kernel picks it when DevState::heavy[par] is set)
     u32 num_chunks_h;

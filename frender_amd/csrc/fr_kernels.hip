@@ -959,7 +959,7 @@ __device__ __forceinline__ void apply_entry(const ScanArgs& a, const Resolved& r
 }
 
 struct Geom {  // the launch's chunk geometry (ScanArgs' normal or heavy set, chosen at the kernel start)
-    u32 chunk_tiles, mid_chunks, num_chunks;
+    u32 chunk_tiles, mid_chunks, num_chunks, down_g;
 };
 // After a chunk's commit (one lane): the launch's last commit decides the next launch's geometry
 // from the device's own counters (no host snapshot): heavy when at least a quarter of the chunks
@@ -1544,7 +1544,7 @@ __device__ __forceinline__ void chunk_bounds(const ScanArgs& a, const Geom& g, u
         return;
     }
     const u32 su = min(a.ramp_up_s, g.chunk_tiles), sd = min(a.ramp_down_s, g.chunk_tiles);
-    const u64 G = a.ramp_g, Gd = a.ramp_down_g;
+    const u64 G = a.ramp_g, Gd = g.down_g;
     const u64 rg = ramp_prefix(g, G, G, su), mid_end = (u64)a.num_tiles - ramp_prefix(g, Gd, Gd, sd);
     if (c < G) {
         tb = (u32)ramp_prefix(g, G, c, su);
@@ -1622,8 +1622,8 @@ __global__ __launch_bounds__(WG, FR_OCC) void chunk_kernel(ScanArgs args) {
     const bool hv = a.num_chunks_h != 0 &&
                     __builtin_amdgcn_readfirstlane(__hip_atomic_load(&a.st->heavy[a.par], __ATOMIC_RELAXED,
                                                                      __HIP_MEMORY_SCOPE_AGENT)) != 0;
-    const Geom g = hv ? Geom{a.chunk_tiles_h, a.mid_chunks_h, a.num_chunks_h}
-                      : Geom{a.chunk_tiles, a.mid_chunks, a.num_chunks};
+    const Geom g = hv ? Geom{a.chunk_tiles_h, a.mid_chunks_h, a.num_chunks_h, a.ramp_down_g_h}
+                      : Geom{a.chunk_tiles, a.mid_chunks, a.num_chunks, a.ramp_down_g};
     const bool limited = a.max_records > 0;
 #if defined(FR_STAMPS) && FR_STAMPS == 1
     const u64 k0_ = __builtin_amdgcn_s_memtime();
@@ -1893,6 +1893,7 @@ __device__ __forceinline__ bool last_block(u32* ctr) {
 
 constexpr int AGG_LNS = 4096;  // LDS slots of one sub-region's aggregation (64 KB: 2 workgroups per CU)
 constexpr int AGG_PROBE = 64;
+constexpr int CLAIM_WORDS = 2048;  // a reduce workgroup's claim bitmap: sub-regions of up to 64K slots (8 KB)
 struct alignas(16) AggSlot {
     u64 key;
     u32 mino, cnt;  // min range offset, records
@@ -1904,9 +1905,20 @@ struct alignas(16) AggSlot {
 // EXCL: no other thread touches these keys' slots while this kernel runs (log_reduce_kernel's buckets
 // partition the keys and nothing else updates the table): a found or claimed slot takes plain stores of
 // the updated count / first / tag instead of three memory-side atomics.
+// A reduce workgroup's claim zone: slots [lo, hi) of its sub-region's home range (base = the range's
+// first slot) that no other workgroup's probe can reach -- every insert gives up after GPROBE probes, so
+// a key homed before the range reaches at most GPROBE - 1 slots into it.  There an empty slot is claimed
+// through the workgroup's LDS bitmap and written with plain stores instead of a memory-side CAS (one
+// round trip and one atomic fewer per new code); elsewhere CAS as usual.  bits == nullptr: no zone.
+struct ClaimZone {
+    u32* bits;
+    u64 base, lo, hi;
+};
+
 template <int B, bool EXCL = false>
 __device__ __forceinline__ u32 insert_rows(const Table& T, DevState* st, const u64 (&key)[B], const u32 (&cnt)[B],
-                                           const u64 (&ord)[B], const u32 (&tag)[B], const bool (&valid)[B]) {
+                                           const u64 (&ord)[B], const u32 (&tag)[B], const bool (&valid)[B],
+                                           const ClaimZone& cz = ClaimZone{nullptr, 0, 0, 0}) {
     u32 h[B];
     bool pend[B];
 #pragma unroll
@@ -1949,7 +1961,20 @@ __device__ __forceinline__ u32 insert_rows(const Table& T, DevState* st, const u
                 }
                 pend[b] = false;
             } else if (k == 0) {
-                cas[b] = true;
+                if (EXCL && cz.bits && h[b] >= cz.lo && h[b] < cz.hi) {
+                    const u32 bit = (u32)(h[b] - cz.base), m = 1u << (bit & 31u);
+                    if (!(atomicOr(&cz.bits[bit >> 5], m) & m)) {  // ours: the whole slot, plain stores
+                        GSlot* sl = &T.slots[h[b]];
+                        *((uint4*)sl) = make_uint4((u32)key[b], (u32)(key[b] >> 32), cnt[b], 0u);
+                        *((uint4*)sl + 1) = make_uint4((u32)ord[b], (u32)(ord[b] >> 32), tag[b], w1[b].w);
+                        made += 1;
+                        pend[b] = false;
+                    } else {  // another lane of this workgroup took it meanwhile
+                        h[b] = (u32)((h[b] + 1ull) & T.mask);
+                    }
+                } else {
+                    cas[b] = true;
+                }
             } else {
                 h[b] = (u32)((h[b] + 1ull) & T.mask);
             }
@@ -1964,6 +1989,10 @@ __device__ __forceinline__ u32 insert_rows(const Table& T, DevState* st, const u
             if (old[b] == 0 || old[b] == key[b]) {
                 GSlot* sl = &T.slots[h[b]];
                 made += old[b] == 0 ? 1u : 0u;
+                if (cz.bits && old[b] == 0 && h[b] >= cz.lo && h[b] < cz.hi) {  // (a fold overflow's claim)
+                    const u32 bit = (u32)(h[b] - cz.base);
+                    atomicOr(&cz.bits[bit >> 5], 1u << (bit & 31u));
+                }
                 if (EXCL && old[b] == 0) {  // claimed an initialised slot (count 0, first ~0, tag 0): ours alone
                     *((u64*)&sl->count) = cnt[b];
                     *((uint4*)sl + 1) = make_uint4((u32)ord[b], (u32)(ord[b] >> 32), tag[b], w1[b].w);
@@ -2086,8 +2115,17 @@ __global__ __launch_bounds__(256) void log_reduce_kernel(Table t, DevState* st, 
                                                          u32 file_tag, u64 ord0) {
     if (st->log_n == 0) return;
     __shared__ AggSlot ls[AGG_LNS];
+    __shared__ u32 zone_bits[CLAIM_WORDS];
     u32 made = 0;
     for (int i = threadIdx.x; i < AGG_LNS; i += 256) ls[i] = AggSlot{0, 0xFFFFFFFFu, 0};
+    // this sub-region's home range: slots [blockIdx.x n, (blockIdx.x + 1) n) of the table (table_home's top
+    // bits are the region and sub-region bits); its claim zone skips the first GPROBE slots
+    const u64 nslots = t.mask + 1ull, rn = nslots >= (u64)LOG_NSUB ? nslots / LOG_NSUB : 0ull;
+    ClaimZone cz{nullptr, 0, 0, 0};
+    if (rn > 2ull * GPROBE && rn <= 32ull * CLAIM_WORDS && !(ABLATE & 2048u)) {
+        cz = ClaimZone{zone_bits, (u64)blockIdx.x * rn, (u64)blockIdx.x * rn + GPROBE, (u64)(blockIdx.x + 1) * rn};
+        for (u32 i = threadIdx.x; i < (u32)(rn / 32); i += 256) zone_bits[i] = 0;
+    }
     __syncthreads();
     const u32 n = min(st->log_scur[blockIdx.x], scap);
     const LogEntry* part = sub + (u64)blockIdx.x * scap;
@@ -2134,7 +2172,7 @@ __global__ __launch_bounds__(256) void log_reduce_kernel(Table t, DevState* st, 
                 const u64 ord1[1] = {ord0 + e.off};
                 const u32 tag1[1] = {file_tag};
                 const bool v1[1] = {true};
-                made += insert_rows<1>(t, st, key1, cnt1, ord1, tag1, v1);
+                made += insert_rows<1>(t, st, key1, cnt1, ord1, tag1, v1, cz);
             }
         }
     }
@@ -2157,7 +2195,7 @@ __global__ __launch_bounds__(256) void log_reduce_kernel(Table t, DevState* st, 
             ord[b] = ord0 + e.mino;
             tag[b] = file_tag;
         }
-        made += insert_rows<FB, true>(t, st, key, cnt, ord, tag, v);
+        made += insert_rows<FB, true>(t, st, key, cnt, ord, tag, v, cz);
     }
     add_created(st, made);
     // every workgroup has read log_n and its cursor (the split pass read the region cursors before

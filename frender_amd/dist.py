@@ -27,7 +27,20 @@ The tree merge (tree_merge) is kept as the alternative protocol for the bench (-
 """
 from __future__ import annotations
 
+import time
 from typing import Callable
+
+# Collective census: every exchange / reduce / gather of this module, counted and timed per kind (wall
+# clock around the blocking call).  `python -m frender_amd scan` prints it per rank to stderr when
+# FRENDER_DIST_CENSUS is set.
+CENSUS: dict = {}
+
+
+def _census(kind: str, t0: float, nbytes: int = 0):
+    c = CENSUS.setdefault(kind, {"calls": 0, "ms": 0.0, "bytes": 0})
+    c["calls"] += 1
+    c["ms"] += (time.perf_counter() - t0) * 1e3
+    c["bytes"] += int(nbytes)
 
 
 def tree_merge(dist, device, n_local: int,
@@ -127,6 +140,7 @@ def exchange(dist, wire, rows, dest):
     received, [m, k] on `wire`, ordered by source rank, then by their order at the source."""
     import torch
 
+    t0 = time.perf_counter()
     world = dist.get_world_size()
     rows = rows.to(wire)
     k = int(rows.shape[1])
@@ -139,16 +153,20 @@ def exchange(dist, wire, rows, dest):
     sc, rc = scount.tolist(), rcount.tolist()
     recv = torch.empty((sum(rc), k), dtype=torch.int64, device=wire)
     dist.all_to_all_single(recv.view(-1), send.view(-1), [k * c for c in rc], [k * c for c in sc])
+    _census("exchange", t0, 8 * k * sum(sc))
     return recv
 
 
 def _reduce(dist, wire, values, op):
     import torch
 
+    t0 = time.perf_counter()
     t = torch.as_tensor(list(values), dtype=torch.int64).to(wire)
     if t.numel():
         dist.all_reduce(t, op=op)
-    return t.cpu().numpy()
+    out = t.cpu().numpy()
+    _census("all_reduce", t0, 8 * t.numel())
+    return out
 
 
 def reduce_sum(dist, wire, values):
@@ -169,6 +187,7 @@ def gather_rows(dist, wire, rows):
     Returns the list of numpy arrays (rank order) on rank 0, None elsewhere."""
     import torch
 
+    t0 = time.perf_counter()
     rank, world = dist.get_rank(), dist.get_world_size()
     rows = rows.to(wire).contiguous()
     k = int(rows.shape[1])
@@ -178,6 +197,7 @@ def gather_rows(dist, wire, rows):
     if rank != 0:
         if n[rank]:
             dist.send(rows, dst=0)
+        _census("gather_rows", t0, 8 * k * n[rank])
         return None
     out = [rows.cpu().numpy()]
     for r in range(1, world):
@@ -185,6 +205,7 @@ def gather_rows(dist, wire, rows):
         if n[r]:
             dist.recv(buf, src=r)
         out.append(buf.cpu().numpy())
+    _census("gather_rows", t0, 8 * k * sum(n))
     return out
 
 

@@ -658,6 +658,12 @@ def frender_scan(args, ctx=None) -> dict:
         else:
             print("It appears that all files are already correctly demultiplexed.")
     report_analysis(table, results, demux_ok, out_csv_name)
+    if getattr(table, "group", None) is not None and os.environ.get("FRENDER_DIST_CENSUS"):
+        import json
+        import sys
+
+        from .dist import CENSUS
+        print("census " + json.dumps({"rank": table.group.get_rank(), "collectives": CENSUS}), file=sys.stderr)
     return {"table": table, "results": results, "out_csv": out_csv_name} if lead else None
 
 

@@ -37,7 +37,7 @@ def main():
         for n in gpus:
             wd = os.path.join(d, f"out{n}")
             os.mkdir(wd)
-            env = dict(os.environ, FRENDER_DIST_CENSUS="1",
+            env = dict(os.environ, FRENDER_DIST_CENSUS="1", PYTHONPATH=ROOT,
                        FRENDER_DIST_BACKEND=os.environ.get("FRENDER_DIST_BACKEND", "gloo"))
             t0 = time.perf_counter()
             p = subprocess.run([sys.executable, "-m", "frender_amd", "scan", "-n", "1", "-c", str(nfiles),

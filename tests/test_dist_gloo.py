@@ -121,3 +121,38 @@ def test_partition_exchange_gloo(world, seed):  # dist.exchange, as partition_me
             want[k] = (c0 + c, min(f0, f))
     assert union == want
     assert all(t == len(want) for _, _, t in got)
+
+
+def _worker_census(rank, world, port, out):
+    from frender_amd import dist as D
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rows = torch.arange(12, dtype=torch.int64).reshape(4, 3) + 100 * rank
+    D.exchange(dist, "cpu", rows, D.owner_of(rows[:, 0], world))
+    D.reduce_sum(dist, "cpu", [1, 2])
+    D.reduce_max(dist, "cpu", [rank])
+    D.gather_rows(dist, "cpu", rows)
+    out.put((rank, {k: (v["calls"], v["bytes"]) for k, v in D.CENSUS.items()}))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_collective_census_gloo():
+    """dist.CENSUS counts every collective of the module per kind with the bytes it moves (what
+    FRENDER_DIST_CENSUS prints after a multi-rank scan)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_census, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    for rank, c in got.items():
+        assert c["exchange"] == (1, 4 * 3 * 8)  # every row sent once
+        assert c["all_reduce"] == (2, 3 * 8)
+        assert c["gather_rows"][0] == 1
+    assert got[0]["gather_rows"][1] == 2 * 4 * 3 * 8 and got[1]["gather_rows"][1] == 4 * 3 * 8

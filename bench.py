@@ -44,6 +44,7 @@ def parse():
     ap.add_argument("--index-len", type=int, default=8)
     ap.add_argument("--read-len", type=int, default=8, help="R: bases per read (8 -> 74 B/record)")
     ap.add_argument("--nsubs", type=int, default=1)
+    ap.add_argument("--launch-gib", type=int, default=16, help="largest tally launch of a device feed (GiB)")
     ap.add_argument("--rc", action="store_true")
     ap.add_argument("--combinatorial", action="store_true", help="12x8 combinatorial sheet (config 4 shape)")
     ap.add_argument("--cpu-reads", type=int, default=24_000_000, help="bounded sample for the CPU baseline (~10-20 s on 8 cores)")
@@ -426,7 +427,9 @@ def main():
     reclen = synth.record_length(args.index_len, args.index_len, args.read_len)
     n = args.reads
     nbytes = n * reclen
-    ctx = _lib.Context(device=local, chunk_bytes=(4 << 30) - (1 << 20), table_slots=1 << 22)
+    # launches of up to 16 GiB: the first feed (no history) is cut into ranges <= 4 GiB that may log;
+    # once a feed's commits did not log, a feed is one launch (fr_feed_device)
+    ctx = _lib.Context(device=local, chunk_bytes=(args.launch_gib << 30) - (1 << 20), table_slots=1 << 22)
     buf = ctx.device_alloc(nbytes + 64)
     ctx.synth_device(buf, rank * n, n, args.read_len, 1, sheet.idx1, sheet.idx2)
     names, nid = _sheet_names(sheet.ids)

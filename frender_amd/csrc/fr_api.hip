@@ -90,10 +90,12 @@ struct fr_ctx {
     Table tab{};
     u64 nslots = 0;
 
-    // launch sizes: chunk_bytes bytes per tally launch of device feeds (<= RANGE_MAX); host feeds
+    // launch sizes: chunk_bytes bytes per tally launch of device feeds (<= RANGE_MAX; <= RANGE_LOG_MAX unless
+    // the previous device feed would not have logged: feed_logged); host feeds
     // go through a pinned ring of ring_bytes slots (<= HOST_CHUNK_MAX)
     u64 chunk_bytes = 0;
     u64 ring_bytes = 0;
+    bool feed_logged = true;  // the last device feed logged (or would have): its ranges stay <= RANGE_LOG_MAX
     u32 chunk_tiles = 320;  // wave-tiles (4 KiB) per full chunk of a ramped launch (FR_CHUNK_TILES; round 2's
                             // 80 workgroup tiles of 16 KiB: 64-96 measured within 2 %, 80 best)
     // Ramped launches after one in which at least a quarter of the chunks since the reset logged their
@@ -588,7 +590,7 @@ static int launch_range(fr_ctx* ctx, const u8* dptr, u64 len, u64 avail, int own
     }
     a.cold_cap = ctx->cold_cap;
     a.cold = ctx->cold;
-    a.log = exo_only ? nullptr : ctx->log;
+    a.log = (exo_only || len > RANGE_LOG_MAX) ? nullptr : ctx->log;  // launch-log offsets are u32
     a.log_cap = ctx->log_cap;
     a.log_rcap = ctx->log_rcap;
     a.log_min = ctx->log_min;
@@ -652,7 +654,8 @@ fr_ctx* fr_create(int device, uint64_t chunk_bytes, uint64_t table_slots) {
     if (!fl || atoi(fl) != 0) {
         // entries: 1 per 256 B of a launch (SYN-v1 config 3 logs ~1 per 700 B), in LOG_NR equal regions;
         // a run past its region's end inserts directly
-        const u64 want = std::min<u64>(std::max<u64>(ctx->chunk_bytes / 256, 1ull << 16), 1ull << 26);
+        const u64 want = std::min<u64>(std::max<u64>(std::min<u64>(ctx->chunk_bytes, RANGE_LOG_MAX) / 256, 1ull << 16),
+                                       1ull << 26);  // logged ranges are <= RANGE_LOG_MAX
         ctx->log_rcap = (u32)(want / LOG_NR);
         ctx->log_cap = (u64)ctx->log_rcap * LOG_NR;
         ctx->log_scap = (u32)std::max<u64>(2ull * ctx->log_rcap / LOG_SUBS, 64);  // 2x the mean share
@@ -1044,8 +1047,12 @@ int fr_feed_device(fr_ctx* ctx, const uint8_t* dev_data, uint64_t len) {
         CK(dalloc(&snap, snap_slots));
         CK(hipMemcpyAsync(snap, ctx->tab.slots, snap_slots * sizeof(GSlot), hipMemcpyDeviceToDevice, ctx->stream));
     }
-    // equal ranges of at most chunk_bytes
-    const u64 nr = (len + ctx->chunk_bytes - 1) / ctx->chunk_bytes;
+    // equal ranges of at most chunk_bytes.  A range over RANGE_LOG_MAX runs without the launch log (its
+    // offsets are u32), so it is taken only for speculative feeds after a feed whose commits did not log
+    // (DevState::log_commits counts the would-be logged commits of an unlogged launch too): one launch
+    // instead of two for the bench's 7.4 GB (the per-launch ramps and tail)
+    const u64 lim = (spec && !ctx->feed_logged) ? ctx->chunk_bytes : std::min<u64>(ctx->chunk_bytes, RANGE_LOG_MAX);
+    const u64 nr = (len + lim - 1) / lim;
     const u64 step = nr ? (len + nr - 1) / nr : 0;
     for (int attempt = 0; attempt < 2; ++attempt) {
         ctx->spec_commit = spec && attempt == 0 ? 1u : 0u;
@@ -1086,6 +1093,7 @@ int fr_feed_device(fr_ctx* ctx, const uint8_t* dev_data, uint64_t len) {
         CK(hipFree(snap));
     }
     if (rc) return rc;
+    ctx->feed_logged = ctx->h_st->log_commits != saved.log_commits;  // read_state above: exact
     // exotic records overflowed the list: grow it to the counted totals and run the feed's launches
     // again capturing exotic records only (the table is already complete), then drain
     rc = read_state(ctx);

@@ -38,8 +38,11 @@ constexpr int MAXSYM = 21;           // fast key: <= 21 symbols of 3 bits
 constexpr u64 WIDE_BIT = 1ull << 63;
 constexpr int WIDE_MAXN = 24;
 constexpr int WIDE_NOPLUS = 31;
-constexpr u64 RANGE_MAX = (4ull << 30) - (1ull << 20);  // bytes per tally launch (device feeds): range
-                                     // offsets, LDS first-offsets and per-range line counts stay u32
+constexpr u64 RANGE_MAX = (16ull << 30) - (1ull << 20);  // bytes per tally launch (device feeds): positions
+                                     // are u32 offsets inside a chunk (ScanShared::cbase), so a range is bounded
+                                     // by the look-back arrays (tiles_cap) only
+constexpr u64 RANGE_LOG_MAX = (4ull << 30) - (1ull << 20);  // a range whose commits may log (launch-log offsets
+                                     // are u32 from the launch start), or whose exact line prefix matters (-s)
 constexpr u64 HOST_CHUNK_MAX = 1ull << 30;  // bytes per host-fed launch (pinned ring slot)
 constexpr u32 SPIN_MAX = 1u << 24;   // look-back spin bound (then FR_ERR_DEVICE)
 constexpr int ORD_SHIFT = 44;        // ordinal = file_tag << 44 | file byte offset
@@ -121,7 +124,8 @@ struct DevState {
     u32 spin_max;        // diagnostics: longest look-back wait (polls)
     u64 spin_total;      // diagnostics: total look-back polls that found a window not ready
     u64 log_n;           // entries appended to the launch log (may exceed its capacity: the rest went to HBM)
-    u64 log_commits;     // commits that went to the launch log since the last reset (never emptied by the aggregation)
+    u64 log_commits;     // commits that went to the launch log since the last reset (never emptied by the aggregation);
+                         // a launch without a log counts the commits that would have logged
     u64 stamp[8];        // diagnostics (FR_STAMPS builds only): per-phase shader cycles, summed over workgroups
     // Heavy chunk geometry, decided on the device: the last workgroup to commit in a
     // launch sets heavy[par ^ 1] = (at least a quarter of the chunks since the reset logged their

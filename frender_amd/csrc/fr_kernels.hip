@@ -240,6 +240,8 @@ struct ScanShared {
     int wphase[NW];          // pass 0: the phase each wave parsed with (mod 4), -1 count only
     u32 rq_tail[NW];         // rare-event ring: events pushed by each wave (monotonic)
     u64 tile_excl;
+    u64 cbase;               // the chunk's first byte in the range: positions inside a chunk are u32 offsets
+                             // from it (chunks are <= 512 tiles), so a range may exceed 4 GiB
     u32 chunk;
     u32 nkeys;               // occupied LDS slots
     u32 created;             // HBM slots this workgroup created (added to n_keys once, at exit)
@@ -281,7 +283,7 @@ __device__ __forceinline__ void lds_barrier() {
 }
 
 __device__ FR_COLD void direct_insert(ScanShared& sh, const ScanArgs& a, u64 key, u32 off) {
-    if (global_insert(a.tabv, a.st, key, 1, make_ord(a, off), a.file_tag)) atomicAdd(&sh.created, 1u);
+    if (global_insert(a.tabv, a.st, key, 1, make_ord(a, sh.cbase + off), a.file_tag)) atomicAdd(&sh.created, 1u);
 }
 
 __device__ __forceinline__ void rare_push(ScanShared& sh, const ScanArgs& a, u32 p, u32 kind, u32 x, u32 y);
@@ -323,7 +325,7 @@ __device__ __forceinline__ void lds_insert(ScanShared& sh, const ScanArgs& a, u6
     if (i < a.cold_cap) {
         u64* c = a.cold + 2ull * ((u64)blockIdx.x * a.cold_cap + i);
         c[0] = key;
-        c[1] = make_ord(a, off);
+        c[1] = make_ord(a, sh.cbase + off);
         return;
     }
     if (sh.spec) {  // cannot insert while speculating: this chunk will be redone exactly
@@ -337,7 +339,7 @@ __device__ __forceinline__ void lds_insert(ScanShared& sh, const ScanArgs& a, u6
 
 // Rare events (exotic codes, headers without ' ', headers whose code leaves the bitmap window,
 // direct HBM inserts, UTF-8 checks) go to the wave's ring in HBM and are handled by drain_rare at
-// the wave's next tile, so their code adds no registers to the tile loop.  Entry: {range offset,
+// the wave's next tile, so their code adds no registers to the tile loop.  Entry: {chunk offset,
 // kind, x, y}.  No fence here (a release would wait for the next tile's loads): drain_rare fences.
 __device__ __forceinline__ void rare_push(ScanShared& sh, const ScanArgs& a, u32 p, u32 kind, u32 x, u32 y) {
     const u32 wid = wave_id();
@@ -410,13 +412,13 @@ __device__ __forceinline__ u64 lookback(const ScanArgs& a, u32 t, u32 agg, int l
 
 // validate UTF-8 for the range bytes [s0, s0+n) (only called when a byte >= 0x80 is present);
 // bytes are read from HBM (the range, and before it when readable), -1 past them.
-__device__ FR_COLD bool utf8_segment_ok(const ScanArgs& a, int s0, int n) {
+__device__ FR_COLD bool utf8_segment_ok(const ScanArgs& a, u64 s0, u32 n) {
     auto byte_at = [&](i64 q) -> int {
         if (q < 0 && !a.pre_valid) return -1;
         if (q >= (i64)a.avail) return -1;
         return (int)a.buf[q];
     };
-    for (i64 q = s0; q < (i64)s0 + n; ++q) {
+    for (i64 q = (i64)s0; q < (i64)s0 + (i64)n; ++q) {
         const int b = byte_at(q);
         if (b < 0x80) continue;
         if (b >= 0x80 && b <= 0xBF) {  // continuation: must be claimed by a lead
@@ -490,7 +492,7 @@ __device__ bool wide_encode(const ScanArgs& a, u64 q, u64 n, u64& key) {
     return true;
 }
 
-// a code the fast encoder did not take (range offsets: header p, code [start, start + n)): exact
+// a code the fast encoder did not take (header p: chunk offset; code [start, start + n): range offsets): exact
 // fast form (defensive), wide key, or an exotic record captured verbatim (speculating: its position
 // is buffered and the bytes stay resident in HBM)
 __device__ void exotic_record(const ScanArgs& a, u32 p, u64 start, u64 n, ScanShared& sh) {
@@ -511,7 +513,7 @@ __device__ void exotic_record(const ScanArgs& a, u32 p, u64 start, u64 n, ScanSh
         const u32 k = atomicAdd(&sh.nexo, 1u);
         if (k < (u32)EXO_BUF) {
             sh.exo_p[k] = p;
-            sh.exo_start[k] = (u32)start;
+            sh.exo_start[k] = (u32)(start - sh.cbase);
             sh.exo_len[k] = (u32)n;
         } else {
             atomicOr(&sh.spec_bad, 1u);
@@ -521,7 +523,7 @@ __device__ void exotic_record(const ScanArgs& a, u32 p, u64 start, u64 n, ScanSh
     const u64 i = atomicAdd((unsigned long long*)&a.st->n_exotic, 1ull);
     const u64 po = atomicAdd((unsigned long long*)&a.st->exo_pool_used, (unsigned long long)n);
     if (i < a.tabv.exo_cap && po + n <= a.tabv.exo_pool_cap) {
-        a.tabv.exo_ord[i] = make_ord(a, p);
+        a.tabv.exo_ord[i] = make_ord(a, sh.cbase + p);
         a.tabv.exo_off[i] = po;
         a.tabv.exo_len[i] = (u32)n;
         for (u64 k = 0; k < n; ++k) a.tabv.exo_pool[po + k] = a.buf[start + k];
@@ -532,16 +534,16 @@ __device__ void exotic_record(const ScanArgs& a, u32 p, u64 start, u64 n, ScanSh
 
 __device__ __forceinline__ void nospace(const ScanArgs& a, u32 p, ScanShared& sh) {  // IndexError (:169)
     if (sh.spec) atomicMin(&sh.err_off, p);
-    else atomicMin((unsigned long long*)&a.st->err_nospace, (unsigned long long)(a.file_offset + p));
+    else atomicMin((unsigned long long*)&a.st->err_nospace, (unsigned long long)(a.file_offset + sh.cbase + p));
 }
 
 // slow path (rare): a header whose code does not end inside its bitmap windows, parsed byte by
 // byte from HBM.  R2 (frender.py:169): the token after the first ' ' up to the next ' ' or line
-// end, then its suffix after the last ':'.  p = the header's range offset.
+// end, then its suffix after the last ':'.  p = the header's chunk offset.
 __device__ FR_COLD void process_header_global(ScanShared& sh, const ScanArgs& a, u32 p) {
     const u64 eof = a.avail;
     auto rd = [&](u64 q) -> u32 { return (u32)a.buf[q]; };
-    u64 q = p;
+    u64 q = sh.cbase + p;
     for (;;) {
         if (q >= eof) return nospace(a, p, sh);
         const u32 c = rd(q);
@@ -770,12 +772,13 @@ __device__ __attribute__((noinline)) void drain_rare(ScanShared& sh, const ScanA
         const uint4 e = q[i & (RARE_WAVE - 1u)];
         if (e.y == 3u) {
             direct_insert(sh, a, ((u64)e.w << 32) | e.z, e.x);
-        } else if (e.y == 4u) {  // UTF-8: the segment's own bytes [e.x, e.x + e.z)
+        } else if (e.y == 4u) {  // UTF-8: the segment's own bytes [e.x, e.x + e.z) of the chunk
+            const u64 x = sh.cbase + e.x;
             bool hi = false;
-            for (u32 k = 0; k < e.z; ++k) hi |= a.buf[e.x + k] >= 0x80;
+            for (u32 k = 0; k < e.z; ++k) hi |= a.buf[x + k] >= 0x80;
             if (hi) {
                 atomicOr(&sh.flags, 1u);
-                if (!utf8_segment_ok(a, (int)e.x, (int)e.z)) atomicOr(&sh.flags, 2u);
+                if (!utf8_segment_ok(a, x, e.z)) atomicOr(&sh.flags, 2u);
             }
         } else {
             slow_header(sh, a, e.x, (int)e.y, e.z, e.w);
@@ -998,6 +1001,7 @@ __device__ __attribute__((noinline)) void commit_buffers(ScanShared& sh, const S
         if (tid == 0) atomicAdd((unsigned long long*)&a.st->stamp[6], 1ull);
     }
     const bool flush = !(ABLATE & 8u);  // ablation 8: no HBM flush of the LDS table / cold list
+    const u64 cb = sh.cbase;  // LDS offsets are chunk offsets
     const u32 nc = flush ? min(sh.ncold, a.cold_cap) : 0u;
     const u32 nl = flush ? sh.nkeys : 0u;  // claimed LDS slots = the live ones
     // heavy commits (at least log_min pairs: many distinct codes per chunk) go to the launch log,
@@ -1053,6 +1057,10 @@ __device__ __attribute__((noinline)) void commit_buffers(ScanShared& sh, const S
             atomicAdd((unsigned long long*)&a.st->log_commits, 1ull);
         }
         logged = sh.log_on != 0;  // else (nothing but hot codes) every pair inserts directly
+    } else if (!a.log && !a.exo_only && tid == 0 && nl + nc && nl + nc >= a.log_min) {
+        // a launch without a log (a range over RANGE_LOG_MAX): count the commit that would have logged, so
+        // the host goes back to logged ranges for the next feed (fr_feed_device) and note_commit sees it
+        atomicAdd((unsigned long long*)&a.st->log_commits, 1ull);
     }
     if (logged) {
         constexpr int CL = NS / WG;
@@ -1079,7 +1087,7 @@ __device__ __attribute__((noinline)) void commit_buffers(ScanShared& sh, const S
             const LSlot e = sh.ls[tid + b * WG];
             hv[b] = e.key && e.cnt >= a.log_hot;
             hk[b] = e.key;
-            if (e.key && !hv[b]) put(e.key, e.mino, e.cnt);
+            if (e.key && !hv[b]) put(e.key, (u32)(cb + e.mino), e.cnt);  // launch offsets: a logged range is < 4 GiB
         }
         for (u32 i0 = tid; i0 < nc; i0 += CB * WG) {
             u64 k[CB], o[CB];
@@ -1099,7 +1107,7 @@ __device__ __attribute__((noinline)) void commit_buffers(ScanShared& sh, const S
         for (int b = 0; b < CL; ++b) {
             if (!hv[b]) continue;
             const LSlot e = sh.ls[tid + b * WG];
-            apply_entry(a, rh[b], e.key, e.cnt, make_ord(a, e.mino));
+            apply_entry(a, rh[b], e.key, e.cnt, make_ord(a, cb + e.mino));
         }
     } else if (flush) {
         constexpr int CL = NS / WG;  // LDS slots per lane; also cold entries per lane per batch
@@ -1159,7 +1167,7 @@ __device__ __attribute__((noinline)) void commit_buffers(ScanShared& sh, const S
 #pragma unroll
         for (int b = 0; b < CL; ++b) {
             const LSlot e = sh.ls[tid + b * WG];
-            if (e.key) apply_entry(a, park[tid + b * WG], e.key, e.cnt, make_ord(a, e.mino));
+            if (e.key) apply_entry(a, park[tid + b * WG], e.key, e.cnt, make_ord(a, cb + e.mino));
         }
 #pragma unroll
         for (int b = 0; b < CL; ++b)
@@ -1187,16 +1195,16 @@ __device__ __attribute__((noinline)) void commit_buffers(ScanShared& sh, const S
         const u64 i = atomicAdd((unsigned long long*)&a.st->n_exotic, 1ull);
         const u64 po = atomicAdd((unsigned long long*)&a.st->exo_pool_used, (unsigned long long)n);
         if (i < a.tabv.exo_cap && po + n <= a.tabv.exo_pool_cap) {
-            a.tabv.exo_ord[i] = make_ord(a, sh.exo_p[k]);
+            a.tabv.exo_ord[i] = make_ord(a, cb + sh.exo_p[k]);
             a.tabv.exo_off[i] = po;
             a.tabv.exo_len[i] = (u32)n;
-            for (u64 q = 0; q < n; ++q) a.tabv.exo_pool[po + q] = a.buf[sh.exo_start[k] + q];
+            for (u64 q = 0; q < n; ++q) a.tabv.exo_pool[po + q] = a.buf[cb + sh.exo_start[k] + q];
         } else {
             atomicOr(&a.st->cap_flags, 4u);
         }
     }
     if (tid == 0 && sh.err_off != 0xFFFFFFFFu)
-        atomicMin((unsigned long long*)&a.st->err_nospace, (unsigned long long)(a.file_offset + sh.err_off));
+        atomicMin((unsigned long long*)&a.st->err_nospace, (unsigned long long)(a.file_offset + cb + sh.err_off));
     // (in here, not in the chunk loop: lane-divergent code at the loop's end made the structurizer move
     // it out of the loop, past the ticket barrier, for one lane)
     if (tid == 0) note_commit(a, g, hv);
@@ -1271,11 +1279,11 @@ __device__ __forceinline__ bool encode_pack(const u32 (&w)[8], u32 start, u32 n,
     return bad == 0;
 }
 
-// the rare header outcomes (range offsets): word-scan fallback, no ' ' (IndexError), or an exotic code
+// the rare header outcomes (chunk offsets): word-scan fallback, no ' ' (IndexError), or an exotic code
 __device__ FR_COLD void slow_header(ScanShared& sh, const ScanArgs& a, u32 p, int r, u32 start, u32 n) {
     if (r == 2) process_header_global(sh, a, p);
     else if (r == 1) nospace(a, p, sh);
-    else exotic_record(a, p, start, n, sh);
+    else exotic_record(a, p, sh.cbase + start, n, sh);
 }
 
 // ---- header parse: two 64-bit bitmap windows, wave-uniform code length encode ---------------
@@ -1384,9 +1392,10 @@ __device__ __forceinline__ void parse_header(ScanShared& sh, const ScanArgs& a, 
 // where they lie.  L0 = lines before the wave-tile (absolute with -s, else mod 4 suffices).  The
 // first header needs the skip-th set bit of the terminator mask; a second one in the same segment
 // (records shorter than 64 B) takes the loop at the end.
-__device__ __forceinline__ void parse_own_headers(ScanShared& sh, const ScanArgs& a, u32 t, const SegClass& sc,
-                                                  u64 L0, int lane, u32 wid) {
+__device__ __forceinline__ void parse_own_headers(ScanShared& sh, const ScanArgs& a, u32 t, u32 ct,
+                                                  const SegClass& sc, u64 L0, int lane, u32 wid) {
     const u64 tile0 = (u64)t * TSTEP;
+    const u32 tile0c = (t - ct) * TSTEP;  // the tile's chunk offset (ct: the chunk's first tile)
     const u32 bl = (u32)min((u64)TILE, a.avail - tile0);
     const u64 rem64 = a.len - tile0;  // line starts p < pend are this launch's (uniform)
     const u32 pend = rem64 >= 0xFFFFFFFFull ? 0xFFFFFFFFu : (u32)rem64 + ((a.own_end && a.len < a.avail) ? 1u : 0u);
@@ -1411,7 +1420,7 @@ __device__ __forceinline__ void parse_own_headers(ScanShared& sh, const ScanArgs
     // m's lowest set bit: the first header terminator.  own0's header at position 0 comes first.
     const u32 p = own0 ? 0u : s0 + ctz64x(m) + 1u;
     const bool ok = own0 || (m != 0 && p < pend && (!limited || (i64)rec < a.max_records));
-    if (ok) parse_header(sh, a, wid, (u32)tile0, p, bl);
+    if (ok) parse_header(sh, a, wid, tile0c, p, bl);
     // another header in this segment (records shorter than 64 B; never at R=8's 74 B): uniform check
     bool more = ok && (own0 ? m != 0 : __popcll(m) > 4);
     if (!__ballot(more)) return;
@@ -1426,7 +1435,7 @@ __device__ __forceinline__ void parse_own_headers(ScanShared& sh, const ScanArgs
         if (more) {
             const u32 pn = s0 + ctz64x(m) + 1u;
             more = pn < pend && (!limited || (i64)rec < a.max_records);
-            if (more) parse_header(sh, a, wid, (u32)tile0, pn, bl);
+            if (more) parse_header(sh, a, wid, tile0c, pn, bl);
             ++rec;
             m &= m - 1ull;
             m &= m - 1ull;
@@ -1443,8 +1452,8 @@ __device__ __forceinline__ void parse_own_headers(ScanShared& sh, const ScanArgs
 // (in registers since the previous step) go to the wave's LDS copy first, so the registers take the
 // next tile's loads at once and those stay in flight through this tile's classify AND its parse;
 // the classify reads the lane's segment back from LDS.
-__device__ __forceinline__ u64 walk_wave(ScanShared& sh, const ScanArgs& a0, u32 tb, u32 te, u64 L0, bool parse,
-                                         int lane, u32 wid) {
+__device__ __forceinline__ u64 walk_wave(ScanShared& sh, const ScanArgs& a0, u32 ct, u32 tb, u32 te, u64 L0,
+                                         bool parse, int lane, u32 wid) {
     const ScanArgs& a = a0;
     u64 lines = 0;
     u32 done = *(const volatile lds_u32*)&sh.rq_tail[wid];
@@ -1465,7 +1474,7 @@ __device__ __forceinline__ u64 walk_wave(ScanShared& sh, const ScanArgs& a0, u32
             const u32x4 v = *(const volatile lds_u32x4*)&mine[k];
             return make_uint4(v.x, v.y, v.z, v.w);
         }, lane);
-        if (sc.hi) rare_push(sh, a, (u32)((u64)t * TSTEP) + lane * SEG, 4u,
+        if (sc.hi) rare_push(sh, a, (t - ct) * TSTEP + lane * SEG, 4u,
                              min((u32)min((u64)TSTEP, a.len - (u64)t * TSTEP) - lane * SEG, (u32)SEG), 0u);
         const u32 tail = *(const volatile lds_u32*)&sh.rq_tail[wid];
         if (tail != done) {  // uniform: the previous tile's rare events (and this tile's UTF-8 checks)
@@ -1479,7 +1488,7 @@ __device__ __forceinline__ u64 walk_wave(ScanShared& sh, const ScanArgs& a0, u32
         // (a speculation buffer that overflowed mid-walk, sh.spec_bad, is not checked per tile: the chunk is
         // redone exactly and everything its walk buffered is discarded, so parsing on is harmless; the check
         // was an LDS round trip per tile)
-        if (parse && !(ABLATE & 1u)) parse_own_headers(sh, a, t, sc, L0 + lines, lane, wid);
+        if (parse && !(ABLATE & 1u)) parse_own_headers(sh, a, t, ct, sc, L0 + lines, lane, wid);
         lines += sc.wtot;
     }
     lds_fence();
@@ -1631,14 +1640,16 @@ __global__ __launch_bounds__(WG, FR_OCC) void chunk_kernel(ScanArgs args) {
     FR_STAMP_DECL
     for (bool first = true;; first = false) {
         if (tid == 0) {
-#ifndef FR_TICKET_ALL
             // the first chunk is the workgroup's own index, the rest go by ticket after the grid's first
             // chunks: 1024 workgroups no longer queue on one counter at the launch start (serialised
             // same-address atomics: ~12 us before the last workgroup had its first chunk)
-            sh.chunk = first ? blockIdx.x : gridDim.x + atomicAdd(&a.st->ticket, 1u);
-#else
-            sh.chunk = atomicAdd(&a.st->ticket, 1u);
-#endif
+            const u32 cn = first ? blockIdx.x : gridDim.x + atomicAdd(&a.st->ticket, 1u);
+            sh.chunk = cn;
+            if (cn < g.num_chunks) {  // the chunk's base for its offsets (published by the barrier)
+                u32 tb0, te0;
+                chunk_bounds(a, g, cn, tb0, te0);
+                sh.cbase = (u64)tb0 * TSTEP;
+            }
             sh.spec = 1u;  // pass 0 runs on guessed phases: side effects are buffered
         }
         __syncthreads();
@@ -1681,7 +1692,7 @@ __global__ __launch_bounds__(WG, FR_OCC) void chunk_kernel(ScanArgs args) {
         u64 base = base_lines;
         for (int pass = 0;; ++pass) {
             FR_TRACE("w%d pass %d run %d [%u,%u) parse %d\n", (int)wid, pass, (int)run, wb, we, (int)parse);
-            const u64 n = run ? walk_wave(sh, a, wb, we, L0, parse, lane, wid) : 0ull;
+            const u64 n = run ? walk_wave(sh, a, tb, wb, we, L0, parse, lane, wid) : 0ull;
             FR_TRACE("w%d walked %llu\n", (int)wid, (unsigned long long)n);
             FR_STAMP(pass == 0 ? 1 : 4);
             if (pass == 0) {

@@ -96,6 +96,7 @@ struct fr_ctx {
     u64 chunk_bytes = 0;
     u64 ring_bytes = 0;
     bool feed_logged = true;  // the last device feed logged (or would have): its ranges stay <= RANGE_LOG_MAX
+    u64 feed_keys = ~0ull;    // codes the last device feed created (a range over RANGE_LOG_MAX also needs table room)
     u32 chunk_tiles = 320;  // wave-tiles (4 KiB) per full chunk of a ramped launch (FR_CHUNK_TILES; round 2's
                             // 80 workgroup tiles of 16 KiB: 64-96 measured within 2 %, 80 best)
     // Ramped launches after one in which at least a quarter of the chunks since the reset logged their
@@ -1051,7 +1052,11 @@ int fr_feed_device(fr_ctx* ctx, const uint8_t* dev_data, uint64_t len) {
     // offsets are u32), so it is taken only for speculative feeds after a feed whose commits did not log
     // (DevState::log_commits counts the would-be logged commits of an unlogged launch too): one launch
     // instead of two for the bench's 7.4 GB (the per-launch ramps and tail)
-    const u64 lim = (spec && !ctx->feed_logged) ? ctx->chunk_bytes : std::min<u64>(ctx->chunk_bytes, RANGE_LOG_MAX);
+    // (and only when the table holds the last feed's new codes again at load <= 1/2: the table grows
+    // between launches, never inside one)
+    const bool big = spec && !ctx->feed_logged && ctx->feed_keys != ~0ull &&
+                     (saved.n_keys + ctx->feed_keys) * 2 <= ctx->nslots;
+    const u64 lim = big ? ctx->chunk_bytes : std::min<u64>(ctx->chunk_bytes, RANGE_LOG_MAX);
     const u64 nr = (len + lim - 1) / lim;
     const u64 step = nr ? (len + nr - 1) / nr : 0;
     for (int attempt = 0; attempt < 2; ++attempt) {
@@ -1094,6 +1099,7 @@ int fr_feed_device(fr_ctx* ctx, const uint8_t* dev_data, uint64_t len) {
     }
     if (rc) return rc;
     ctx->feed_logged = ctx->h_st->log_commits != saved.log_commits;  // read_state above: exact
+    ctx->feed_keys = ctx->h_st->n_keys - saved.n_keys;
     // exotic records overflowed the list: grow it to the counted totals and run the feed's launches
     // again capturing exotic records only (the table is already complete), then drain
     rc = read_state(ctx);

@@ -67,6 +67,9 @@ def parse():
     ap.add_argument("--cfg5-pairs", type=int, default=2_000_000)
     ap.add_argument("--cfg5-files", type=int, default=4, help="file pairs")
     ap.add_argument("--cfg5-cpu-pairs", type=int, default=100_000)
+    ap.add_argument("--tuning", default="",
+                    help="A/B runs only: fr_tuning fields for the bench's context, e.g. 'log_min=0,chunk_tiles=400' "
+                         "(results never change; a tuned run reports them in config.tuning)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r04.json"),
                     help="per-launch HBM bytes of the tally kernel from rocprofv3 PMC (scripts/make_traffic.py); "
                          "used only when taken on this source tree and this launch shape, else traffic is null")
@@ -429,7 +432,9 @@ def main():
     nbytes = n * reclen
     # launches of up to 16 GiB: the first feed (no history) is cut into ranges <= 4 GiB that may log;
     # once a feed's commits did not log, a feed is one launch (fr_feed_device)
-    ctx = _lib.Context(device=local, chunk_bytes=(args.launch_gib << 30) - (1 << 20), table_slots=1 << 22)
+    tuning = {k: int(v) for k, v in (kv.split("=", 1) for kv in args.tuning.split(",") if kv)}
+    ctx = _lib.Context(device=local, chunk_bytes=(args.launch_gib << 30) - (1 << 20), table_slots=1 << 22,
+                       tuning=tuning or None)
     buf = ctx.device_alloc(nbytes + 64)
     ctx.synth_device(buf, rank * n, n, args.read_len, 1, sheet.idx1, sheet.idx2)
     names, nid = _sheet_names(sheet.ids)
@@ -545,7 +550,7 @@ def main():
                                    f"decoded FASTQ resident in HBM",
                        "reads_per_gpu": n, "bytes_per_record": reclen, "samples": args.samples,
                        "nsubs": args.nsubs, "rc": bool(args.rc), "unique_codes": int(U),
-                       "table_checksum": f"{csum:016x}", "reference_pin": pinned,
+                       "table_checksum": f"{csum:016x}", "reference_pin": pinned, "tuning": tuning or None,
                        "parallelism": f"dp{world} (record shards) + {'RCCL' if args.dist_backend == 'nccl' else 'gloo'} "
                                       + ("all-to-all hash-partitioned merge" if args.merge == "a2a" else "tree merge") if world > 1 else "1 GPU"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

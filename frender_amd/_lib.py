@@ -64,6 +64,16 @@ class Timing(C.Structure):
                 ("log_ms", C.c_double)]
 
 
+class Tuning(C.Structure):
+    """fr_tuning (include/frender_amd.h): the tally's geometry and thresholds.  Results never depend on
+    them; tests and A/B runs pass them on purpose (Context(tuning={...})), nothing reads the environment."""
+    _fields_ = [("size", C.c_uint32), ("grid", C.c_int32), ("flush_at", C.c_uint32), ("cold_cap", C.c_uint32),
+                ("log", C.c_int32), ("log_min", C.c_uint32), ("log_hot", C.c_uint32), ("chunk_tiles", C.c_uint32),
+                ("chunk_tiles_heavy", C.c_uint32), ("ramp", C.c_int32), ("ramp_up_s", C.c_uint32),
+                ("ramp_down_s", C.c_uint32), ("ramp_down_pct", C.c_uint32), ("ramp_down_pct_h", C.c_uint32),
+                ("spec_commit", C.c_int32), ("nbr", C.c_int32), ("ovf_cap", C.c_uint64)]
+
+
 if not os.path.exists(LIB_PATH):
     raise ImportError(f"frender_amd: HIP library {LIB_PATH} is not built (run __graft_entry__.build())")
 lib = C.CDLL(LIB_PATH)
@@ -72,6 +82,8 @@ P = C.c_void_p
 u64p = C.POINTER(C.c_uint64)
 _SIGS = {
     "fr_create": (P, [C.c_int, C.c_uint64, C.c_uint64]),
+    "fr_tuning_defaults": (None, [C.POINTER(Tuning)]),
+    "fr_create_tuned": (P, [C.c_int, C.c_uint64, C.c_uint64, C.POINTER(Tuning)]),
     "fr_destroy": (None, [P]),
     "fr_last_error": (C.c_char_p, [P]),
     "fr_get_timing": (C.c_int, [P, C.POINTER(Timing)]),
@@ -119,6 +131,7 @@ _SIGS = {
     "fr_gz_part_error": (C.c_char_p, [P]),
     "fr_gz_part_close": (None, [P]),
     "fr_gz_close": (None, [P]),
+    "fr_gz_trim": (None, []),
     # demux (row f-1)
     "fr_dmx_create": (P, [C.c_int]),
     "fr_dmx_destroy": (None, [P]),
@@ -441,12 +454,41 @@ class Demux:
         return out
 
 
+def _torch_stream_done(device: int):
+    """Wait for the work queued on torch's current stream of `device` (no-op without torch / CUDA)."""
+    if torch is not None and torch.cuda.is_available() and torch.cuda.is_initialized():
+        torch.cuda.current_stream(torch.device("cuda", device)).synchronize()
+
+
+def tuning_defaults() -> Tuning:
+    """The library's default fr_tuning (fr_tuning_defaults)."""
+    t = Tuning()
+    lib.fr_tuning_defaults(C.byref(t))
+    return t
+
+
+def gz_trim():
+    """Return the native inflate's cached decode buffers to the OS (fr_gz_trim)."""
+    lib.fr_gz_trim()
+
+
 class Context:
     """One GPU's scan state (fr_ctx)."""
 
-    def __init__(self, device: int = 0, chunk_bytes: int = 256 << 20, table_slots: int = 1 << 20):
+    def __init__(self, device: int = 0, chunk_bytes: int = 256 << 20, table_slots: int = 1 << 20,
+                 tuning: dict | None = None):
+        """tuning: fr_tuning fields to change from the library's defaults (tests and A/B runs only; the
+        product never passes any)."""
         self.device = int(device)
-        self.h = lib.fr_create(device, chunk_bytes, table_slots)
+        if tuning:
+            t = tuning_defaults()
+            for k, v in tuning.items():
+                if k == "size" or not hasattr(t, k):
+                    raise ValueError(f"unknown fr_tuning field {k!r}")
+                setattr(t, k, int(v))
+            self.h = lib.fr_create_tuned(device, chunk_bytes, table_slots, C.byref(t))
+        else:
+            self.h = lib.fr_create(device, chunk_bytes, table_slots)
         if not self.h:
             raise FrenderError("fr_create returned NULL")
         err = lib.fr_last_error(self.h)
@@ -676,18 +718,17 @@ class Context:
         return t
 
     def diag(self) -> dict:
-        v = np.zeros(20, dtype=np.uint64)
-        self._ck(lib.fr_get_diag(self.h, _ptr(v), 20), "fr_get_diag")
+        v = np.zeros(21, dtype=np.uint64)
+        self._ck(lib.fr_get_diag(self.h, _ptr(v), 21), "fr_get_diag")
         d = dict(zip(("spin_max", "spin_total", "keys", "overflow", "presence", "exotic", "grid", "slots"),
                      v[:8].tolist()))
         d["spec_replays"] = int(v[16])
         d["exo_replays"] = int(v[17])
         d["chunk_tiles"] = int(v[18])  # full-chunk size of the next ramped launch (larger once commits log)
         d["heavy_launches"] = int(v[19])  # ramped launches since the reset that walked the heavy chunk size
+        d["big_rollbacks"] = int(v[20])  # big feeds replayed in logged ranges (the table ran out of room)
         if v[8:16].any():  # FR_TIMING build / FR_ABLATE=64: per-phase cycles or commit counts
-            names = (("lookback", "barrier", "headers", "parse", "stage", "count", "flush", "prologue")
-                     if os.environ.get("FR_KERNEL") == "0" else
-                     ("guess", "walk0", "wait0", "resolve", "walk1", "commit", "kernel", "chunks"))
+            names = ("guess", "walk0", "wait0", "resolve", "walk1", "commit", "kernel", "chunks")
             d["stamps"] = dict(zip(names, v[8:].tolist()))
         return d
 
@@ -699,6 +740,12 @@ class Context:
         self._ck(lib.fr_set_timing(self.h, 1 if on else 0), "fr_set_timing")
 
     def export_unique_device(self, keys_ptr: int, counts_ptr: int, first_ptr: int, cap: int):
+        """Copy the finalized table into device buffers (fr_export_unique_device: queued on the library's
+        stream, which it synchronises before returning).  Stream contract: buffers that
+        torch allocated may still be in use by work queued on torch's stream (its caching allocator hands
+        a block back as soon as its last use is QUEUED), so torch's stream is drained first; afterwards the
+        rows are complete in HBM and any stream (torch's, RCCL's) may read them."""
+        _torch_stream_done(self.device)
         self._ck(lib.fr_export_unique_device(self.h, P(keys_ptr), P(counts_ptr), P(first_ptr), cap),
                  "fr_export_unique_device")
 

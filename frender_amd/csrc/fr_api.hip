@@ -83,6 +83,8 @@ struct fr_ctx {
     u64 tiles_cap = 0;
     bool spec_ok = true;        // FR_SPEC_COMMIT=0: every chunk waits for its exact prefix
     u64 spec_replays = 0;       // feeds replayed after a wrong speculative guess (diagnostics)
+    u64 big_rollbacks = 0;      // device feeds replayed in smaller ranges: the table ran out of room in a launch
+    bool grow_sync = false;     // maybe_grow waits for the previous launch's state (room replays)
     u32 spec_commit = 0;        // the current feed commits speculative chunks at once
     u32 epoch = 0;
     u32 par = 0;
@@ -334,7 +336,8 @@ static int flush_presence(fr_ctx* ctx) {
 // called before each tally launch: act on the latest asynchronous snapshot, if ready
 static int maybe_grow(fr_ctx* ctx) {
     if (ctx->st_pending) {
-        if (hipEventQuery(ctx->st_ev) != hipSuccess) return FR_OK;
+        if (ctx->grow_sync) CK(hipEventSynchronize(ctx->st_ev));
+        else if (hipEventQuery(ctx->st_ev) != hipSuccess) return FR_OK;
         ctx->st_pending = false;
     } else if (!ctx->st_fresh) {
         return FR_OK;  // nothing new since the last decision
@@ -622,7 +625,40 @@ static int launch_range(fr_ctx* ctx, const u8* dptr, u64 len, u64 avail, int own
 
 extern "C" {
 
+void fr_tuning_defaults(fr_tuning* t) {
+    if (!t) return;
+    const fr_ctx d{};  // the defaults live in fr_ctx's initialisers
+    std::memset(t, 0, sizeof(*t));
+    t->size = sizeof(fr_tuning);
+    t->grid = 0;
+    t->flush_at = d.flush_at;
+    t->cold_cap = d.cold_cap;
+    t->log = 1;
+    t->log_min = d.log_min;
+    t->log_hot = d.log_hot;
+    t->chunk_tiles = d.chunk_tiles;
+    t->chunk_tiles_heavy = d.chunk_tiles_heavy;
+    t->ramp = d.ramp ? 1 : 0;
+    t->ramp_up_s = d.ramp_up_s;
+    t->ramp_down_s = d.ramp_down_s;
+    t->ramp_down_pct = d.ramp_down_pct;
+    t->ramp_down_pct_h = d.ramp_down_pct_h;
+    t->spec_commit = d.spec_ok ? 1 : 0;
+    t->nbr = d.nbr_enabled ? 1 : 0;
+    t->ovf_cap = 0;
+}
+
 fr_ctx* fr_create(int device, uint64_t chunk_bytes, uint64_t table_slots) {
+    return fr_create_tuned(device, chunk_bytes, table_slots, nullptr);
+}
+
+fr_ctx* fr_create_tuned(int device, uint64_t chunk_bytes, uint64_t table_slots, const fr_tuning* tuning) {
+    fr_tuning t;
+    fr_tuning_defaults(&t);
+    if (tuning) {  // the caller's fields up to its size; the rest keep their defaults
+        const size_t n = std::min<size_t>(std::max<uint32_t>(tuning->size, sizeof(uint32_t)), sizeof(fr_tuning));
+        std::memcpy((char*)&t + sizeof(uint32_t), (const char*)tuning + sizeof(uint32_t), n - sizeof(uint32_t));
+    }
     fr_ctx* ctx = new fr_ctx();
     ctx->device = device;
     auto bad = [&](const char* what, hipError_t e) {
@@ -636,23 +672,30 @@ fr_ctx* fr_create(int device, uint64_t chunk_bytes, uint64_t table_slots) {
     hipDeviceProp_t prop;
     if ((e = hipGetDeviceProperties(&prop, device)) != hipSuccess) return bad("props", e);
     const int per_cu = chunk_occupancy();  // ~40 KB LDS per workgroup; VGPRs sized by __launch_bounds__
-    ctx->grid = prop.multiProcessorCount * per_cu;
-    if (const char* g = getenv("FR_GRID")) ctx->grid = std::max(1, atoi(g));
-    if (const char* f = getenv("FR_FLUSH_AT")) ctx->flush_at = (u32)atoi(f);
-    if (const char* f = getenv("FR_NBR")) ctx->nbr_enabled = atoi(f) != 0;
-    if (const char* f = getenv("FR_COLD_CAP")) ctx->cold_cap = (u32)std::max(1024, atoi(f));
+    ctx->grid = t.grid > 0 ? t.grid : prop.multiProcessorCount * per_cu;
+    ctx->flush_at = std::min<u32>(t.flush_at, NS);
+    ctx->nbr_enabled = t.nbr != 0;
+    ctx->cold_cap = std::max<u32>(1024, t.cold_cap);
+    ctx->log_min = t.log_min;
+    ctx->log_hot = std::max<u32>(1, t.log_hot);
+    ctx->chunk_tiles = std::max<u32>(2, t.chunk_tiles);
+    ctx->chunk_tiles_heavy = std::max<u32>(2, t.chunk_tiles_heavy);
+    ctx->ramp = t.ramp != 0;
+    ctx->ramp_up_s = std::max<u32>(1, t.ramp_up_s);
+    ctx->ramp_down_s = std::max<u32>(1, t.ramp_down_s);
+    ctx->ramp_down_pct = std::min<u32>(100, std::max<u32>(1, t.ramp_down_pct));
+    ctx->ramp_down_pct_h = std::min<u32>(100, std::max<u32>(1, t.ramp_down_pct_h));
+    ctx->spec_ok = t.spec_commit != 0;
     if ((e = dalloc(&ctx->cold, 2ull * ctx->cold_cap * (u64)ctx->grid)) != hipSuccess) return bad("cold lists", e);
     if ((e = dalloc(&ctx->rare, (u64)RARE_RING * (u64)ctx->grid)) != hipSuccess) return bad("rare rings", e);
 
-    if (const char* f = getenv("FR_LAUNCH_BYTES")) chunk_bytes = strtoull(f, nullptr, 10);  // launch-size A/B
     ctx->chunk_bytes = chunk_bytes ? ((chunk_bytes + TILE - 1) / TILE) * TILE : (256ull << 20);
     if (ctx->chunk_bytes > RANGE_MAX) ctx->chunk_bytes = RANGE_MAX;
     ctx->ring_bytes = std::min<u64>(ctx->chunk_bytes, HOST_CHUNK_MAX);
     // launch log: room for one pair per 256 B of a launch (SYN-v1 needs one per 350-500 B; a commit
     // that does not fit inserts into the table directly).  Only heavy commits log (ScanArgs::log_min);
-    // FR_LOG=0 turns the log off, FR_LOG_MIN sets the threshold (pairs per commit)
-    const char* fl = getenv("FR_LOG");
-    if (!fl || atoi(fl) != 0) {
+    // fr_tuning::log = 0 turns the log off
+    if (t.log) {
         // entries: 1 per 256 B of a launch (SYN-v1 config 3 logs ~1 per 700 B), in LOG_NR equal regions;
         // a run past its region's end inserts directly
         const u64 want = std::min<u64>(std::max<u64>(std::min<u64>(ctx->chunk_bytes, RANGE_LOG_MAX) / 256, 1ull << 16),
@@ -663,15 +706,6 @@ fr_ctx* fr_create(int device, uint64_t chunk_bytes, uint64_t table_slots) {
         if ((e = dalloc(&ctx->log, ctx->log_cap)) != hipSuccess) return bad("launch log", e);
         if ((e = dalloc(&ctx->log_sub, (u64)ctx->log_scap * LOG_NSUB)) != hipSuccess) return bad("launch log parts", e);
     }
-    if (const char* f = getenv("FR_LOG_MIN")) ctx->log_min = (u32)std::max(0, atoi(f));
-    if (const char* f = getenv("FR_LOG_HOT")) ctx->log_hot = (u32)std::max(1, atoi(f));
-    if (const char* f = getenv("FR_CHUNK_TILES")) ctx->chunk_tiles = (u32)std::max(2, atoi(f));
-    if (const char* f = getenv("FR_CHUNK_TILES_HEAVY")) ctx->chunk_tiles_heavy = (u32)std::max(2, atoi(f));
-    if (const char* f = getenv("FR_RAMP")) ctx->ramp = atoi(f) != 0;
-    if (const char* f = getenv("FR_RAMP_UP_S")) ctx->ramp_up_s = (u32)std::max(1, atoi(f));
-    if (const char* f = getenv("FR_RAMP_DOWN_S")) ctx->ramp_down_s = (u32)std::max(1, atoi(f));
-    if (const char* f = getenv("FR_RAMP_DOWN_PCT")) ctx->ramp_down_pct = (u32)std::min(100, std::max(1, atoi(f)));
-    if (const char* f = getenv("FR_RAMP_DOWN_PCT_H")) ctx->ramp_down_pct_h = (u32)std::min(100, std::max(1, atoi(f)));
     ctx->tiles_cap = RANGE_MAX / TSTEP + 2;
     ctx->nslots = pow2_at_least(std::max<u64>(table_slots, 1024));
     if ((e = hipMalloc((void**)&ctx->st, sizeof(DevState))) != hipSuccess) return bad("state", e);
@@ -694,11 +728,10 @@ fr_ctx* fr_create(int device, uint64_t chunk_bytes, uint64_t table_slots) {
     if ((e = hipEventCreateWithFlags(&ctx->st_ev, hipEventDisableTiming)) != hipSuccess) return bad("event", e);
     if ((e = dalloc(&ctx->tiles, ctx->tiles_cap)) != hipSuccess) return bad("tiles", e);
     if ((e = dalloc(&ctx->chunk_info, ctx->tiles_cap)) != hipSuccess) return bad("chunk info", e);
-    if (const char* f = getenv("FR_SPEC_COMMIT")) ctx->spec_ok = atoi(f) != 0;
     if ((e = hipMemset(ctx->tiles, 0, ctx->tiles_cap * sizeof(u64))) != hipSuccess) return bad("tiles", e);
     if ((e = dalloc(&ctx->tab.slots, ctx->nslots)) != hipSuccess) return bad("table", e);
     ctx->tab.mask = ctx->nslots - 1;
-    ctx->tab.ovf_cap = 1ull << 22;
+    ctx->tab.ovf_cap = t.ovf_cap ? std::max<u64>(t.ovf_cap, 1024) : (1ull << 22);
     ctx->tab.pres_cap = 1ull << 22;
     ctx->tab.exo_cap = 1ull << 20;
     ctx->tab.exo_pool_cap = 64ull << 20;
@@ -771,7 +804,7 @@ int fr_get_diag(fr_ctx* ctx, uint64_t* out, int n) {
                           (uint64_t)ctx->grid, ctx->nslots, s.stamp[0], s.stamp[1], s.stamp[2], s.stamp[3],
                           s.stamp[4],  s.stamp[5],  s.stamp[6], s.stamp[7], ctx->spec_replays, ctx->exo_replays,
                           s.heavy[ctx->par] ? ctx->chunk_tiles_heavy : ctx->chunk_tiles,  // the next ramped launch's
-                          s.heavy_launches};
+                          s.heavy_launches, ctx->big_rollbacks};
     for (int i = 0; i < n && i < (int)(sizeof(v) / sizeof(v[0])); ++i) out[i] = v[i];
     return FR_OK;
 }
@@ -1054,13 +1087,21 @@ int fr_feed_device(fr_ctx* ctx, const uint8_t* dev_data, uint64_t len) {
     // instead of two for the bench's 7.4 GB (the per-launch ramps and tail)
     // (and only when the table holds the last feed's new codes again at load <= 1/2: the table grows
     // between launches, never inside one)
-    const bool big = spec && !ctx->feed_logged && ctx->feed_keys != ~0ull &&
-                     (saved.n_keys + ctx->feed_keys) * 2 <= ctx->nslots;
-    const u64 lim = big ? ctx->chunk_bytes : std::min<u64>(ctx->chunk_bytes, RANGE_LOG_MAX);
-    const u64 nr = (len + lim - 1) / lim;
-    const u64 step = nr ? (len + nr - 1) / nr : 0;
-    for (int attempt = 0; attempt < 2; ++attempt) {
-        ctx->spec_commit = spec && attempt == 0 ? 1u : 0u;
+    // The decision rests on the previous feed (fr_reset keeps it: a bench or a seam scanning the same
+    // kind of data again).  A feed whose new codes outgrow the table inside one launch -- past the free
+    // slots and the overflow list -- is rolled back like a wrong speculation and replayed in ranges of an
+    // eighth of the size, with the table grown between them (each launch's state read before the next),
+    // down to RANGE_ROOM_MIN (speculative feeds: the rollback needs the snapshot).
+    bool big = spec && !ctx->feed_logged && ctx->feed_keys != ~0ull &&
+               (saved.n_keys + ctx->feed_keys) * 2 <= ctx->nslots;
+    bool spec_now = spec;
+    u64 step = 0, lim_room = ~0ull;
+    for (int attempt = 0; attempt < 12; ++attempt) {
+        const u64 lim = std::min<u64>(big ? ctx->chunk_bytes : std::min<u64>(ctx->chunk_bytes, RANGE_LOG_MAX),
+                                      lim_room);
+        const u64 nr = (len + lim - 1) / lim;
+        step = nr ? (len + nr - 1) / nr : 0;
+        ctx->spec_commit = spec_now ? 1u : 0u;
         for (u64 off = 0; off < len; off += step) {
             const u64 n = std::min<u64>(step, len - off);
             rc = launch_range(ctx, dev_data + off, n, len - off, off == 0 ? 1 : 0, 1, off ? 1 : 0);
@@ -1070,7 +1111,19 @@ int fr_feed_device(fr_ctx* ctx, const uint8_t* dev_data, uint64_t len) {
         // the feed's last byte lands with the state read below (one host round trip for both)
         if (!rc && len) CK(hipMemcpyAsync(ctx->h_byte, dev_data + len - 1, 1, hipMemcpyDeviceToHost, ctx->stream));
         if (!rc) rc = read_state(ctx);
-        if (rc || !spec || attempt == 1 || !ctx->h_st->spec_fail) break;
+        if (rc) break;
+        const bool spec_bad = spec_now && ctx->h_st->spec_fail;
+        // the overflow list ran out (fr_end_file would report FR_ERR_CAPACITY): smaller ranges, if any left
+        const bool room_bad = spec && (ctx->h_st->cap_flags & 2u) && step > RANGE_ROOM_MIN;
+        if (!spec_bad && !room_bad) break;
+        if (room_bad) {
+            big = false;
+            lim_room = std::max<u64>(RANGE_ROOM_MIN, ((step / 8) + TILE - 1) / TILE * TILE);
+            ctx->grow_sync = true;  // the replay's launches each see the table grown after the previous one
+            ctx->big_rollbacks++;
+        } else {
+            spec_now = false;
+        }
         // roll back: the table as it was (its size too), the device state, the launch parity
         if (ctx->nslots != snap_slots) {
             GSlot* fresh = nullptr;
@@ -1091,8 +1144,9 @@ int fr_feed_device(fr_ctx* ctx, const uint8_t* dev_data, uint64_t len) {
         ctx->st_fresh = true;
         ctx->par = par0;
         ctx->file_offset = ctx->file_base;
-        ctx->spec_replays++;
+        if (!room_bad) ctx->spec_replays++;
     }
+    ctx->grow_sync = false;
     if (snap) {
         CK(hipStreamSynchronize(ctx->stream));
         CK(hipFree(snap));

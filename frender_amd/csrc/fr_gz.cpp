@@ -93,6 +93,14 @@ class BufCache {
         b.resize(n);
         return b;
     }
+    void trim() {  // every cached buffer back to the OS
+        std::vector<Bytes> drop;
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            drop.swap(v_);
+            bytes_ = 0;
+        }
+    }
     void give(Bytes&& b) {
         Bytes drop = std::move(b);  // freed outside the lock when it does not stay
         if (drop.capacity() < (1u << 20)) return;
@@ -1013,6 +1021,7 @@ bool part_extend(fr_gz_part* p, uint64_t want) {
 // byte at decoded offset x (-1 past the file's end); data must cover it
 inline int part_byte(const fr_gz_part* p, uint64_t x) {
     if (x >= p->total) return -1;
+    if (x < p->dbase || x - p->dbase >= p->data.size()) abort();  // callers extend first: never read past data
     return p->data[x - p->dbase];
 }
 
@@ -1100,8 +1109,15 @@ int fr_gz_part_open(const char* path, int part, int nparts, int threads, fr_gz_p
             p->kn = p->ms.size();
         }
         p->inflated = p->data.size();
+        // the byte at M1 must be decoded too (a '\r' at M1 - 1 looks at it): the member found at M1 can
+        // be empty (an EOF block left mid-file by `cat` of BGZF files), so extend past it when needed
+        if (p->M1 < p->total && !part_extend(p, p->M1 + 1)) {
+            delete p;
+            fclose(fp);
+            return FR_ERR_IO;
+        }
         // terminators with their terminating byte in [M0, M1): every '\n', and every '\r' not followed
-        // by '\n' (the byte after M1 - 1 is the first of the member at M1, decoded above)
+        // by '\n' (the byte after M1 - 1 is decoded above)
         uint64_t n = 0;
         if (p->M1 > p->M0) {
             const uint8_t* b = p->data.data() + (p->M0 - p->dbase);
@@ -1178,6 +1194,8 @@ void fr_gz_part_close(fr_gz_part* p) {
 }  // extern "C"
 
 extern "C" {
+
+void fr_gz_trim(void) { buf_cache().trim(); }
 
 void fr_gz_close(fr_gz* g) {
     if (!g) return;

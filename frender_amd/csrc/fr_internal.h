@@ -44,6 +44,7 @@ constexpr u64 RANGE_MAX = (16ull << 30) - (1ull << 20);  // bytes per tally laun
 constexpr u64 RANGE_LOG_MAX = (4ull << 30) - (1ull << 20);  // a range whose commits may log (launch-log offsets
                                      // are u32 from the launch start), or whose exact line prefix matters (-s)
 constexpr u64 HOST_CHUNK_MAX = 1ull << 30;  // bytes per host-fed launch (pinned ring slot)
+constexpr u64 RANGE_ROOM_MIN = 1ull << 20;  // smallest range of a device feed replayed for table room
 constexpr u32 SPIN_MAX = 1u << 24;   // look-back spin bound (then FR_ERR_DEVICE)
 constexpr int ORD_SHIFT = 44;        // ordinal = file_tag << 44 | file byte offset
 constexpr int EXO_BUF = 32;          // chunk kernel: exotic records buffered while speculating

@@ -1638,12 +1638,14 @@ __global__ __launch_bounds__(WG, FR_OCC) void chunk_kernel(ScanArgs args) {
     const u64 k0_ = __builtin_amdgcn_s_memtime();
 #endif
     FR_STAMP_DECL
-    for (bool first = true;; first = false) {
+    for (;;) {
         if (tid == 0) {
-            // the first chunk is the workgroup's own index, the rest go by ticket after the grid's first
-            // chunks: 1024 workgroups no longer queue on one counter at the launch start (serialised
-            // same-address atomics: ~12 us before the last workgroup had its first chunk)
-            const u32 cn = first ? blockIdx.x : gridDim.x + atomicAdd(&a.st->ticket, 1u);
+            // every chunk goes by ticket, the first too: the chunk a look-back waits on is then always
+            // held by a workgroup that is already running.  (Round 4 gave each workgroup its own index
+            // as its first chunk; a resident workgroup could then wait on a chunk whose workgroup was not
+            // dispatched yet -- a grid larger than the free CUs, or another process's kernels holding
+            // them -- for a 0.2 % shorter launch head.)
+            const u32 cn = atomicAdd(&a.st->ticket, 1u);
             sh.chunk = cn;
             if (cn < g.num_chunks) {  // the chunk's base for its offsets (published by the barrier)
                 u32 tb0, te0;

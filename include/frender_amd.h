@@ -67,10 +67,38 @@ typedef struct fr_timing {
 } fr_timing;
 
 /* ---- lifecycle ------------------------------------------------------------------ */
-/* chunk_bytes: bytes per tally launch, at most 4 GiB - 1 MiB (device feeds are cut into equal
- * ranges of at most this size; host feeds use a pinned ring of min(chunk_bytes, 1 GiB) slots).
- * table_slots: initial HBM hash-table slots (grown between launches). */
+/* chunk_bytes: bytes per tally launch of a device feed, at most 16 GiB - 1 MiB (device feeds are cut
+ * into equal ranges of at most this size, and of at most 4 GiB - 1 MiB while their commits may go to
+ * the launch log; host feeds use a pinned ring of min(chunk_bytes, 1 GiB) slots).
+ * table_slots: initial HBM hash-table slots (grown between launches).  Nothing in the environment
+ * changes a context's geometry: fr_create uses the library's defaults, fr_create_tuned the caller's
+ * fr_tuning (tests, A/B runs). */
 fr_ctx* fr_create(int device, uint64_t chunk_bytes, uint64_t table_slots);
+/* The tally's launch geometry and thresholds.  Results never depend on them (every setting gives the
+ * same table); only the speed does.  Fill with fr_tuning_defaults, change fields, pass to
+ * fr_create_tuned.  `size` = sizeof(fr_tuning) of the caller (fields past it keep their defaults). */
+typedef struct fr_tuning {
+    uint32_t size;
+    int32_t grid;               /* tally workgroups; 0 = CUs x the kernel's occupancy */
+    uint32_t flush_at;          /* LDS-table keys per chunk before new codes go to the cold list */
+    uint32_t cold_cap;          /* cold-list entries per workgroup (>= 1024) */
+    int32_t log;                /* 1: heavy commits may go to the launch log; 0: every commit inserts directly */
+    uint32_t log_min;           /* pairs from which a commit logs (0: every commit) */
+    uint32_t log_hot;           /* a logged commit's LDS entries of >= log_hot records insert directly (>= 1) */
+    uint32_t chunk_tiles;       /* 4-KiB wave-tiles per full chunk (>= 2) */
+    uint32_t chunk_tiles_heavy; /* the same once commits log (>= 2) */
+    int32_t ramp;               /* 1: ramped chunk sizes; 0: one uniform chunk per workgroup */
+    uint32_t ramp_up_s;         /* the ramps' smallest chunks (tiles, >= 1) */
+    uint32_t ramp_down_s;
+    uint32_t ramp_down_pct;     /* ramp-down chunks, % of the grid (1..100), normal / heavy geometry */
+    uint32_t ramp_down_pct_h;
+    int32_t spec_commit;        /* 1: device feeds commit speculative chunks at once (checked at the launch end) */
+    int32_t nbr;                /* 1: classify through the sheet's neighbourhood maps; 0: row scan only */
+    uint64_t ovf_cap;           /* overflow-list entries (new codes a launch adds past the table's probe bound;
+                                 * 0 = 4 Mi; a device feed that overflows it is replayed in smaller ranges) */
+} fr_tuning;
+void fr_tuning_defaults(fr_tuning* t);
+fr_ctx* fr_create_tuned(int device, uint64_t chunk_bytes, uint64_t table_slots, const fr_tuning* t);
 void fr_destroy(fr_ctx* ctx);
 const char* fr_last_error(const fr_ctx* ctx);
 int fr_get_timing(fr_ctx* ctx, fr_timing* out);
@@ -81,7 +109,8 @@ int fr_get_timing(fr_ctx* ctx, fr_timing* out);
 int fr_set_timing(fr_ctx* ctx, int on);
 int fr_sync(fr_ctx* ctx);
 /* diagnostics: {look-back max polls, total polls, keys, overflow, presence, exotic, grid, slots,
- * 8 phase stamps, speculation replays, exotic-only replays} */
+ * 8 phase stamps, speculation replays, exotic-only replays, next full-chunk size, heavy launches,
+ * big-feed rollbacks} */
 int fr_get_diag(fr_ctx* ctx, uint64_t* out, int n);
 
 /* ---- sample sheet (the idx1/idx2/id lists of get_indexes, frender.py:90-116) -------
@@ -190,6 +219,10 @@ int fr_write_scan_csv(const char* path, const char* header, uint64_t n_rows, con
                       const uint64_t* exo_off);
 const char* fr_gz_error(const fr_gz* g);
 void fr_gz_close(fr_gz* g);
+/* Decode buffers outlive their pool: a process-wide cache keeps up to 4 GiB of them for the next scan
+ * (no page faults per GB).  fr_gz_trim returns every cached buffer to the OS (long-lived processes that
+ * scan once, e.g. the seam, call it after a scan). */
+void fr_gz_trim(void);
 
 /* The whole current file is already resident in HBM (bench / device producers). */
 int fr_feed_device(fr_ctx* ctx, const uint8_t* dev_data, uint64_t len);

@@ -145,18 +145,17 @@ def test_no_trailing_newline_and_truncated(ctx, lib):
 
 
 @pytest.mark.parametrize("log_min", [None, "0"])
-def test_speculative_commit_replay(lib, monkeypatch, log_min):
+def test_speculative_commit_replay(lib, log_min):
     """A file whose chunks look like 4-line FASTQ one line off the true phase: every chunk after
     the first guesses the wrong line phase, commits at once, the launch-end check catches it and
     the feed is replayed with every chunk waiting for its exact prefix (fr_feed_device).  With
-    FR_LOG_MIN=0 the failed attempt's commits went through the launch log and its aggregation."""
-    if log_min is not None:
-        monkeypatch.setenv("FR_LOG_MIN", log_min)
+    log_min=0 the failed attempt's commits went through the launch log and its aggregation."""
     recs = ["L 1:N:0:AAAA+CCCC\n"] + [f"@r{i} 1:N:0:ACGT+ACGT\nACGT\n+\nA AC\n" for i in range(60000)]
     data = "".join(recs).encode()
     exp = oracle_tally([data])
     assert list(exp[0]) == ["AAAA+CCCC", "AC"]
-    c = lib.Context(device=0, chunk_bytes=1 << 20, table_slots=1 << 16)
+    c = lib.Context(device=0, chunk_bytes=1 << 20, table_slots=1 << 16,
+                    tuning=None if log_min is None else {"log_min": int(log_min)})
     try:
         assert_same(gpu_tally(c, lib, [data], mode="device"), exp)
         assert c.diag()["spec_replays"] == 1
@@ -168,20 +167,19 @@ def test_speculative_commit_replay(lib, monkeypatch, log_min):
 
 
 @pytest.mark.parametrize("log_min", ["0", "60", "100000000"])
-def test_launch_log_commits(lib, monkeypatch, log_min):
-    """Commits of at least FR_LOG_MIN pairs go to the launch log and are aggregated after the launch
+def test_launch_log_commits(lib, log_min):
+    """Commits of at least fr_tuning.log_min pairs go to the launch log and are aggregated after the launch
     (count / scatter / LDS reduce / round-based table inserts); smaller ones insert directly.  Every
     commit logged (0), a mix (60: these 2-wave-tile chunks commit ~30-110 pairs), and none must give the
     oracle's tally, including a table that has to grow between launches."""
     from frender_amd import synth
-    monkeypatch.setenv("FR_LOG_MIN", log_min)
     rng = random.Random(int(log_min) + 7)
     sheet = synth.make_sheet(384, 10, 10)
     files = [synth.generate_bytes(sheet, 0, 300000, R=8, seed=3), random_fastq(rng, 20000, blank_seq=True),
              synth.generate_bytes(sheet, 300000, 5000, R=8, seed=3)]
     exp = oracle_tally(files)
     for mode, slots in (("device", 1 << 12), ("host", 1 << 20)):
-        c = lib.Context(device=0, chunk_bytes=1 << 22, table_slots=slots)
+        c = lib.Context(device=0, chunk_bytes=1 << 22, table_slots=slots, tuning={"log_min": int(log_min)})
         try:
             assert_same(gpu_tally(c, lib, files, mode=mode, pieces=lambda r: r.choice([4096, 1 << 20, 1 << 23]),
                                   rng=rng), exp)
@@ -189,7 +187,7 @@ def test_launch_log_commits(lib, monkeypatch, log_min):
             c.close()
 
 
-def test_heavy_chunk_switch(lib, monkeypatch):
+def test_heavy_chunk_switch(lib):
     """Ramped launches switch to the heavy chunk size once at least a quarter of the chunks since the
     reset logged their commits; the device decides at the end of each launch for the next one
     (fr_kernels.hip note_commit) and fr_reset clears it.  A 6-workgroup grid makes 1 MiB launches
@@ -198,11 +196,8 @@ def test_heavy_chunk_switch(lib, monkeypatch):
     chunks again, and a third pass switches again; every tally equals the oracle's."""
     from frender_amd import synth
     from oracle.frender_oracle import tally_text
-    monkeypatch.setenv("FR_GRID", "6")
-    monkeypatch.setenv("FR_LOG_MIN", "100")
-    monkeypatch.setenv("FR_CHUNK_TILES", "5")
-    monkeypatch.setenv("FR_CHUNK_TILES_HEAVY", "7")
-    c = lib.Context(device=0, chunk_bytes=1 << 20, table_slots=1 << 16)
+    c = lib.Context(device=0, chunk_bytes=1 << 20, table_slots=1 << 16,
+                    tuning={"grid": 6, "log_min": 100, "chunk_tiles": 5, "chunk_tiles_heavy": 7})
     try:
         assert c.diag()["chunk_tiles"] == 5
         sheet = synth.make_sheet(384, 10, 10)
@@ -349,8 +344,8 @@ def test_classify_random(ctx, lib, nsubs, rc):
 
 @pytest.mark.parametrize("nsubs", [0, 1, 2, 3])
 @pytest.mark.parametrize("rc", [False, True])
-def test_classify_neighbourhood_maps(lib, monkeypatch, nsubs, rc):
-    """The map path (a few probes per code) against the row scan (FR_NBR=0) and the oracle on an
+def test_classify_neighbourhood_maps(lib, nsubs, rc):
+    """The map path (a few probes per code) against the row scan (fr_tuning.nbr = 0) and the oracle on an
     adversarial 10+10 sheet: values 1 and 2 substitutions apart (codes near several values take the
     scan), repeated values (combinatorial rows), a lower-case and an 'x' entry, duplicated names."""
     from frender_amd.host import reverse_complement
@@ -386,9 +381,8 @@ def test_classify_neighbourhood_maps(lib, monkeypatch, nsubs, rc):
     data = "".join(f"@r{i} 1:N:0:{c}\n\n+\n\n" for i, c in enumerate(codes)).encode()
     names, nid = _sheet_names(ids)
     outs = []
-    for nbr in ("1", "0"):
-        monkeypatch.setenv("FR_NBR", nbr)
-        c = lib.Context(device=0, chunk_bytes=1 << 20, table_slots=1 << 16)
+    for nbr in (1, 0):
+        c = lib.Context(device=0, chunk_bytes=1 << 20, table_slots=1 << 16, tuning={"nbr": nbr})
         try:
             c.reset()
             c.begin_file(None)
@@ -415,14 +409,12 @@ def test_classify_neighbourhood_maps(lib, monkeypatch, nsubs, rc):
 
 
 @pytest.mark.parametrize("grid,cap,chunk", [(1, 1536, 1 << 24), (4, 0, 1 << 26), (64, 16, 1 << 26), (512, 1536, 1 << 30)])
-def test_many_tiles_per_workgroup(lib, monkeypatch, grid, cap, chunk):
+def test_many_tiles_per_workgroup(lib, grid, cap, chunk):
     """Few workgroups walking many tiles each (look-back windows sliding past 64 tiles),
     with the LDS table capped so most codes take the direct-to-HBM path."""
     from frender_amd import synth
     from oracle.frender_oracle import tally_text
-    monkeypatch.setenv("FR_GRID", str(grid))
-    monkeypatch.setenv("FR_FLUSH_AT", str(cap))
-    c = lib.Context(device=0, chunk_bytes=chunk, table_slots=1 << 16)
+    c = lib.Context(device=0, chunk_bytes=chunk, table_slots=1 << 16, tuning={"grid": grid, "flush_at": cap})
     try:
         sheet = synth.make_sheet(96, 8, 8)
         n = 1_500_000
@@ -1068,21 +1060,74 @@ def test_per_file_counts(lib, mode):
         c.close()
 
 
-def test_stray_ablation_env_has_no_effect(lib, monkeypatch):
-    """Timing ablations are compile-time only (FR_ABLATE in experiment builds): a stray FR_ABLATE in
-    the environment of the product library changes nothing (128 used to turn the commit's atomics
-    into plain stores)."""
+FORMER_KNOBS = {  # environment variables fr_create read before round 5, each at a hostile value
+    "FR_ABLATE": "128", "FR_GRID": "1", "FR_FLUSH_AT": "0", "FR_NBR": "0", "FR_COLD_CAP": "1",
+    "FR_LAUNCH_BYTES": "4096", "FR_LOG": "0", "FR_LOG_MIN": "0", "FR_LOG_HOT": "1", "FR_CHUNK_TILES": "2",
+    "FR_CHUNK_TILES_HEAVY": "2", "FR_RAMP": "0", "FR_RAMP_UP_S": "100", "FR_RAMP_DOWN_S": "100",
+    "FR_RAMP_DOWN_PCT": "1", "FR_RAMP_DOWN_PCT_H": "1", "FR_SPEC_COMMIT": "0"}
+
+
+def test_stray_env_has_no_effect(lib, monkeypatch):
+    """The product library reads no tuning from the environment (the geometry comes from fr_create's
+    defaults or an explicit fr_tuning; timing ablations are compile-time FR_ABLATE builds): with every
+    former knob set to a hostile value, a scan gives the identical table, classification, launch count
+    and geometry as without them (FR_LAUNCH_BYTES used to override the caller's chunk_bytes)."""
     from frender_amd import synth
+    from frender_amd.host import reverse_complement
+    from frender_amd.scan import _sheet_names
+
     sheet = synth.make_sheet(24, 8, 8)
-    data = synth.generate_bytes(sheet, 0, 300000, R=8, seed=4)
-    for v in ("128", "15"):
-        monkeypatch.setenv("FR_ABLATE", v)
+    n = 300000
+    data = synth.generate_bytes(sheet, 0, n, R=8, seed=4)
+    names, nid = _sheet_names(sheet.ids)
+
+    def run():
         c = lib.Context(device=0, chunk_bytes=1 << 22, table_slots=1 << 14)
         try:
-            got = gpu_tally(c, lib, [data])
+            p = c.device_alloc(len(data) + 16)
+            c.copy_to_device(p, data)
+            c.reset()
+            c.begin_file(None)
+            c.feed_device(p, len(data))
+            st = c.end_file()
+            c.device_free(p)
+            c.finalize()
+            keys, counts, first = c.unique()
+            c.set_sheet(sheet.idx1, sheet.idx2, [reverse_complement(x) for x in sheet.idx2], nid, len(names))
+            out = c.classify(1, True)
+            d = c.diag()
+            return (st.records, keys.tolist(), counts.tolist(), first.tolist(),
+                    {k: np.asarray(v).tolist() for k, v in out.items()}, c.timing().scan_launches,
+                    d["grid"], d["chunk_tiles"], d["spec_replays"])
         finally:
             c.close()
-        assert_same(got, oracle_tally([data]))
+
+    base = run()
+    for k, v in FORMER_KNOBS.items():
+        monkeypatch.setenv(k, v)
+    assert run() == base
+    assert base[5] == -(-len(data) // (1 << 22))  # launches of the caller's chunk_bytes
+
+
+def test_tuning_struct_changes_geometry_not_results(lib):
+    """fr_create_tuned: an explicit fr_tuning changes the launch geometry (grid, chunk size, logging,
+    ramps, speculation) but never the table."""
+    from frender_amd import synth
+
+    sheet = synth.make_sheet(96, 8, 8)
+    data = synth.generate_bytes(sheet, 0, 400000, R=8, seed=6)
+    exp = oracle_tally([data])
+    for tuning in (None, {"grid": 3, "chunk_tiles": 2, "ramp": 0}, {"log_min": 0, "log_hot": 1},
+                   {"spec_commit": 0, "cold_cap": 1024, "flush_at": 8}, {"ramp_up_s": 7, "ramp_down_pct": 10}):
+        c = lib.Context(device=0, chunk_bytes=1 << 21, table_slots=1 << 14, tuning=tuning)
+        try:
+            assert_same(gpu_tally(c, lib, [data], mode="device"), exp)
+            if tuning and "grid" in tuning:
+                assert c.diag()["grid"] == 3
+        finally:
+            c.close()
+    with pytest.raises(ValueError):
+        lib.Context(device=0, tuning={"no_such_field": 1})
 
 
 @pytest.mark.parametrize("world", [2, 3])

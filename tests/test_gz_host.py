@@ -79,3 +79,55 @@ def test_native_inflate_grows_past_the_trailer_hint(tmp_path):
     assert len(t) > 4 * os.path.getsize(p)
     for threads in (1, 2):
         assert decoded([p], threads) == [t]
+
+
+@pytest.mark.parametrize("eol", [b"\n", b"\r", b"\r\n"])
+def test_bgzf_parts_of_concatenated_files(tmp_path, eol):
+    """BGZF files joined by `cat` leave an empty EOF member mid-file.  A part cut that lands on it (here
+    the halfway point of two equal halves) must still decode the byte after it: with '\\r' line ends the
+    terminator count looks at that byte (fr_gz_part_open).  Every part split gives back the whole text,
+    each part starting at a record start, for LF, CR and CRLF records."""
+    rng = np.random.default_rng(len(eol))
+    half = fastq(rng, 3000).replace(b"\n", eol)
+    other = fastq(rng, 3000).replace(b"\n", eol)
+    other = other[:len(half)] if len(other) >= len(half) else other + b"@" * 0
+    text = half + other
+    p = str(tmp_path / "cat.fq.gz")
+    with open(p, "wb") as f:
+        f.write(bgzf(half, block=5000) + bgzf(other, block=5000))
+    assert gzip.decompress(open(p, "rb").read()) == text
+    starts = {0}
+    lines = text.replace(b"\r\n", b"\n").replace(b"\r", b"\n").split(b"\n")
+    off = 0
+    for i, ln in enumerate(lines[:-1]):  # byte offsets of record starts (every 4th line) in `text`
+        off += len(ln)
+        off += 2 if text[off:off + 2] == b"\r\n" else 1
+        if (i + 1) % 4 == 0:
+            starts.add(off)
+    for nparts in (2, 3, 4, 7):
+        parts = [_lib.GzPart.open(p, j, nparts) for j in range(nparts)]
+        try:
+            assert all(x is not None for x in parts)
+            before, got = 0, []
+            for x in parts:
+                data, base = x.data(before)
+                assert base in starts or base == len(text), (nparts, base)
+                got.append((base, data))
+                before += x.lines
+            assert b"".join(d for _, d in got) == text, nparts
+            assert [b for b, _ in got] == sorted(b for b, _ in got)
+        finally:
+            for x in parts:
+                x.close()
+
+
+def test_gz_trim_releases_the_cache(tmp_path):
+    """fr_gz_trim hands the cached decode buffers back; the next pool decodes into fresh ones."""
+    rng = np.random.default_rng(3)
+    t = fastq(rng, 20000)
+    p = str(tmp_path / "t.fq.gz")
+    with open(p, "wb") as f:
+        f.write(gzip.compress(t, compresslevel=1))
+    assert decoded([p], 1) == [t]
+    _lib.gz_trim()
+    assert decoded([p], 2) == [t]

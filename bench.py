@@ -58,9 +58,10 @@ def parse():
     ap.add_argument("--rank-check", action="store_true",
                     help="launcher check: every rank joins the process group over gloo, rank 0 prints the world "
                          "size it sees, nothing touches a GPU")
-    ap.add_argument("--pin-json", default=os.path.join(ROOT, "tests", "golden", "cfg2_pin.json"),
-                    help="the reference's own rows for BASELINE config 2 (tests/golden/make_golden_cfg2.py): at N=1 "
-                         "on that exact shape the classified table must reproduce them (checked after timing)")
+    ap.add_argument("--pin-json", default=None,
+                    help="the reference's own rows for this shape (default tests/golden/cfg{2,3,4}_pin.json, made by "
+                         "tests/golden/make_golden_cfg2.py / make_golden_cfg34.py): at N=1 on that exact shape and read "
+                         "count the classified table must reproduce them (checked after timing)")
     ap.add_argument("--cfg5", action="store_true",
                     help="instead of the headline metric: BASELINE config 5's shape end to end (paired .fastq.gz, "
                          "R=150 -> scan + demux CLIs) beside the reference's CPU path (oracle port) on a bounded sample")
@@ -351,27 +352,40 @@ def cfg5(args):
             "note": "two CLI processes for the product (each pays its Python/torch start and GPU context)"}
 
 
-def pin_check(args, ctx, sheet, idx2rc, nid, names):
-    """BASELINE config 2 at N=1: the benchmarked table (the last timed step's), classified, must equal
-    the reference's own tally_barcodes + process rows on the same records (tests/golden/cfg2_pin.json:
-    unique codes, sha256 over every row in order, first/last 1000 rows).  Outside the timed region."""
-    from frender_amd import _lib, synth
+PIN_FILES = {"BASELINE config 2": "cfg2_pin.json", "BASELINE config 3 shape (384 samples, 10+10, -rc)": "cfg3_pin.json",
+             "BASELINE config 4 shape (96 combinatorial, n=2)": "cfg4_pin.json"}
 
-    with open(args.pin_json) as f:
+
+def pin_path(args):
+    if args.pin_json:
+        return args.pin_json
+    f = PIN_FILES.get(config_name(args))
+    return os.path.join(ROOT, "tests", "golden", f) if f else None
+
+
+def pin_check(args, ctx, sheet):
+    """At N=1 on a pinned shape (BASELINE config 2, the config-3 and config-4 shapes at the pin's read
+    count), the benchmarked table (the last timed step's), classified by the reference's own sequence
+    (synth.pin_rows: process; with -rc pass A, the per-name call, the idx2 rewrite and pass B), must
+    equal the reference's rows on the same records (tests/golden/cfg*_pin.json: unique codes, sha256
+    over every row in order, first/last 1000 rows; with -rc also pass A's rows and every rc call).
+    Outside the timed region."""
+    from frender_amd import synth
+
+    path = pin_path(args)
+    with open(path) as f:
         pin = json.load(f)
-    keys, counts, _ = ctx.unique()
-    ctx.set_sheet(sheet.idx1, sheet.idx2, idx2rc, nid, len(names))
-    out = ctx.classify(args.nsubs, False)
-    digest, first, last = synth.rows_digest(_lib.decode_keys(keys), counts, out, sheet.idx1, sheet.idx2, sheet.ids)
-    ok = (len(keys) == pin["unique_codes"] and digest == pin["rows_sha256"] and first == pin["first_rows"]
-          and last == pin["last_rows"])
-    if not ok:
-        raise SystemExit(f"bench: the benchmarked table differs from the reference's rows ({args.pin_json}): "
-                         f"{len(keys)} vs {pin['unique_codes']} codes, sha256 {digest} vs {pin['rows_sha256']}")
-    return {"file": os.path.relpath(args.pin_json, ROOT), "unique_codes": pin["unique_codes"],
-            "rows_sha256": digest, "equal": True,
-            "source": "reference frender.py tally_barcodes + process on the same records (imported in the "
-                      "build container by tests/golden/make_golden_cfg2.py)"}
+    if pin.get("reads", args.reads) != args.reads:
+        return None
+    got = synth.pin_rows(ctx, sheet, args.nsubs, args.rc)
+    bad = synth.pin_differences(got, pin)
+    if bad:
+        raise SystemExit(f"bench: the benchmarked table differs from the reference's rows ({path}): {bad}; "
+                         f"{got['unique_codes']} vs {pin['unique_codes']} codes")
+    return {"file": os.path.relpath(path, ROOT), "unique_codes": pin["unique_codes"], "rows_sha256": got["rows_sha256"],
+            "equal": True, "rc_calls_equal": True if args.rc else None,
+            "source": f"reference frender.py tally_barcodes + process{' (+ rc call and pass B)' if args.rc else ''} on "
+                      f"the same records (imported in the build container by {pin.get('generated_by', '').split(':')[0]})"}
 
 
 def rank_check(world):
@@ -526,8 +540,9 @@ def main():
         U, csum = (int(x) for x in reduce_sum(dist, wire, [U, csum]))
     csum &= (1 << 64) - 1
     pinned = None
-    if world == 1 and config_name(args) == "BASELINE config 2" and os.path.exists(args.pin_json):
-        pinned = pin_check(args, ctx, sheet, idx2rc, nid, names)
+    pp = pin_path(args)
+    if world == 1 and pp and os.path.exists(pp):
+        pinned = pin_check(args, ctx, sheet)
     if rank == 0:
         cpu = None if (args.no_cpu or world > 1) else cpu_baseline(args, ctx, sheet, reclen)  # N=1 only
         value = world * n / (ms / 1e3) / 1e6

@@ -92,13 +92,12 @@ struct fr_ctx {
     Table tab{};
     u64 nslots = 0;
 
-    // launch sizes: chunk_bytes bytes per tally launch of device feeds (<= RANGE_MAX; <= RANGE_LOG_MAX unless
-    // the previous device feed would not have logged: feed_logged); host feeds
+    // launch sizes: chunk_bytes bytes per tally launch of device feeds (<= RANGE_MAX; <= RANGE_FIRST_MAX until a
+    // previous device feed's new codes are known to fit the table again: feed_keys); host feeds
     // go through a pinned ring of ring_bytes slots (<= HOST_CHUNK_MAX)
     u64 chunk_bytes = 0;
     u64 ring_bytes = 0;
-    bool feed_logged = true;  // the last device feed logged (or would have): its ranges stay <= RANGE_LOG_MAX
-    u64 feed_keys = ~0ull;    // codes the last device feed created (a range over RANGE_LOG_MAX also needs table room)
+    u64 feed_keys = ~0ull;    // codes the last device feed created (a range over RANGE_FIRST_MAX needs table room for them)
     u32 chunk_tiles = 320;  // wave-tiles (4 KiB) per full chunk of a ramped launch (FR_CHUNK_TILES; round 2's
                             // 80 workgroup tiles of 16 KiB: 64-96 measured within 2 %, 80 best)
     // Ramped launches after one in which at least a quarter of the chunks since the reset logged their
@@ -594,7 +593,7 @@ static int launch_range(fr_ctx* ctx, const u8* dptr, u64 len, u64 avail, int own
     }
     a.cold_cap = ctx->cold_cap;
     a.cold = ctx->cold;
-    a.log = (exo_only || len > RANGE_LOG_MAX) ? nullptr : ctx->log;  // launch-log offsets are u32
+    a.log = exo_only ? nullptr : ctx->log;  // log entries carry 34-bit launch offsets: any range may log
     a.log_cap = ctx->log_cap;
     a.log_rcap = ctx->log_rcap;
     a.log_min = ctx->log_min;
@@ -698,8 +697,7 @@ fr_ctx* fr_create_tuned(int device, uint64_t chunk_bytes, uint64_t table_slots, 
     if (t.log) {
         // entries: 1 per 256 B of a launch (SYN-v1 config 3 logs ~1 per 700 B), in LOG_NR equal regions;
         // a run past its region's end inserts directly
-        const u64 want = std::min<u64>(std::max<u64>(std::min<u64>(ctx->chunk_bytes, RANGE_LOG_MAX) / 256, 1ull << 16),
-                                       1ull << 26);  // logged ranges are <= RANGE_LOG_MAX
+        const u64 want = std::min<u64>(std::max<u64>(ctx->chunk_bytes / 256, 1ull << 16), 1ull << 26);
         ctx->log_rcap = (u32)(want / LOG_NR);
         ctx->log_cap = (u64)ctx->log_rcap * LOG_NR;
         ctx->log_scap = (u32)std::max<u64>(2ull * ctx->log_rcap / LOG_SUBS, 64);  // 2x the mean share
@@ -1081,23 +1079,19 @@ int fr_feed_device(fr_ctx* ctx, const uint8_t* dev_data, uint64_t len) {
         CK(dalloc(&snap, snap_slots));
         CK(hipMemcpyAsync(snap, ctx->tab.slots, snap_slots * sizeof(GSlot), hipMemcpyDeviceToDevice, ctx->stream));
     }
-    // equal ranges of at most chunk_bytes.  A range over RANGE_LOG_MAX runs without the launch log (its
-    // offsets are u32), so it is taken only for speculative feeds after a feed whose commits did not log
-    // (DevState::log_commits counts the would-be logged commits of an unlogged launch too): one launch
-    // instead of two for the bench's 7.4 GB (the per-launch ramps and tail)
-    // (and only when the table holds the last feed's new codes again at load <= 1/2: the table grows
-    // between launches, never inside one)
-    // The decision rests on the previous feed (fr_reset keeps it: a bench or a seam scanning the same
+    // Equal ranges of at most chunk_bytes: one launch (one set of ramps and tail, one launch-log aggregation)
+    // for the bench's 7.4 GB, DESIGN.md §4.1.  The table grows between launches, never inside one, so a range
+    // over RANGE_FIRST_MAX is taken only for speculative feeds whose table holds the last feed's new codes
+    // again at load <= 1/2.  The decision rests on the previous feed (fr_reset keeps it: a bench or a seam scanning the same
     // kind of data again).  A feed whose new codes outgrow the table inside one launch -- past the free
     // slots and the overflow list -- is rolled back like a wrong speculation and replayed in ranges of an
     // eighth of the size, with the table grown between them (each launch's state read before the next),
     // down to RANGE_ROOM_MIN (speculative feeds: the rollback needs the snapshot).
-    bool big = spec && !ctx->feed_logged && ctx->feed_keys != ~0ull &&
-               (saved.n_keys + ctx->feed_keys) * 2 <= ctx->nslots;
+    bool big = spec && ctx->feed_keys != ~0ull && (saved.n_keys + ctx->feed_keys) * 2 <= ctx->nslots;
     bool spec_now = spec;
     u64 step = 0, lim_room = ~0ull;
     for (int attempt = 0; attempt < 12; ++attempt) {
-        const u64 lim = std::min<u64>(big ? ctx->chunk_bytes : std::min<u64>(ctx->chunk_bytes, RANGE_LOG_MAX),
+        const u64 lim = std::min<u64>(big ? ctx->chunk_bytes : std::min<u64>(ctx->chunk_bytes, RANGE_FIRST_MAX),
                                       lim_room);
         const u64 nr = (len + lim - 1) / lim;
         step = nr ? (len + nr - 1) / nr : 0;
@@ -1152,7 +1146,6 @@ int fr_feed_device(fr_ctx* ctx, const uint8_t* dev_data, uint64_t len) {
         CK(hipFree(snap));
     }
     if (rc) return rc;
-    ctx->feed_logged = ctx->h_st->log_commits != saved.log_commits;  // read_state above: exact
     ctx->feed_keys = ctx->h_st->n_keys - saved.n_keys;
     // exotic records overflowed the list: grow it to the counted totals and run the feed's launches
     // again capturing exotic records only (the table is already complete), then drain

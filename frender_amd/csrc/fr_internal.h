@@ -41,8 +41,8 @@ constexpr int WIDE_NOPLUS = 31;
 constexpr u64 RANGE_MAX = (16ull << 30) - (1ull << 20);  // bytes per tally launch (device feeds): positions
                                      // are u32 offsets inside a chunk (ScanShared::cbase), so a range is bounded
                                      // by the look-back arrays (tiles_cap) only
-constexpr u64 RANGE_LOG_MAX = (4ull << 30) - (1ull << 20);  // a range whose commits may log (launch-log offsets
-                                     // are u32 from the launch start), or whose exact line prefix matters (-s)
+constexpr u64 RANGE_FIRST_MAX = (4ull << 30) - (1ull << 20);  // ranges of a device feed with no history (the
+                                     // table grows between launches: a first feed of unknown cardinality is cut here)
 constexpr u64 HOST_CHUNK_MAX = 1ull << 30;  // bytes per host-fed launch (pinned ring slot)
 constexpr u64 RANGE_ROOM_MIN = 1ull << 20;  // smallest range of a device feed replayed for table room
 constexpr u32 SPIN_MAX = 1u << 24;   // look-back spin bound (then FR_ERR_DEVICE)
@@ -89,9 +89,14 @@ struct alignas(32) Overflow {
 // table sees one insert per distinct code per launch instead of one per commit and miss.
 struct alignas(16) LogEntry {
     u64 key;
-    u32 off;             // min range offset of the entry's records (the launch's file tag / offset complete the ordinal)
-    u32 cnt;
+    u64 oc;              // min launch offset of the entry's records << LOG_CNT_BITS | records (log_pack): offsets of
+                         // ranges up to RANGE_MAX (34 bits), so a logged launch may exceed 4 GiB
 };
+constexpr int LOG_CNT_BITS = 24;     // records of one key in one commit (a chunk): < 2^24 (else it inserts directly)
+constexpr u64 LOG_CNT_MAX = (1ull << LOG_CNT_BITS) - 1ull;
+__host__ __device__ inline u64 log_pack(u64 off, u64 cnt) { return (off << LOG_CNT_BITS) | cnt; }
+__host__ __device__ inline u64 log_off(u64 oc) { return oc >> LOG_CNT_BITS; }
+__host__ __device__ inline u32 log_cnt(u64 oc) { return (u32)(oc & LOG_CNT_MAX); }
 #ifndef FR_LOG_REGION_BITS
 #define FR_LOG_REGION_BITS 6
 #endif

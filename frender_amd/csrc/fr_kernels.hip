@@ -1058,8 +1058,8 @@ __device__ __attribute__((noinline)) void commit_buffers(ScanShared& sh, const S
         }
         logged = sh.log_on != 0;  // else (nothing but hot codes) every pair inserts directly
     } else if (!a.log && !a.exo_only && tid == 0 && nl + nc && nl + nc >= a.log_min) {
-        // a launch without a log (a range over RANGE_LOG_MAX): count the commit that would have logged, so
-        // the host goes back to logged ranges for the next feed (fr_feed_device) and note_commit sees it
+        // a launch without a log (fr_tuning log = 0): count the commit that would have logged (note_commit's
+        // heavy-geometry decision sees it)
         atomicAdd((unsigned long long*)&a.st->log_commits, 1ull);
     }
     if (logged) {
@@ -1067,12 +1067,12 @@ __device__ __attribute__((noinline)) void commit_buffers(ScanShared& sh, const S
         const u64 ord0 = make_ord(a, 0);
         // a pair past its region's end inserts directly (the region's claimed range up to its end is
         // always written: the aggregation reads min(cursor, log_rcap) entries)
-        auto put = [&](u64 k, u32 off, u32 cnt) {
+        auto put = [&](u64 k, u64 off, u32 cnt) {
             const u32 r = log_region(k);
             const u64 pos = (u64)rbase[r] + atomicAdd(&rcur[r], 1u);
-            if (pos < a.log_rcap) {
-                a.log[(u64)r * a.log_rcap + pos] = LogEntry{k, off, cnt};
-            } else {
+            const bool fits = cnt <= LOG_CNT_MAX;  // (a chunk holds fewer records unless its geometry is extreme)
+            if (pos < a.log_rcap) a.log[(u64)r * a.log_rcap + pos] = fits ? LogEntry{k, log_pack(off, cnt)} : LogEntry{0, 0};
+            if (pos >= a.log_rcap || !fits) {  // (a zero key is skipped by the aggregation)
                 const u64 k1[1] = {k};
                 const bool v1[1] = {true};
                 Resolved r1[1];
@@ -1087,7 +1087,7 @@ __device__ __attribute__((noinline)) void commit_buffers(ScanShared& sh, const S
             const LSlot e = sh.ls[tid + b * WG];
             hv[b] = e.key && e.cnt >= a.log_hot;
             hk[b] = e.key;
-            if (e.key && !hv[b]) put(e.key, (u32)(cb + e.mino), e.cnt);  // launch offsets: a logged range is < 4 GiB
+            if (e.key && !hv[b]) put(e.key, cb + e.mino, e.cnt);  // launch offsets (a logged range may exceed 4 GiB)
         }
         for (u32 i0 = tid; i0 < nc; i0 += CB * WG) {
             u64 k[CB], o[CB];
@@ -1099,7 +1099,7 @@ __device__ __attribute__((noinline)) void commit_buffers(ScanShared& sh, const S
             }
 #pragma unroll
             for (int q = 0; q < CB; ++q)
-                if (i0 + q * WG < nc) put(k[q], (u32)(o[q] - ord0), 1u);
+                if (i0 + q * WG < nc) put(k[q], o[q] - ord0, 1u);
         }
         Resolved rh[CL];
         made += resolve_batch<CL>(a, hk, hv, rh);
@@ -1907,9 +1907,15 @@ __device__ __forceinline__ bool last_block(u32* ctr) {
 constexpr int AGG_LNS = 4096;  // LDS slots of one sub-region's aggregation (64 KB: 2 workgroups per CU)
 constexpr int AGG_PROBE = 64;
 constexpr int CLAIM_WORDS = 2048;  // a reduce workgroup's claim bitmap: sub-regions of up to 64K slots (8 KB)
+// One folded code: w = min launch offset << AGG_CNT_BITS | records, updated with one 64-bit LDS CAS (offsets of
+// ranges up to RANGE_MAX need 34 bits: the min and the sum share the word so the slot stays 16 bytes)
+constexpr int AGG_CNT_BITS = 30;
+constexpr u64 AGG_CNT_MAX = (1ull << AGG_CNT_BITS) - 1ull;
+constexpr u64 AGG_W0 = ~0ull << AGG_CNT_BITS;  // empty: offset all ones, no records
+static_assert(RANGE_MAX < (1ull << (64 - AGG_CNT_BITS)), "fold offsets");
 struct alignas(16) AggSlot {
     u64 key;
-    u32 mino, cnt;  // min range offset, records
+    u64 w;
 };
 
 // distinct (key, count, first, last tag) rows into the HBM table in rounds: every pending row's probe
@@ -2070,7 +2076,7 @@ __global__ __launch_bounds__(256) void log_split_kernel(Table t, DevState* st, c
 #pragma unroll
         for (int q = 0; q < SPLIT_PER; ++q) {
             const u32 i = t0 + w * 64 * SPLIT_PER + q * 64 + lane;
-            e[q] = i < n ? part[i] : LogEntry{0, 0, 0};
+            e[q] = i < n ? part[i] : LogEntry{0, 0};
         }
 #pragma unroll
         for (int q = 0; q < SPLIT_PER; ++q) {
@@ -2108,8 +2114,8 @@ __global__ __launch_bounds__(256) void log_split_kernel(Table t, DevState* st, c
                 sub[(u64)(r * LOG_SUBS + sb[q]) * scap + pos] = e[q];
             } else {
                 const u64 key1[1] = {e[q].key};
-                const u32 cnt1[1] = {e[q].cnt};
-                const u64 ord1[1] = {ord0 + e[q].off};
+                const u32 cnt1[1] = {log_cnt(e[q].oc)};
+                const u64 ord1[1] = {ord0 + log_off(e[q].oc)};
                 const u32 tag1[1] = {file_tag};
                 const bool v1[1] = {true};
                 made += insert_rows<1>(t, st, key1, cnt1, ord1, tag1, v1);
@@ -2130,7 +2136,7 @@ __global__ __launch_bounds__(256) void log_reduce_kernel(Table t, DevState* st, 
     __shared__ AggSlot ls[AGG_LNS];
     __shared__ u32 zone_bits[CLAIM_WORDS];
     u32 made = 0;
-    for (int i = threadIdx.x; i < AGG_LNS; i += 256) ls[i] = AggSlot{0, 0xFFFFFFFFu, 0};
+    for (int i = threadIdx.x; i < AGG_LNS; i += 256) ls[i] = AggSlot{0, AGG_W0};
     // this sub-region's home range: slots [blockIdx.x n, (blockIdx.x + 1) n) of the table (table_home's top
     // bits are the region and sub-region bits); its claim zone skips the first GPROBE slots
     const u64 nslots = t.mask + 1ull, rn = nslots >= (u64)LOG_NSUB ? nslots / LOG_NSUB : 0ull;
@@ -2147,14 +2153,14 @@ __global__ __launch_bounds__(256) void log_reduce_kernel(Table t, DevState* st, 
     const u32 nn = (ABLATE & 512u) ? 0u : n;  // 512: timing ablation
     LogEntry nx[LB];
 #pragma unroll
-    for (int q = 0; q < LB; ++q) nx[q] = threadIdx.x + q * 256 < nn ? part[threadIdx.x + q * 256] : LogEntry{0, 0, 0};
+    for (int q = 0; q < LB; ++q) nx[q] = threadIdx.x + q * 256 < nn ? part[threadIdx.x + q * 256] : LogEntry{0, 0};
     for (u32 i0 = threadIdx.x; i0 < nn; i0 += LB * 256) {
         LogEntry ev[LB];
 #pragma unroll
         for (int q = 0; q < LB; ++q) {
             ev[q] = nx[q];
             const u32 j = i0 + LB * 256 + q * 256;
-            nx[q] = j < nn ? part[j] : LogEntry{0, 0, 0};
+            nx[q] = j < nn ? part[j] : LogEntry{0, 0};
         }
 #pragma unroll
         for (int q = 0; q < LB; ++q) {
@@ -2164,6 +2170,8 @@ __global__ __launch_bounds__(256) void log_reduce_kernel(Table t, DevState* st, 
                 sink ^= e.key;
                 continue;
             }
+            const u64 eoff = log_off(e.oc);
+            const u32 ecnt = log_cnt(e.oc);
             u32 h = (u32)mix64(e.key) & (AGG_LNS - 1);
             bool done = false;
             for (int pr = 0; pr < AGG_PROBE && !done; ++pr) {
@@ -2173,16 +2181,29 @@ __global__ __launch_bounds__(256) void log_reduce_kernel(Table t, DevState* st, 
                     k = old == 0 ? e.key : old;
                 }
                 if (k == e.key) {
-                    atomicAdd(&ls[h].cnt, e.cnt);
-                    if (e.off < ls[h].mino) atomicMin(&ls[h].mino, e.off);
-                    done = true;
+                    // min offset and record sum in one word: CAS until it holds (a sum that would pass
+                    // AGG_CNT_MAX leaves the slot alone and the row inserts on its own below)
+                    u64 cur = *(volatile u64*)&ls[h].w;
+                    for (;;) {
+                        const u64 c = (cur & AGG_CNT_MAX) + ecnt;
+                        if (c > AGG_CNT_MAX) break;
+                        const u64 nw = (min(cur >> AGG_CNT_BITS, eoff) << AGG_CNT_BITS) | c;
+                        const u64 old = atomicCAS((unsigned long long*)&ls[h].w, (unsigned long long)cur,
+                                                  (unsigned long long)nw);
+                        if (old == cur) {
+                            done = true;
+                            break;
+                        }
+                        cur = old;
+                    }
+                    break;
                 }
                 h = (h + 1) & (AGG_LNS - 1);
             }
-            if (!done) {  // a full LDS table: this row goes in on its own
+            if (!done) {  // a full LDS table (or a saturated slot): this row goes in on its own
                 const u64 key1[1] = {e.key};
-                const u32 cnt1[1] = {e.cnt};
-                const u64 ord1[1] = {ord0 + e.off};
+                const u32 cnt1[1] = {ecnt};
+                const u64 ord1[1] = {ord0 + eoff};
                 const u32 tag1[1] = {file_tag};
                 const bool v1[1] = {true};
                 made += insert_rows<1>(t, st, key1, cnt1, ord1, tag1, v1, cz);
@@ -2201,11 +2222,11 @@ __global__ __launch_bounds__(256) void log_reduce_kernel(Table t, DevState* st, 
 #pragma unroll
         for (int b = 0; b < FB; ++b) {
             const int i = i0 + b * 256;
-            const AggSlot e = i < AGG_LNS ? ls[i] : AggSlot{0, 0, 0};
-            v[b] = e.key != 0;
+            const AggSlot e = i < AGG_LNS ? ls[i] : AggSlot{0, AGG_W0};
+            v[b] = e.key != 0 && (e.w & AGG_CNT_MAX) != 0;
             key[b] = e.key;
-            cnt[b] = e.cnt;
-            ord[b] = ord0 + e.mino;
+            cnt[b] = (u32)(e.w & AGG_CNT_MAX);
+            ord[b] = ord0 + (e.w >> AGG_CNT_BITS);
             tag[b] = file_tag;
         }
         made += insert_rows<FB, true>(t, st, key, cnt, ord, tag, v, cz);

@@ -40,6 +40,7 @@ from collections.abc import Mapping
 
 import numpy as np
 
+from . import _lib
 from . import scan as _scan
 from .host import reverse_complement
 
@@ -211,8 +212,13 @@ def _table_of(counter) -> tuple:
 
 
 def tally_barcodes(cores, files, sample=None, ctx=None) -> BarcodeCounter:
-    """frender.py:183-207 on the GPU (frender_amd.scan.tally_barcodes), the reference's shape."""
-    return BarcodeCounter(_scan.tally_barcodes(cores, files, sample, ctx=ctx))
+    """frender.py:183-207 on the GPU (frender_amd.scan.tally_barcodes), the reference's shape.  A seam
+    caller is a long-lived process that may scan once: the inflate's cached decode buffers (up to 4 GiB)
+    go back to the OS afterwards (fr_gz_trim)."""
+    try:
+        return BarcodeCounter(_scan.tally_barcodes(cores, files, sample, ctx=ctx))
+    finally:
+        _lib.gz_trim()
 
 
 def process(cores, barcode_counter, indexes, num_subs, rc_mode, ctx=None) -> ResultsMapping:

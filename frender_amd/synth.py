@@ -269,22 +269,73 @@ def make_dataset(outdir: str, sheet: Sheet, n_reads: int, n_files: int = 1, R: i
 CLASS_NAMES = ("undetermined", "index_hop", "demuxable", "ambiguous")
 
 
-def rows_digest(codes, counts, out, idx1, idx2, ids, keep: int = 1000):
+def rows_digest(codes, counts, out, idx1, idx2, ids, keep: int = 1000, idx2rc=None):
     """sha256 over a classified unique table in its order, one line per code
     f"{code}\\t{reads}\\t{matched_idx1}\\t{matched_idx2}\\t{read_type}\\t{sample_name}\\n" (the row format
-    of tests/golden/cfg2_pin.json, which tests/golden/make_golden_cfg2.py computed from the reference's
-    own tally_barcodes + process), plus the first and last `keep` lines.  `out` holds fr_classify's
-    m1 / m2 / cls / row arrays."""
+    of tests/golden/cfg{2,3,4}_pin.json, which tests/golden/make_golden_cfg2.py / make_golden_cfg34.py
+    computed from the reference's own tally_barcodes + process), plus the first and last `keep` lines.
+    `out` holds fr_classify's m1 / m2 / cls / row arrays.  idx2rc given (an -rc pass A): each line also
+    carries \\t{matched_rc_idx2}\\t{rc_read_type}\\t{rc_sample_name} before its \\n (the rc_* arrays), as
+    the reference's analyze_barcodes_with_rc dicts do (frender.py:325-349)."""
     import hashlib
 
     m1, m2, cls, row = (np.asarray(out[k]).tolist() for k in ("m1", "m2", "cls", "row"))
+    if idx2rc is not None:
+        rm2, rcls, rrow = (np.asarray(out[k]).tolist() for k in ("rc_m2", "rc_cls", "rc_row"))
     h = hashlib.sha256()
     lines = []
     n = len(codes)
     for j, (c, k) in enumerate(zip(codes, np.asarray(counts).tolist())):
         line = (f"{c}\t{k}\t{idx1[m1[j]] if m1[j] >= 0 else ''}\t{idx2[m2[j]] if m2[j] >= 0 else ''}\t"
-                f"{CLASS_NAMES[cls[j]]}\t{ids[row[j]] if row[j] >= 0 else ''}\n")
+                f"{CLASS_NAMES[cls[j]]}\t{ids[row[j]] if row[j] >= 0 else ''}")
+        if idx2rc is not None:
+            line += (f"\t{idx2rc[rm2[j]] if rm2[j] >= 0 else ''}\t{CLASS_NAMES[rcls[j]]}\t"
+                     f"{ids[rrow[j]] if rrow[j] >= 0 else ''}")
+        line += "\n"
         h.update(line.encode())
         if j < keep or j >= n - keep:
             lines.append(line)
     return h.hexdigest(), lines[:keep], lines[-keep:] if n >= keep else lines
+
+
+def pin_rows(ctx, sheet: Sheet, nsubs: int, rc: bool, keep: int = 1000) -> dict:
+    """The reference's frender_scan sequence (frender.py:606-630) on ctx's finalized table, in the form
+    of tests/golden/cfg{2,3,4}_pin.json (make_golden_cfg2.py / make_golden_cfg34.py): process (:610); with
+    -rc its pass-A rows (with the rc columns), call_rc_mode_per_id's calls (:614, :367-388: use rc iff
+    f < rc), the idx2 rewrite (:618-623) and pass B (:628-630).  Returns unique_codes, rows_sha256,
+    first_rows, last_rows (the final pass) and, with -rc, pass_a and rc_calls [[name, f, rc, call]]."""
+    from ._lib import decode_keys
+    from .host import reverse_complement
+    from .scan import _sheet_names
+
+    names, nid = _sheet_names(sheet.ids)
+    idx2rc = [reverse_complement(x) for x in sheet.idx2]
+    keys, counts, _ = ctx.unique()
+    codes = decode_keys(keys)
+    ctx.set_sheet(sheet.idx1, sheet.idx2, idx2rc, nid, len(names))
+    out = ctx.classify(nsubs, rc)
+    res: dict = {"unique_codes": len(codes)}
+    idx2_final = list(sheet.idx2)
+    if rc:
+        d, f, l = rows_digest(codes, counts, out, sheet.idx1, sheet.idx2, sheet.ids, keep, idx2rc=idx2rc)
+        res["pass_a"] = {"rows_sha256": d, "first_rows": f, "last_rows": l}
+        fr, rr = ctx.rc_counts()
+        use = [int(a) < int(b) for a, b in zip(fr, rr)]
+        res["rc_calls"] = [[n, int(a), int(b), u] for n, a, b, u in zip(names, fr, rr, use)]
+        idx2_final = [reverse_complement(x) if use[nid[i]] else x for i, x in enumerate(sheet.idx2)]
+        ctx.set_sheet(sheet.idx1, idx2_final, [reverse_complement(x) for x in idx2_final], nid, len(names))
+        out = ctx.classify(nsubs, False)
+    d, f, l = rows_digest(codes, counts, out, sheet.idx1, idx2_final, sheet.ids, keep)
+    res.update({"rows_sha256": d, "first_rows": f, "last_rows": l})
+    return res
+
+
+def pin_differences(got: dict, pin: dict) -> list:
+    """The fields of a pin_rows result that differ from a committed pin (empty list = equal)."""
+    bad = [k for k in ("unique_codes", "rows_sha256", "first_rows", "last_rows") if got.get(k) != pin.get(k)]
+    if "pass_a" in pin:
+        bad += [f"pass_a.{k}" for k in ("rows_sha256", "first_rows", "last_rows")
+                if (got.get("pass_a") or {}).get(k) != pin["pass_a"].get(k)]
+        if got.get("rc_calls") != pin.get("rc_calls"):
+            bad.append("rc_calls")
+    return bad

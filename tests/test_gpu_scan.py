@@ -1012,6 +1012,48 @@ def test_bench_geometry_pinned_to_reference(lib, launch_gib):
         c.close()
 
 
+@pytest.mark.parametrize("cfg", [3, 4])
+def test_bench_geometry_pinned_cfg34(lib, cfg):
+    """bench.py's config-3 shape (384 samples, 10+10, n=1, -rc: 100M SYN-v1 records = 7.8 GB in HBM, heavy
+    commits logged, launch-log split/reduce, then -rc pass A, the per-name call, the idx2 rewrite and pass
+    B) and config-4 shape (96 combinatorial 12x8 dual indexes, n=2), each one launch after the first feed against the REFERENCE's own frender_scan
+    sequence on the same records (tests/golden/cfg3_pin.json / cfg4_pin.json, made by
+    tests/golden/make_golden_cfg34.py): unique codes, every final row in order (sha256), the first/last
+    1000 rows, and for config 3 every pass-A row (with the rc columns) and every per-name rc call.  Two
+    steps on one context with 16-GiB launches, as bench.py runs them."""
+    import json
+
+    from frender_amd import synth
+
+    path = os.path.join(os.path.dirname(__file__), "golden", f"cfg{cfg}_pin.json")
+    if not os.path.exists(path):
+        pytest.skip(f"{path} not generated")
+    with open(path) as f:
+        pin = json.load(f)
+    n = pin["reads"]
+    L, S = (10, 384) if cfg == 3 else (8, 96)
+    sheet = synth.make_sheet(S, L, L, combinatorial=(12, 8) if cfg == 4 else None)
+    reclen = synth.record_length(L, L, 8)
+    c = lib.Context(device=0, chunk_bytes=(16 << 30) - (1 << 20), table_slots=1 << 22)
+    buf = c.device_alloc(n * reclen + 64)
+    try:
+        c.synth_device(buf, 0, n, 8, 1, sheet.idx1, sheet.idx2)
+        for step in range(2):
+            c.reset()
+            c.begin_file(None, file_index=0, byte_base=0)
+            c.feed_device(buf, n * reclen)
+            st = c.end_file()
+            assert st.records == pin["total_reads"] and st.error == 0
+            launches = c.timing().scan_launches
+            c.finalize()
+            got = synth.pin_rows(c, sheet, 1 if cfg == 3 else 2, cfg == 3)
+            assert synth.pin_differences(got, pin) == [], (cfg, step)
+        assert launches == 1, launches  # the second feed: one launch (the first feed's codes fit the table)
+    finally:
+        c.device_free(buf)
+        c.close()
+
+
 @pytest.mark.parametrize("mode", ["host", "device"])
 def test_per_file_counts(lib, mode):
     """fr_get_presence_counts: the reads of each code in each file (the reference's per-file tables,

@@ -63,3 +63,63 @@ def test_oracle_cfg2_prefix_pinned():
                                             sheet.ids, keep=len(pin["first_rows"]))
     assert first == pin["first_rows"] and last == pin["last_rows"]
     assert digest == pin["rows_sha256"]
+
+
+def _rows(codes, counts, res, rc):
+    lines = []
+    for c, r in zip(codes, res):
+        line = f"{c}\t{counts[c]}\t{r['matched_idx1']}\t{r['matched_idx2']}\t{r['read_type']}\t{r['sample_name']}"
+        if rc:
+            line += f"\t{r['matched_rc_idx2']}\t{r['rc_read_type']}\t{r['rc_sample_name']}"
+        lines.append(line + "\n")
+    return hashlib.sha256("".join(lines).encode()).hexdigest(), lines
+
+
+@pytest.mark.parametrize("cfg", [3, 4])
+def test_oracle_cfg34_prefix_pinned(cfg):
+    """The oracle on the first records of the config-3 shape (384 samples, 10+10, -rc: pass A, the
+    per-name call, pass B) and the config-4 shape (12x8 combinatorial, n=2) reproduces the reference's
+    own frender_scan sequence (tests/golden/cfg{3,4}_pin_1m.json, made by tests/golden/make_golden_cfg34.py
+    with the reference imported)."""
+    import json
+    from multiprocessing import Pool
+
+    from frender_amd import synth
+    from frender_amd.host import reverse_complement
+    from oracle import frender_oracle as O
+
+    path = os.path.join(os.path.dirname(__file__), "golden", f"cfg{cfg}_pin_1m.json")
+    if not os.path.exists(path):
+        pytest.skip(f"{path} not generated")
+    with open(path) as f:
+        pin = json.load(f)
+    rc = cfg == 3
+    nsubs = 1 if cfg == 3 else 2
+    L, S = (10, 384) if cfg == 3 else (8, 96)
+    sheet = synth.make_sheet(S, L, L, combinatorial=(12, 8) if cfg == 4 else None)
+    counts, records = O.tally_text(synth.generate_bytes(sheet, 0, pin["reads"], R=8, seed=1).decode())
+    assert records == pin["total_reads"] and len(counts) == pin["unique_codes"]
+    codes = list(counts)
+    keep = len(pin["first_rows"])
+    idx2 = list(sheet.idx2)
+    with Pool(8) as pool:
+        res = pool.starmap(O.classify_code, [(c, counts[c], sheet.idx1, idx2, sheet.ids, nsubs, rc) for c in codes])
+        if rc:
+            digest, lines = _rows(codes, counts, res, True)
+            assert lines[:keep] == pin["pass_a"]["first_rows"] and lines[-keep:] == pin["pass_a"]["last_rows"]
+            assert digest == pin["pass_a"]["rows_sha256"]
+            sums = {n: [0, 0] for n in dict.fromkeys(sheet.ids)}
+            for r in res:
+                if r["sample_name"]:
+                    sums[r["sample_name"]][0] += r["reads"]
+                if r["rc_sample_name"]:
+                    sums[r["rc_sample_name"]][1] += r["reads"]
+            calls = [[n, f, b, f < b] for n, (f, b) in sums.items()]
+            assert calls == pin["rc_calls"]
+            use = {n: c for n, _, _, c in calls}
+            idx2 = [reverse_complement(x) if use[i] else x for i, x in zip(sheet.ids, idx2)]
+            res = pool.starmap(O.classify_code, [(c, counts[c], sheet.idx1, idx2, sheet.ids, nsubs, False)
+                                                 for c in codes])
+    digest, lines = _rows(codes, counts, res, False)
+    assert lines[:keep] == pin["first_rows"] and lines[-keep:] == pin["last_rows"]
+    assert digest == pin["rows_sha256"]

@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--cpu-reads", type=int, default=24_000_000, help="bounded sample for the CPU baseline (~10-20 s on 8 cores)")
     ap.add_argument("--cpu-cores", type=int, default=8)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-single", action="store_true",
+                    help="skip e2e.single_member (the cpu_baseline's records as one single-member .fastq.gz)")
     ap.add_argument("--merge", choices=["a2a", "tree"], default="a2a",
                     help="N>1 table merge: hash-partitioned all-to-all (every rank merges and classifies its "
                          "partition) or a binary tree into rank 0")
@@ -191,6 +193,44 @@ def e2e_scan(args, ns, d, n, cores):
                       f"cold_value = first run incl. context creation; host-inflate-bound"}
 
 
+def e2e_single(ns, d, path, n):
+    """The product `scan` on the same records as ONE single-member .fastq.gz (one NovaSeq lane's shape):
+    with `-c 16` every pool thread decodes the member together (fr_pinflate.h, the parallel single-member
+    inflate), with `-c 1` one thread decodes it (the rate before the parallel decoder).  Each is run
+    twice and timed warm; CSV contents are compared with the CPU baseline's (8-file) outputs."""
+    import argparse
+    import contextlib
+    import io
+
+    from frender_amd import _lib
+    from frender_amd import scan as S
+
+    out = {"unit": "M reads/s", "sample": f"{n} reads as one single-member gzip -1 .fastq.gz "
+                                          f"({os.path.getsize(path)} B compressed)"}
+    for cores in (16, 1):
+        times = []
+        for k in range(2):
+            sub = os.path.join(d, f"single_c{cores}_{k}")
+            os.mkdir(sub)
+            cwd = os.getcwd()
+            os.chdir(sub)
+            before = _lib.gz_parallel_members()
+            try:
+                with contextlib.redirect_stdout(io.StringIO()):
+                    t0 = time.perf_counter()
+                    S.frender_scan(argparse.Namespace(**dict(vars(ns), c=float(cores), files=[path])))
+                    times.append(time.perf_counter() - t0)
+            finally:
+                os.chdir(cwd)
+            parallel = _lib.gz_parallel_members() > before
+        same = sorted(open(os.path.join(d, sub, f), "rb").read() for f in os.listdir(os.path.join(d, sub))) == \
+            sorted(open(os.path.join(d, "out", f), "rb").read() for f in os.listdir(os.path.join(d, "out")))
+        out[f"c{cores}"] = {"value": round(n / times[1] / 1e6, 3), "cold_value": round(n / times[0] / 1e6, 3),
+                            "cores": cores, "parallel_inflate": parallel, "outputs_equal_cpu_baseline": same}
+    out["speedup_c16_over_c1"] = round(out["c16"]["value"] / out["c1"]["value"], 2)
+    return out
+
+
 def cpu_baseline(args, ctx, sheet, reclen):
     """The reference's CPU path, as restated by the oracle port (oracle.frender_oracle.scan: a
     Pool of `cores` workers over the input files, gzip text reader, tally, classify, CSV, exactly
@@ -218,6 +258,12 @@ def cpu_baseline(args, ctx, sheet, reclen):
         sheet.write_csv(os.path.join(d, "sheet.csv"))
         with Pool(cores) as pool:
             blobs = pool.map(_gz, [data[cuts[i] * reclen:cuts[i + 1] * reclen] for i in range(cores)])
+        single = None
+        if not args.no_single:  # the same records as ONE single-member .fastq.gz (gzip -1 of the whole text)
+            os.mkdir(os.path.join(d, "single"))
+            single = os.path.join(d, "single", "syn_L001_R1_001.fastq.gz")
+            with open(single, "wb") as f:
+                f.write(_gz(data))
         del data
         files = []
         for i, blob in enumerate(blobs):
@@ -239,6 +285,8 @@ def cpu_baseline(args, ctx, sheet, reclen):
         finally:
             os.chdir(cwd)
         e2e = e2e_scan(args, ns, d, n, cores)
+        if single:
+            e2e["single_member"] = e2e_single(ns, d, single, n)
     global _E2E
     _E2E = e2e
     cal = ""

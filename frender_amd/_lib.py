@@ -132,6 +132,7 @@ _SIGS = {
     "fr_gz_part_close": (None, [P]),
     "fr_gz_close": (None, [P]),
     "fr_gz_trim": (None, []),
+    "fr_gz_parallel_members": (C.c_uint64, []),
     # demux (row f-1)
     "fr_dmx_create": (P, [C.c_int]),
     "fr_dmx_destroy": (None, [P]),
@@ -465,6 +466,11 @@ def tuning_defaults() -> Tuning:
     t = Tuning()
     lib.fr_tuning_defaults(C.byref(t))
     return t
+
+
+def gz_parallel_members() -> int:
+    """Files this process decoded with the parallel single-member inflate (fr_gz_parallel_members)."""
+    return int(lib.fr_gz_parallel_members())
 
 
 def gz_trim():

@@ -43,6 +43,7 @@
 #include <vector>
 
 #include "../../include/frender_amd.h"
+#include "fr_pinflate.h"
 
 // Byte buffers whose resize() does not zero-fill: every byte of a decode buffer is written by the
 // decoder before anything reads it, and zeroing 1-2 GB per scan cost as much as the copies.
@@ -181,6 +182,9 @@ constexpr size_t BGZF_MAX_IN = 1ull << 30;   // BGZF files: compressed bytes for
 constexpr size_t BGZF_MAX_BLOCK = 65536;     // the format's bound on a member's size and ISIZE
 constexpr size_t BGZF_WINDOW = 64ull << 20;  // decoded bytes per parallel BGZF window
 constexpr size_t WHOLE_BUDGET = 3ull << 30;  // whole-file buffers (input + output) held at once per pool
+constexpr size_t PGZ_MIN_IN = 16ull << 20;   // single-member files from this compressed size decode in parallel
+constexpr size_t PGZ_CHUNK_MIN = 2ull << 20;  // compressed bytes per parallel chunk (about 4 per thread)
+constexpr size_t PGZ_CHUNK_MAX = 32ull << 20;
 
 struct Member {
     size_t off, len, dst, isize;
@@ -278,6 +282,72 @@ void give_budget(fr_gz* g, size_t bytes) {
     g->whole_used -= bytes;
 }
 
+// One big gzip member (plus NUL padding) decoded by every idle thread of the pool (fr_pinflate.h):
+// true when the file's bytes were queued (or the scan cancelled it); false leaves nothing queued (not a
+// single clean member, no budget, or any decode / CRC / ISIZE failure) and the caller decodes the file
+// with one thread, whose decoders own the exact error behaviour.
+std::atomic<uint64_t> g_parallel_members{0};  // files decoded by inflate_member_parallel (fr_gz_parallel_members)
+
+bool inflate_member_parallel(fr_gz* g, GzFile& f, const Bytes& in) {
+    const size_t n = in.size();
+    if (n < 32 || in[0] != 0x1f || in[1] != 0x8b || in[2] != 8 || (in[3] & 0xE0)) return false;
+    const uint8_t flg = in[3];
+    size_t h = 10;
+    if (flg & 4) {  // FEXTRA
+        if (h + 2 > n) return false;
+        h += 2 + le16(&in[h]);
+    }
+    for (int bit : {8, 16})  // FNAME, FCOMMENT: zero-terminated
+        if (flg & bit) {
+            while (h < n && in[h]) ++h;
+            ++h;
+        }
+    if (flg & 2) h += 2;  // FHCRC
+    if (h + 8 >= n) return false;
+    // the trailer's ISIZE sizes the output budget (exact up to 4 GiB decoded; otherwise 4x the input)
+    const size_t hint = le32(&in[n - 4]);
+    const size_t est = hint >= n ? hint : 4 * n;
+    if (!take_budget(g, est)) return false;
+    struct Hold {
+        fr_gz* g;
+        size_t b;
+        ~Hold() { give_budget(g, b); }
+    } hold{g, est};
+    const int nh = take_threads(g, g->threads - 1);
+    struct Threads {
+        fr_gz* g;
+        int k;
+        ~Threads() { give_threads(g, k); }
+    } held{g, nh};
+    const int T = nh + 1;
+    if (T < 2) return false;
+    const size_t chunk = std::min<size_t>(PGZ_CHUNK_MAX, std::max<size_t>(PGZ_CHUNK_MIN, (n - h) / (4 * (size_t)T)));
+    std::vector<Bytes> pieces;
+    frpz::Result r;
+    bool ok = frpz::inflate_parallel<Bytes>(in.data() + h, n - h, T, chunk, pieces, r);
+    // the member's trailer (CRC-32, ISIZE), then nothing but NUL padding: one clean member
+    if (ok) {
+        const size_t t = h + r.dend;
+        ok = t + 8 <= n && le32(&in[t]) == r.crc && le32(&in[t + 4]) == (uint32_t)r.total;
+        for (size_t q = t + 8; ok && q < n; ++q) ok = in[q] == 0;
+    }
+    if (!ok) {
+        for (auto& b : pieces) buf_cache().give(std::move(b));
+        return false;
+    }
+    g_parallel_members.fetch_add(1);
+    for (auto& b : pieces) {
+        std::unique_lock<std::mutex> lk(g->m);
+        g->cv.wait(lk, [&] { return f.q.size() < g->depth || f.cancel || g->stop; });
+        if (f.cancel || g->stop) break;
+        if (!b.empty()) f.q.push_back(std::move(b));
+        g->cv.notify_all();
+    }
+    for (auto& b : pieces)
+        if (b.capacity()) buf_cache().give(std::move(b));
+    return true;
+}
+
 // the libdeflate fast path: true when the whole file was decoded and queued (or the scan cancelled
 // it); false leaves nothing queued and the zlib stream takes the file from its start
 bool inflate_whole(fr_gz* g, GzFile& f) {
@@ -337,6 +407,7 @@ bool inflate_whole(fr_gz* g, GzFile& f) {
         }
         return true;
     }
+    if (n >= PGZ_MIN_IN && g->threads >= 2 && inflate_member_parallel(g, f, in)) return true;
     if (n > LD_MAX_IN || n < 18) return false;
     // the last member's ISIZE (decoded length mod 2^32): a file that will not fit LD_MAX_OUT streams
     const size_t hint = le32(&in[n - 4]);
@@ -1196,6 +1267,8 @@ void fr_gz_part_close(fr_gz_part* p) {
 extern "C" {
 
 void fr_gz_trim(void) { buf_cache().trim(); }
+
+uint64_t fr_gz_parallel_members(void) { return g_parallel_members.load(); }
 
 void fr_gz_close(fr_gz* g) {
     if (!g) return;

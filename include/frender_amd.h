@@ -223,6 +223,13 @@ void fr_gz_close(fr_gz* g);
  * (no page faults per GB).  fr_gz_trim returns every cached buffer to the OS (long-lived processes that
  * scan once, e.g. the seam, call it after a scan). */
 void fr_gz_trim(void);
+/* Large single-member gzip files (the usual .fastq.gz of one lane) are not one thread's work: a member of
+ * at least 16 MiB compressed is decoded by all of the pool's idle threads at once (chunks of the
+ * compressed stream decoded from candidate block starts with their unknown 32 KiB windows as markers,
+ * stitched and resolved in order, checked against the member's CRC-32 and ISIZE; any failure decodes the
+ * file with one thread instead, whose decoders own the error behaviour).  The number of files decoded
+ * that way in this process (diagnostics, tests). */
+uint64_t fr_gz_parallel_members(void);
 
 /* The whole current file is already resident in HBM (bench / device producers). */
 int fr_feed_device(fr_ctx* ctx, const uint8_t* dev_data, uint64_t len);

@@ -131,3 +131,69 @@ def test_gz_trim_releases_the_cache(tmp_path):
     assert decoded([p], 1) == [t]
     _lib.gz_trim()
     assert decoded([p], 2) == [t]
+
+
+@pytest.fixture(scope="module")
+def big_text():
+    """~90 MB of SYN-v1 FASTQ (1.2M records at R=8 plus R=40 ones): single members of > 16 MiB compressed."""
+    from frender_amd import synth
+
+    sheet = synth.make_sheet(96, 8, 8)
+    return synth.generate_bytes(sheet, 0, 1_000_000, R=8, seed=31) + synth.generate_bytes(sheet, 0, 250_000, R=40,
+                                                                                           seed=32)
+
+
+def _gzip_member(text, level, name=None):
+    co = zlib.compressobj(level, zlib.DEFLATED, -15)
+    body = co.compress(text) + co.flush()
+    flg = 8 if name else 0
+    head = b"\x1f\x8b\x08" + bytes([flg]) + b"\0\0\0\0\0\xff" + ((name + b"\0") if name else b"")
+    return head + body + struct.pack("<II", zlib.crc32(text), len(text) & 0xFFFFFFFF)
+
+
+@pytest.mark.parametrize("level,name,pad", [(1, None, 0), (6, b"lane1.fastq", 7)])
+def test_parallel_single_member(tmp_path, big_text, level, name, pad):
+    """One big member (>= 16 MiB compressed: the parallel decoder, fr_pinflate.h) equals Python's gzip for
+    levels 1 and 6, with an FNAME header field and NUL padding after the member; the pool's threads decode
+    it together (fr_gz_parallel_members counts it)."""
+    blob = _gzip_member(big_text, level, name) + b"\0" * pad
+    assert len(blob) >= 16 << 20
+    p = str(tmp_path / "big.fq.gz")
+    with open(p, "wb") as f:
+        f.write(blob)
+    before = _lib.gz_parallel_members()
+    assert decoded([p], 6) == [gzip.decompress(blob)]
+    assert _lib.gz_parallel_members() == before + 1
+
+
+@pytest.mark.parametrize("damage", ["flip", "crc", "isize", "truncate", "trailing", "second_member"])
+def test_parallel_single_member_errors(tmp_path, big_text, damage):
+    """A damaged big member never yields bytes Python's gzip would not: the parallel decoder refuses it and
+    the one-thread decoders take the file (the same error, or the same bytes for a valid multi-member file)."""
+    blob = bytearray(_gzip_member(big_text, 1))
+    if damage == "flip":
+        blob[len(blob) // 2] ^= 0x5A
+    elif damage == "crc":
+        blob[-8] ^= 1
+    elif damage == "isize":
+        blob[-1] ^= 1
+    elif damage == "truncate":
+        blob = blob[: len(blob) - 1000]
+    elif damage == "trailing":
+        blob += b"garbage!"
+    else:
+        blob += gzip.compress(b"@x 1:N:0:ACGT+TTTT\nA\n+\nF\n")
+    p = str(tmp_path / "bad.fq.gz")
+    with open(p, "wb") as f:
+        f.write(bytes(blob))
+    try:
+        exp = gzip.decompress(bytes(blob))
+    except Exception:  # noqa: BLE001 - Python's gzip rejects it
+        exp = None
+    before = _lib.gz_parallel_members()
+    if exp is None:
+        with pytest.raises(_lib.GzError):
+            decoded([p], 6)
+    else:
+        assert decoded([p], 6) == [exp]
+    assert _lib.gz_parallel_members() == before  # never the parallel decoder's output

@@ -46,6 +46,9 @@ def parse():
     ap.add_argument("--nsubs", type=int, default=1)
     ap.add_argument("--launch-gib", type=int, default=16, help="largest tally launch of a device feed (GiB)")
     ap.add_argument("--rc", action="store_true")
+    ap.add_argument("--files", type=int, default=1,
+                    help="feed each GPU's records as this many consecutive files (per-file presence scans and the "
+                         "presence map in the timed step; the headline is one file, BASELINE config 2's one stream)")
     ap.add_argument("--combinatorial", action="store_true", help="12x8 combinatorial sheet (config 4 shape)")
     ap.add_argument("--cpu-reads", type=int, default=24_000_000, help="bounded sample for the CPU baseline (~10-20 s on 8 cores)")
     ap.add_argument("--cpu-cores", type=int, default=8)
@@ -89,7 +92,7 @@ def config_name(args) -> str:
         return "BASELINE config 3 shape (384 samples, 10+10, -rc)"
     if (std and args.reads == 100_000_000 and args.samples == 96 and args.index_len == 8 and args.nsubs == 1
             and not args.rc and not args.combinatorial):
-        return "BASELINE config 2"
+        return "BASELINE config 2" + (f" as {args.files} files" if args.files > 1 else "")
     return "custom shape"
 
 
@@ -407,7 +410,7 @@ PIN_FILES = {"BASELINE config 2": "cfg2_pin.json", "BASELINE config 3 shape (384
 def pin_path(args):
     if args.pin_json:
         return args.pin_json
-    f = PIN_FILES.get(config_name(args))
+    f = PIN_FILES.get(config_name(args).split(" as ")[0])  # K files hold the same rows in the same order
     return os.path.join(ROOT, "tests", "golden", f) if f else None
 
 
@@ -504,6 +507,8 @@ def main():
     wire = "cpu" if args.dist_backend == "gloo" else "cuda"  # where small collectives' tensors live
     idx2rc = [reverse_complement(x) for x in sheet.idx2]
 
+    # --files K: record cuts at multiples of 8 records (device feeds start 16-byte aligned: 8 x 74 B = 37 x 16 B)
+    cuts = [(n * i // max(args.files, 1)) // 8 * 8 for i in range(max(args.files, 1))] + [n]
     tally_timing = []
     timing_on = [False]  # the step whose tally launches are timed (the last timed one) reads them back
 
@@ -511,10 +516,17 @@ def main():
         ctx.reset()
         # rank r's records are the byte range [r n reclen, (r+1) n reclen) of one logical file:
         # global ordinals, so the merged first-occurrence order is the single-GPU one
-        ctx.begin_file(None, file_index=0, byte_base=rank * nbytes)
-        ctx.feed_device(buf, nbytes)
-        st = ctx.end_file()
-        assert st.records == n and st.error == 0, (st.records, st.error)
+        if args.files <= 1:
+            ctx.begin_file(None, file_index=0, byte_base=rank * nbytes)
+            ctx.feed_device(buf, nbytes)
+            st = ctx.end_file()
+            assert st.records == n and st.error == 0, (st.records, st.error)
+        else:  # --files K: the same records as K consecutive files (per-file presence scans at each file's end)
+            for i in range(args.files):
+                ctx.begin_file(None, file_index=rank * args.files + i, byte_base=0)
+                ctx.feed_device(buf + cuts[i] * reclen, (cuts[i + 1] - cuts[i]) * reclen)
+                st = ctx.end_file()
+                assert st.records == cuts[i + 1] - cuts[i] and st.error == 0, (i, st.records, st.error)
         if timing_on[0] or not tally_timing:  # the tally launches of this step (the merge resets the context)
             tally_timing[:] = [ctx.timing()]
         U, _, _ = ctx.finalize()

@@ -264,6 +264,12 @@ static int read_state(fr_ctx* ctx) {  // exact snapshot (a host round trip only 
     return FR_OK;
 }
 
+// every slot range may hold keys (DevState::sub_used): after inserts that bypass the launch log's reduce
+static hipError_t mark_ranges_used(fr_ctx* ctx) {
+    ctx->st_fresh = false;
+    return hipMemsetAsync(&ctx->st->sub_used[0], 0xFF, sizeof(ctx->st->sub_used), ctx->stream);
+}
+
 // grow the table (x4) and/or re-insert overflow entries; stream-ordered between launches
 static int grow_table(fr_ctx* ctx, bool force_bigger) {
     int rc = read_state(ctx);
@@ -281,6 +287,7 @@ static int grow_table(fr_ctx* ctx, bool force_bigger) {
         t.slots = ns_slots;
         t.mask = ns - 1;
         CK(launch_rehash(t, ctx->st, ctx->tab.slots, ctx->nslots, ctx->stream));
+        CK(mark_ranges_used(ctx));
         CK(hipStreamSynchronize(ctx->stream));
         CK(hipFree(ctx->tab.slots));
         ctx->tab = t;
@@ -293,6 +300,7 @@ static int grow_table(fr_ctx* ctx, bool force_bigger) {
         ctx->tab.ovf = fresh;
         CK(hipMemsetAsync(&ctx->st->n_overflow, 0, sizeof(u64), ctx->stream));
         CK(launch_reinsert_overflow(ctx->tab, ctx->st, old, novf, ctx->stream));
+        CK(mark_ranges_used(ctx));
         ctx->st_fresh = false;
         CK(hipStreamSynchronize(ctx->stream));
         CK(hipFree(old));
@@ -1664,6 +1672,7 @@ int fr_merge_unique_device(fr_ctx* ctx, const void* dev_keys, const void* dev_co
     ctx->st_fresh = false;
     CK(launch_merge(ctx->tab, ctx->st, (const u64*)dev_keys, (const u64*)dev_counts, (const u64*)dev_first, n,
                     ctx->stream));
+    CK(mark_ranges_used(ctx));
     return grow_table(ctx, false);
 }
 

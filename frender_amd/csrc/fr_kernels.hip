@@ -283,7 +283,10 @@ __device__ __forceinline__ void lds_barrier() {
 }
 
 __device__ FR_COLD void direct_insert(ScanShared& sh, const ScanArgs& a, u64 key, u32 off) {
-    if (global_insert(a.tabv, a.st, key, 1, make_ord(a, sh.cbase + off), a.file_tag)) atomicAdd(&sh.created, 1u);
+    if (global_insert(a.tabv, a.st, key, 1, make_ord(a, sh.cbase + off), a.file_tag)) {
+        atomicAdd(&sh.created, 1u);
+        __hip_atomic_store(&a.st->direct_claimed, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 __device__ __forceinline__ void rare_push(ScanShared& sh, const ScanArgs& a, u32 p, u32 kind, u32 x, u32 y);
@@ -1187,7 +1190,10 @@ __device__ __attribute__((noinline)) void commit_buffers(ScanShared& sh, const S
                 if (cv[b]) apply_entry(a, rc[b], ck[b], 1u, co[b]);
         }
     }
-    if (made) atomicAdd(&sh.created, made);
+    if (made) {
+        atomicAdd(&sh.created, made);
+        __hip_atomic_store(&a.st->direct_claimed, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     // buffered exotic records and the first "no space" error
     const u32 ne = min(sh.nexo, (u32)EXO_BUF);
     for (u32 k = tid; k < ne; k += WG) {
@@ -2123,6 +2129,7 @@ __global__ __launch_bounds__(256) void log_split_kernel(Table t, DevState* st, c
         }
         __syncthreads();  // wcnt / sbase are reused by the next tile
     }
+    if (made) __hip_atomic_store(&st->direct_claimed, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     add_created(st, made);
 }
 
@@ -2145,6 +2152,11 @@ __global__ __launch_bounds__(256) void log_reduce_kernel(Table t, DevState* st, 
         cz = ClaimZone{zone_bits, (u64)blockIdx.x * rn, (u64)blockIdx.x * rn + GPROBE, (u64)(blockIdx.x + 1) * rn};
         for (u32 i = threadIdx.x; i < (u32)(rn / 32); i += 256) zone_bits[i] = 0;
     }
+    // a fresh range (nothing inserted into it since the reset, no claims outside the reduces this launch):
+    // its zone's slots are empty unless this workgroup's bitmap says otherwise
+    const bool fresh = cz.bits && !(ABLATE & 4096u) &&
+                       !__hip_atomic_load(&st->direct_claimed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) &&
+                       !((st->sub_used[blockIdx.x >> 5] >> (blockIdx.x & 31u)) & 1u);
     __syncthreads();
     const u32 n = min(st->log_scur[blockIdx.x], scap);
     const LogEntry* part = sub + (u64)blockIdx.x * scap;
@@ -2229,12 +2241,45 @@ __global__ __launch_bounds__(256) void log_reduce_kernel(Table t, DevState* st, 
             ord[b] = ord0 + (e.w >> AGG_CNT_BITS);
             tag[b] = file_tag;
         }
+        if (fresh) {  // codes homed in the zone: the first free bit from the home, then two plain stores
+#pragma unroll
+            for (int b = 0; b < FB; ++b) {
+                if (!v[b]) continue;
+                const u64 hm = table_home(key[b], t.mask);
+                if (hm < cz.lo || hm >= cz.hi) continue;
+                const u32 end = (u32)(cz.hi - cz.base);
+                u32 bit = (u32)(hm - cz.base);
+                for (; bit < end; ++bit) {
+                    const u32 m = 1u << (bit & 31u);
+                    if (!(atomicOr(&cz.bits[bit >> 5], m) & m)) break;
+                }
+                if (bit == end) continue;  // the zone is full from here: the probing path below
+                GSlot* sl = &t.slots[cz.base + bit];
+                *((uint4*)sl) = make_uint4((u32)key[b], (u32)(key[b] >> 32), cnt[b], 0u);
+                *((uint4*)sl + 1) = make_uint4((u32)ord[b], (u32)(ord[b] >> 32), tag[b], 0u);
+                made += 1;
+                v[b] = false;
+            }
+        }
         made += insert_rows<FB, true>(t, st, key, cnt, ord, tag, v, cz);
+    }
+    // this range (and, through probes past its end, the next one) may hold keys from now on
+    if (__syncthreads_or(made != 0) && threadIdx.x == 0) {
+        const u32 b0 = blockIdx.x, b1 = (blockIdx.x + 1u) % (u32)LOG_NSUB;
+        atomicOr(&st->sub_used[b0 >> 5], 1u << (b0 & 31u));
+        atomicOr(&st->sub_used[b1 >> 5], 1u << (b1 & 31u));
     }
     add_created(st, made);
     // every workgroup has read log_n and its cursor (the split pass read the region cursors before
     // this launch): the last one empties the log
     if (last_block(&st->log_red_done)) {
+        if (__hip_atomic_load(&st->direct_claimed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+            // claims outside the reduces' own ranges: any range may hold keys now
+            for (int i = threadIdx.x; i < LOG_NSUB / 32; i += 256)
+                __hip_atomic_store(&st->sub_used[i], ~0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __syncthreads();
+            if (threadIdx.x == 0) __hip_atomic_store(&st->direct_claimed, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         for (int i = threadIdx.x; i < LOG_NR; i += 256)
             __hip_atomic_store(&st->log_rcur[i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         for (int i = threadIdx.x; i < LOG_NSUB; i += 256)

@@ -166,12 +166,13 @@ def test_speculative_commit_replay(lib, log_min):
         c.close()
 
 
-@pytest.mark.parametrize("log_min", ["0", "60", "100000000"])
-def test_launch_log_commits(lib, log_min):
+@pytest.mark.parametrize("log_min,log_hot", [("0", 4), ("0", 1 << 30), ("60", 4), ("100000000", 4)])
+def test_launch_log_commits(lib, log_min, log_hot):
     """Commits of at least fr_tuning.log_min pairs go to the launch log and are aggregated after the launch
     (count / scatter / LDS reduce / round-based table inserts); smaller ones insert directly.  Every
     commit logged (0), a mix (60: these 2-wave-tile chunks commit ~30-110 pairs), and none must give the
-    oracle's tally, including a table that has to grow between launches."""
+    oracle's tally, including a table that has to grow between launches.  log_hot 2^30 logs the hot
+    codes too (no direct inserts: the reduce's fresh-range claims from its LDS bitmap alone)."""
     from frender_amd import synth
     rng = random.Random(int(log_min) + 7)
     sheet = synth.make_sheet(384, 10, 10)
@@ -179,7 +180,8 @@ def test_launch_log_commits(lib, log_min):
              synth.generate_bytes(sheet, 300000, 5000, R=8, seed=3)]
     exp = oracle_tally(files)
     for mode, slots in (("device", 1 << 12), ("host", 1 << 20)):
-        c = lib.Context(device=0, chunk_bytes=1 << 22, table_slots=slots, tuning={"log_min": int(log_min)})
+        c = lib.Context(device=0, chunk_bytes=1 << 22, table_slots=slots,
+                        tuning={"log_min": int(log_min), "log_hot": log_hot})
         try:
             assert_same(gpu_tally(c, lib, files, mode=mode, pieces=lambda r: r.choice([4096, 1 << 20, 1 << 23]),
                                   rng=rng), exp)
@@ -965,8 +967,8 @@ def test_timing_events_off_same_table(lib):
     assert out[0] == out[1]
 
 
-@pytest.mark.parametrize("launch_gib", [4, 16])
-def test_bench_geometry_pinned_to_reference(lib, launch_gib):
+@pytest.mark.parametrize("launch_gib,tuning", [(4, None), (16, None), (16, {"log_min": 0, "log_hot": 1 << 30})])
+def test_bench_geometry_pinned_to_reference(lib, launch_gib, tuning):
     """bench.py's exact workload and launch geometry (BASELINE config 2: 100M SYN-v1 records in HBM,
     one device feed cut into two 3.7 GB launches of the 1024-workgroup ramped grid -- or, with 16-GiB
     launches, two for the first feed and ONE 7.4 GB launch for the next (chunk offsets past 4 GiB, no
@@ -985,7 +987,7 @@ def test_bench_geometry_pinned_to_reference(lib, launch_gib):
     n = pin["reads"]
     sheet = synth.make_sheet(96, 8, 8)
     reclen = synth.record_length(8, 8, 8)
-    c = lib.Context(device=0, chunk_bytes=(launch_gib << 30) - (1 << 20), table_slots=1 << 22)
+    c = lib.Context(device=0, chunk_bytes=(launch_gib << 30) - (1 << 20), table_slots=1 << 22, tuning=tuning)
     buf = c.device_alloc(n * reclen + 64)
     try:
         c.synth_device(buf, 0, n, 8, 1, sheet.idx1, sheet.idx2)

@@ -53,6 +53,7 @@ def parse():
     ap.add_argument("--cpu-reads", type=int, default=24_000_000, help="bounded sample for the CPU baseline (~10-20 s on 8 cores)")
     ap.add_argument("--cpu-cores", type=int, default=8)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-pin", action="store_true", help="skip the reference-pin check (ablation builds only)")
     ap.add_argument("--no-single", action="store_true",
                     help="skip e2e.single_member (the cpu_baseline's records as one single-member .fastq.gz)")
     ap.add_argument("--merge", choices=["a2a", "tree"], default="a2a",
@@ -601,7 +602,7 @@ def main():
     csum &= (1 << 64) - 1
     pinned = None
     pp = pin_path(args)
-    if world == 1 and pp and os.path.exists(pp):
+    if world == 1 and pp and os.path.exists(pp) and not args.no_pin:
         pinned = pin_check(args, ctx, sheet)
     if rank == 0:
         cpu = None if (args.no_cpu or world > 1) else cpu_baseline(args, ctx, sheet, reclen)  # N=1 only

@@ -98,6 +98,10 @@ struct fr_ctx {
     u64 chunk_bytes = 0;
     u64 ring_bytes = 0;
     u64 feed_keys = ~0ull;    // codes the last device feed created (a range over RANGE_FIRST_MAX needs table room for them)
+    bool feed_logged = true;  // the last device feed's commits went to the launch log: its ranges stay <= RANGE_FIRST_MAX
+                              // (one aggregation over a bigger range has more distinct codes per sub-region than
+                              // log_reduce_kernel's LDS fold holds: measured 15 ms instead of 0.28 per launch at the
+                              // config-3 shape)
     u32 chunk_tiles = 320;  // wave-tiles (4 KiB) per full chunk of a ramped launch (FR_CHUNK_TILES; round 2's
                             // 80 workgroup tiles of 16 KiB: 64-96 measured within 2 %, 80 best)
     // Ramped launches after one in which at least a quarter of the chunks since the reset logged their
@@ -264,12 +268,6 @@ static int read_state(fr_ctx* ctx) {  // exact snapshot (a host round trip only 
     return FR_OK;
 }
 
-// every slot range may hold keys (DevState::sub_used): after inserts that bypass the launch log's reduce
-static hipError_t mark_ranges_used(fr_ctx* ctx) {
-    ctx->st_fresh = false;
-    return hipMemsetAsync(&ctx->st->sub_used[0], 0xFF, sizeof(ctx->st->sub_used), ctx->stream);
-}
-
 // grow the table (x4) and/or re-insert overflow entries; stream-ordered between launches
 static int grow_table(fr_ctx* ctx, bool force_bigger) {
     int rc = read_state(ctx);
@@ -287,7 +285,6 @@ static int grow_table(fr_ctx* ctx, bool force_bigger) {
         t.slots = ns_slots;
         t.mask = ns - 1;
         CK(launch_rehash(t, ctx->st, ctx->tab.slots, ctx->nslots, ctx->stream));
-        CK(mark_ranges_used(ctx));
         CK(hipStreamSynchronize(ctx->stream));
         CK(hipFree(ctx->tab.slots));
         ctx->tab = t;
@@ -300,7 +297,6 @@ static int grow_table(fr_ctx* ctx, bool force_bigger) {
         ctx->tab.ovf = fresh;
         CK(hipMemsetAsync(&ctx->st->n_overflow, 0, sizeof(u64), ctx->stream));
         CK(launch_reinsert_overflow(ctx->tab, ctx->st, old, novf, ctx->stream));
-        CK(mark_ranges_used(ctx));
         ctx->st_fresh = false;
         CK(hipStreamSynchronize(ctx->stream));
         CK(hipFree(old));
@@ -601,7 +597,10 @@ static int launch_range(fr_ctx* ctx, const u8* dptr, u64 len, u64 avail, int own
     }
     a.cold_cap = ctx->cold_cap;
     a.cold = ctx->cold;
-    a.log = exo_only ? nullptr : ctx->log;  // log entries carry 34-bit launch offsets: any range may log
+    // launch-log offsets fold as u32 in log_reduce_kernel, and one aggregation's distinct codes must fit its
+    // LDS fold: a range over RANGE_FIRST_MAX runs without the log (fr_feed_device takes one only after a feed
+    // that did not log)
+    a.log = (exo_only || len > RANGE_FIRST_MAX) ? nullptr : ctx->log;
     a.log_cap = ctx->log_cap;
     a.log_rcap = ctx->log_rcap;
     a.log_min = ctx->log_min;
@@ -705,7 +704,8 @@ fr_ctx* fr_create_tuned(int device, uint64_t chunk_bytes, uint64_t table_slots, 
     if (t.log) {
         // entries: 1 per 256 B of a launch (SYN-v1 config 3 logs ~1 per 700 B), in LOG_NR equal regions;
         // a run past its region's end inserts directly
-        const u64 want = std::min<u64>(std::max<u64>(ctx->chunk_bytes / 256, 1ull << 16), 1ull << 26);
+        const u64 want = std::min<u64>(std::max<u64>(std::min<u64>(ctx->chunk_bytes, RANGE_FIRST_MAX) / 256, 1ull << 16),
+                                       1ull << 26);  // logged ranges are <= RANGE_FIRST_MAX
         ctx->log_rcap = (u32)(want / LOG_NR);
         ctx->log_cap = (u64)ctx->log_rcap * LOG_NR;
         ctx->log_scap = (u32)std::max<u64>(2ull * ctx->log_rcap / LOG_SUBS, 64);  // 2x the mean share
@@ -1087,15 +1087,16 @@ int fr_feed_device(fr_ctx* ctx, const uint8_t* dev_data, uint64_t len) {
         CK(dalloc(&snap, snap_slots));
         CK(hipMemcpyAsync(snap, ctx->tab.slots, snap_slots * sizeof(GSlot), hipMemcpyDeviceToDevice, ctx->stream));
     }
-    // Equal ranges of at most chunk_bytes: one launch (one set of ramps and tail, one launch-log aggregation)
-    // for the bench's 7.4 GB, DESIGN.md §4.1.  The table grows between launches, never inside one, so a range
-    // over RANGE_FIRST_MAX is taken only for speculative feeds whose table holds the last feed's new codes
-    // again at load <= 1/2.  The decision rests on the previous feed (fr_reset keeps it: a bench or a seam scanning the same
+    // Equal ranges of at most chunk_bytes: one launch (one set of ramps and tail) for the bench's 7.4 GB,
+    // DESIGN.md §4.1.  The table grows between launches, never inside one, so a range over RANGE_FIRST_MAX is
+    // taken only for speculative feeds whose table holds the last feed's new codes again at load <= 1/2, and
+    // whose last feed did not log (feed_logged).  The decision rests on the previous feed (fr_reset keeps it: a bench or a seam scanning the same
     // kind of data again).  A feed whose new codes outgrow the table inside one launch -- past the free
     // slots and the overflow list -- is rolled back like a wrong speculation and replayed in ranges of an
     // eighth of the size, with the table grown between them (each launch's state read before the next),
     // down to RANGE_ROOM_MIN (speculative feeds: the rollback needs the snapshot).
-    bool big = spec && ctx->feed_keys != ~0ull && (saved.n_keys + ctx->feed_keys) * 2 <= ctx->nslots;
+    bool big = spec && !ctx->feed_logged && ctx->feed_keys != ~0ull &&
+               (saved.n_keys + ctx->feed_keys) * 2 <= ctx->nslots;
     bool spec_now = spec;
     u64 step = 0, lim_room = ~0ull;
     for (int attempt = 0; attempt < 12; ++attempt) {
@@ -1155,6 +1156,7 @@ int fr_feed_device(fr_ctx* ctx, const uint8_t* dev_data, uint64_t len) {
     }
     if (rc) return rc;
     ctx->feed_keys = ctx->h_st->n_keys - saved.n_keys;
+    ctx->feed_logged = ctx->h_st->log_commits != saved.log_commits;  // read_state above: exact
     // exotic records overflowed the list: grow it to the counted totals and run the feed's launches
     // again capturing exotic records only (the table is already complete), then drain
     rc = read_state(ctx);
@@ -1672,7 +1674,6 @@ int fr_merge_unique_device(fr_ctx* ctx, const void* dev_keys, const void* dev_co
     ctx->st_fresh = false;
     CK(launch_merge(ctx->tab, ctx->st, (const u64*)dev_keys, (const u64*)dev_counts, (const u64*)dev_first, n,
                     ctx->stream));
-    CK(mark_ranges_used(ctx));
     return grow_table(ctx, false);
 }
 

@@ -144,14 +144,6 @@ struct DevState {
     u32 log_rcur[LOG_NR];  // per launch-log region: entries claimed this launch (the aggregation zeroes them)
     u32 log_scur[LOG_NSUB];  // per sub-region: entries the split pass placed (the aggregation zeroes them)
     u32 log_red_done;    // aggregation workgroups finished (the last zeroes it)
-    // Fresh slot ranges (log_reduce_kernel): bit s of sub_used set = sub-region s's home range may hold a key
-    // (fr_reset zeroes it; the host sets every bit after a rehash, a re-insert or a merge).  Any slot
-    // claimed outside a reduce's own range during a launch (the tally's direct inserts, the split pass's
-    // overflow) sets direct_claimed, and the aggregation then counts every range as used.  A reduce
-    // workgroup whose range is fresh claims slots in its claim zone from its LDS bitmap alone: no probe
-    // loads from HBM.
-    u32 sub_used[LOG_NSUB / 32];
-    u32 direct_claimed;
 };
 
 struct Table {

@@ -283,10 +283,7 @@ __device__ __forceinline__ void lds_barrier() {
 }
 
 __device__ FR_COLD void direct_insert(ScanShared& sh, const ScanArgs& a, u64 key, u32 off) {
-    if (global_insert(a.tabv, a.st, key, 1, make_ord(a, sh.cbase + off), a.file_tag)) {
-        atomicAdd(&sh.created, 1u);
-        __hip_atomic_store(&a.st->direct_claimed, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (global_insert(a.tabv, a.st, key, 1, make_ord(a, sh.cbase + off), a.file_tag)) atomicAdd(&sh.created, 1u);
 }
 
 __device__ __forceinline__ void rare_push(ScanShared& sh, const ScanArgs& a, u32 p, u32 kind, u32 x, u32 y);
@@ -1190,10 +1187,7 @@ __device__ __attribute__((noinline)) void commit_buffers(ScanShared& sh, const S
                 if (cv[b]) apply_entry(a, rc[b], ck[b], 1u, co[b]);
         }
     }
-    if (made) {
-        atomicAdd(&sh.created, made);
-        __hip_atomic_store(&a.st->direct_claimed, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (made) atomicAdd(&sh.created, made);
     // buffered exotic records and the first "no space" error
     const u32 ne = min(sh.nexo, (u32)EXO_BUF);
     for (u32 k = tid; k < ne; k += WG) {
@@ -1913,15 +1907,9 @@ __device__ __forceinline__ bool last_block(u32* ctr) {
 constexpr int AGG_LNS = 4096;  // LDS slots of one sub-region's aggregation (64 KB: 2 workgroups per CU)
 constexpr int AGG_PROBE = 64;
 constexpr int CLAIM_WORDS = 2048;  // a reduce workgroup's claim bitmap: sub-regions of up to 64K slots (8 KB)
-// One folded code: w = min launch offset << AGG_CNT_BITS | records, updated with one 64-bit LDS CAS (offsets of
-// ranges up to RANGE_MAX need 34 bits: the min and the sum share the word so the slot stays 16 bytes)
-constexpr int AGG_CNT_BITS = 30;
-constexpr u64 AGG_CNT_MAX = (1ull << AGG_CNT_BITS) - 1ull;
-constexpr u64 AGG_W0 = ~0ull << AGG_CNT_BITS;  // empty: offset all ones, no records
-static_assert(RANGE_MAX < (1ull << (64 - AGG_CNT_BITS)), "fold offsets");
 struct alignas(16) AggSlot {
     u64 key;
-    u64 w;
+    u32 mino, cnt;  // min launch offset (logged launches are <= RANGE_FIRST_MAX: u32), records
 };
 
 // distinct (key, count, first, last tag) rows into the HBM table in rounds: every pending row's probe
@@ -2129,7 +2117,6 @@ __global__ __launch_bounds__(256) void log_split_kernel(Table t, DevState* st, c
         }
         __syncthreads();  // wcnt / sbase are reused by the next tile
     }
-    if (made) __hip_atomic_store(&st->direct_claimed, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     add_created(st, made);
 }
 
@@ -2143,7 +2130,7 @@ __global__ __launch_bounds__(256) void log_reduce_kernel(Table t, DevState* st, 
     __shared__ AggSlot ls[AGG_LNS];
     __shared__ u32 zone_bits[CLAIM_WORDS];
     u32 made = 0;
-    for (int i = threadIdx.x; i < AGG_LNS; i += 256) ls[i] = AggSlot{0, AGG_W0};
+    for (int i = threadIdx.x; i < AGG_LNS; i += 256) ls[i] = AggSlot{0, 0xFFFFFFFFu, 0};
     // this sub-region's home range: slots [blockIdx.x n, (blockIdx.x + 1) n) of the table (table_home's top
     // bits are the region and sub-region bits); its claim zone skips the first GPROBE slots
     const u64 nslots = t.mask + 1ull, rn = nslots >= (u64)LOG_NSUB ? nslots / LOG_NSUB : 0ull;
@@ -2152,11 +2139,6 @@ __global__ __launch_bounds__(256) void log_reduce_kernel(Table t, DevState* st, 
         cz = ClaimZone{zone_bits, (u64)blockIdx.x * rn, (u64)blockIdx.x * rn + GPROBE, (u64)(blockIdx.x + 1) * rn};
         for (u32 i = threadIdx.x; i < (u32)(rn / 32); i += 256) zone_bits[i] = 0;
     }
-    // a fresh range (nothing inserted into it since the reset, no claims outside the reduces this launch):
-    // its zone's slots are empty unless this workgroup's bitmap says otherwise
-    const bool fresh = cz.bits && !(ABLATE & 4096u) &&
-                       !__hip_atomic_load(&st->direct_claimed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) &&
-                       !((st->sub_used[blockIdx.x >> 5] >> (blockIdx.x & 31u)) & 1u);
     __syncthreads();
     const u32 n = min(st->log_scur[blockIdx.x], scap);
     const LogEntry* part = sub + (u64)blockIdx.x * scap;
@@ -2182,7 +2164,7 @@ __global__ __launch_bounds__(256) void log_reduce_kernel(Table t, DevState* st, 
                 sink ^= e.key;
                 continue;
             }
-            const u64 eoff = log_off(e.oc);
+            const u32 eoff = (u32)log_off(e.oc);  // (a logged launch is < 4 GiB)
             const u32 ecnt = log_cnt(e.oc);
             u32 h = (u32)mix64(e.key) & (AGG_LNS - 1);
             bool done = false;
@@ -2193,26 +2175,14 @@ __global__ __launch_bounds__(256) void log_reduce_kernel(Table t, DevState* st, 
                     k = old == 0 ? e.key : old;
                 }
                 if (k == e.key) {
-                    // min offset and record sum in one word: CAS until it holds (a sum that would pass
-                    // AGG_CNT_MAX leaves the slot alone and the row inserts on its own below)
-                    u64 cur = *(volatile u64*)&ls[h].w;
-                    for (;;) {
-                        const u64 c = (cur & AGG_CNT_MAX) + ecnt;
-                        if (c > AGG_CNT_MAX) break;
-                        const u64 nw = (min(cur >> AGG_CNT_BITS, eoff) << AGG_CNT_BITS) | c;
-                        const u64 old = atomicCAS((unsigned long long*)&ls[h].w, (unsigned long long)cur,
-                                                  (unsigned long long)nw);
-                        if (old == cur) {
-                            done = true;
-                            break;
-                        }
-                        cur = old;
-                    }
+                    atomicAdd(&ls[h].cnt, ecnt);  // (fire-and-forget LDS atomics: no wait in the fold's chain)
+                    if (eoff < ls[h].mino) atomicMin(&ls[h].mino, eoff);
+                    done = true;
                     break;
                 }
                 h = (h + 1) & (AGG_LNS - 1);
             }
-            if (!done) {  // a full LDS table (or a saturated slot): this row goes in on its own
+            if (!done) {  // a full LDS table: this row goes in on its own
                 const u64 key1[1] = {e.key};
                 const u32 cnt1[1] = {ecnt};
                 const u64 ord1[1] = {ord0 + eoff};
@@ -2234,52 +2204,19 @@ __global__ __launch_bounds__(256) void log_reduce_kernel(Table t, DevState* st, 
 #pragma unroll
         for (int b = 0; b < FB; ++b) {
             const int i = i0 + b * 256;
-            const AggSlot e = i < AGG_LNS ? ls[i] : AggSlot{0, AGG_W0};
-            v[b] = e.key != 0 && (e.w & AGG_CNT_MAX) != 0;
+            const AggSlot e = i < AGG_LNS ? ls[i] : AggSlot{0, 0xFFFFFFFFu, 0};
+            v[b] = e.key != 0;
             key[b] = e.key;
-            cnt[b] = (u32)(e.w & AGG_CNT_MAX);
-            ord[b] = ord0 + (e.w >> AGG_CNT_BITS);
+            cnt[b] = e.cnt;
+            ord[b] = ord0 + e.mino;
             tag[b] = file_tag;
         }
-        if (fresh) {  // codes homed in the zone: the first free bit from the home, then two plain stores
-#pragma unroll
-            for (int b = 0; b < FB; ++b) {
-                if (!v[b]) continue;
-                const u64 hm = table_home(key[b], t.mask);
-                if (hm < cz.lo || hm >= cz.hi) continue;
-                const u32 end = (u32)(cz.hi - cz.base);
-                u32 bit = (u32)(hm - cz.base);
-                for (; bit < end; ++bit) {
-                    const u32 m = 1u << (bit & 31u);
-                    if (!(atomicOr(&cz.bits[bit >> 5], m) & m)) break;
-                }
-                if (bit == end) continue;  // the zone is full from here: the probing path below
-                GSlot* sl = &t.slots[cz.base + bit];
-                *((uint4*)sl) = make_uint4((u32)key[b], (u32)(key[b] >> 32), cnt[b], 0u);
-                *((uint4*)sl + 1) = make_uint4((u32)ord[b], (u32)(ord[b] >> 32), tag[b], 0u);
-                made += 1;
-                v[b] = false;
-            }
-        }
         made += insert_rows<FB, true>(t, st, key, cnt, ord, tag, v, cz);
-    }
-    // this range (and, through probes past its end, the next one) may hold keys from now on
-    if (__syncthreads_or(made != 0) && threadIdx.x == 0) {
-        const u32 b0 = blockIdx.x, b1 = (blockIdx.x + 1u) % (u32)LOG_NSUB;
-        atomicOr(&st->sub_used[b0 >> 5], 1u << (b0 & 31u));
-        atomicOr(&st->sub_used[b1 >> 5], 1u << (b1 & 31u));
     }
     add_created(st, made);
     // every workgroup has read log_n and its cursor (the split pass read the region cursors before
     // this launch): the last one empties the log
     if (last_block(&st->log_red_done)) {
-        if (__hip_atomic_load(&st->direct_claimed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-            // claims outside the reduces' own ranges: any range may hold keys now
-            for (int i = threadIdx.x; i < LOG_NSUB / 32; i += 256)
-                __hip_atomic_store(&st->sub_used[i], ~0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __syncthreads();
-            if (threadIdx.x == 0) __hip_atomic_store(&st->direct_claimed, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
         for (int i = threadIdx.x; i < LOG_NR; i += 256)
             __hip_atomic_store(&st->log_rcur[i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         for (int i = threadIdx.x; i < LOG_NSUB; i += 256)

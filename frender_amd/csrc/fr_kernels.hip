@@ -1906,7 +1906,7 @@ __device__ __forceinline__ bool last_block(u32* ctr) {
 
 constexpr int AGG_LNS = 4096;  // LDS slots of one sub-region's aggregation (64 KB: 2 workgroups per CU)
 constexpr int AGG_PROBE = 64;
-constexpr int CLAIM_WORDS = 2048;  // a reduce workgroup's claim bitmap: sub-regions of up to 64K slots (8 KB)
+constexpr int CLAIM_WORDS = 1024;  // a reduce workgroup's claim bitmap: sub-regions of up to 32K slots (4 KB; tables of up to 16 Mi slots)
 struct alignas(16) AggSlot {
     u64 key;
     u32 mino, cnt;  // min launch offset (logged launches are <= RANGE_FIRST_MAX: u32), records
@@ -2129,6 +2129,8 @@ __global__ __launch_bounds__(256) void log_reduce_kernel(Table t, DevState* st, 
     if (st->log_n == 0) return;
     __shared__ AggSlot ls[AGG_LNS];
     __shared__ u32 zone_bits[CLAIM_WORDS];
+    __shared__ u16 occ[AGG_LNS];  // the occupied slots of ls, listed for the inserts
+    __shared__ u32 occ_n;
     u32 made = 0;
     for (int i = threadIdx.x; i < AGG_LNS; i += 256) ls[i] = AggSlot{0, 0xFFFFFFFFu, 0};
     // this sub-region's home range: slots [blockIdx.x n, (blockIdx.x + 1) n) of the table (table_home's top
@@ -2194,18 +2196,25 @@ __global__ __launch_bounds__(256) void log_reduce_kernel(Table t, DevState* st, 
     }
     if (sink == 1) atomicAdd((unsigned long long*)&st->stamp[7], 1ull);  // keeps the ablation's loads
     __syncthreads();
-    // the distinct codes into the table, FB slots per thread in flight (LDS limits this kernel to two
-    // workgroups per CU, so registers are plentiful)
+    // the distinct codes into the table: the occupied slots listed first (LDS), then FB of them per thread in
+    // flight -- one batch of probe loads covers 256 * FB codes, instead of one batch per FB slots scanned
+    // (half of them empty at the fold's usual load)
+    if (threadIdx.x == 0) occ_n = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < AGG_LNS; i += 256)
+        if (ls[i].key) occ[atomicAdd(&occ_n, 1u)] = (u16)i;
+    __syncthreads();
     constexpr int FB = 8;
-    for (int i0 = threadIdx.x; i0 < ((ABLATE & 256u) ? 0 : AGG_LNS); i0 += FB * 256) {  // 256: timing ablation
+    const u32 nocc = (ABLATE & 256u) ? 0u : occ_n;  // 256: timing ablation
+    for (u32 i0 = threadIdx.x; i0 < nocc; i0 += FB * 256) {
         u64 key[FB], ord[FB];
         u32 cnt[FB], tag[FB];
         bool v[FB];
 #pragma unroll
         for (int b = 0; b < FB; ++b) {
-            const int i = i0 + b * 256;
-            const AggSlot e = i < AGG_LNS ? ls[i] : AggSlot{0, 0xFFFFFFFFu, 0};
-            v[b] = e.key != 0;
+            const u32 j = i0 + b * 256;
+            v[b] = j < nocc;
+            const AggSlot e = v[b] ? ls[occ[j]] : AggSlot{0, 0, 0};
             key[b] = e.key;
             cnt[b] = e.cnt;
             ord[b] = ord0 + e.mino;

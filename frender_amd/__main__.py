@@ -46,7 +46,11 @@ def main(argv=None):
     d.add_argument("--strict-header", action="store_true",
                    help="reject a results file in scan's own column order, as frender.py does (default: accept it)")
     d.add_argument("--gz-level", type=int, default=9,
-                   help="gzip level of the outputs (the reference writes gzip.open's default, 9)")
+                   help="gzip level of the host writers (the reference writes gzip.open's default, 9)")
+    d.add_argument("--gz-writer", choices=("gpu", "libdeflate", "zlib"), default="gpu",
+                   help="who compresses the outputs: gpu (default: the routed bytes are deflated on the GPU, "
+                        "no larger than zlib level 9 makes them on FASTQ), libdeflate or zlib (host threads at "
+                        "--gz-level)")
     d.add_argument("--gpus", type=int, default=1,
                    help="GPUs (one process each; file pairs are dealt to them, rank 0 writes the outputs)")
     d.add_argument("files", nargs="+", help="Fastq file, list of fastq files, or directory path")

@@ -145,6 +145,15 @@ _SIGS = {
     "fr_dmx_patch": (C.c_int, [P, P, P, C.c_uint64]),
     "fr_dmx_route": (C.c_int, [P, C.c_int, C.c_uint64, C.POINTER(C.c_int64), C.POINTER(C.c_int32), P, P]),
     "fr_dmx_fetch": (C.c_int, [P, C.c_int, P, C.c_uint64]),
+    "fr_dmx_deflate": (C.c_int, [P, C.c_int, C.c_int, P, P]),
+    "fr_dmx_fetch_deflated": (C.c_int, [P, C.c_int, P, C.c_uint64]),
+    "fr_defl_create": (P, [C.c_int]),
+    "fr_defl_destroy": (None, [P]),
+    "fr_defl_last_error": (C.c_char_p, [P]),
+    "fr_defl_run": (C.c_int, [P, P, P, C.c_int, P, P]),
+    "fr_defl_run_host": (C.c_int, [P, P, C.c_uint64, P, C.c_int, P, P]),
+    "fr_defl_out_bytes": (C.c_uint64, [P]),
+    "fr_defl_fetch": (C.c_int, [P, P, C.c_uint64]),
 }
 for _name, (_res, _args) in _SIGS.items():
     _f = getattr(lib, _name)
@@ -453,6 +462,54 @@ class Demux:
         out = np.empty(nbytes, np.uint8)
         self._ck(lib.fr_dmx_fetch(self.h, mate, _ptr(out), nbytes), "fr_dmx_fetch")
         return out
+
+    def deflate(self, mate: int, n_dest: int) -> tuple:
+        """The routed bytes of a mate as one raw deflate stream per destination (fr_dmx_deflate):
+        (stream bytes per destination, CRC-32 per destination, the streams concatenated)."""
+        comp, crc = np.zeros(n_dest, np.uint64), np.zeros(n_dest, np.uint32)
+        self._ck(lib.fr_dmx_deflate(self.h, mate, n_dest, _ptr(comp), _ptr(crc)), "fr_dmx_deflate")
+        out = np.empty(int(comp.sum()), np.uint8)
+        self._ck(lib.fr_dmx_fetch_deflated(self.h, mate, _ptr(out), out.size), "fr_dmx_fetch_deflated")
+        return comp, crc, out
+
+
+class Deflater:
+    """GPU deflate over byte ranges (fr_defl): see include/frender_amd.h."""
+
+    def __init__(self, device: int = 0):
+        self.h = lib.fr_defl_create(device)
+        err = lib.fr_defl_last_error(self.h) if self.h else b"fr_defl_create returned NULL"
+        if err:
+            raise FrenderError(f"fr_defl_create: {err.decode()}")
+
+    def close(self):
+        if self.h:
+            lib.fr_defl_destroy(self.h)
+            self.h = None
+
+    def compress(self, data, offsets=None) -> tuple:
+        """Raw deflate streams of the ranges [offsets[s], offsets[s + 1]) of host bytes `data` (one
+        range when offsets is None): (stream bytes per range, CRC-32 per range, the streams)."""
+        a = np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+        a = np.ascontiguousarray(a, dtype=np.uint8)
+        offs = np.ascontiguousarray([0, a.size] if offsets is None else offsets, dtype=np.uint64)
+        n = offs.size - 1
+        comp, crc = np.zeros(n, np.uint64), np.zeros(n, np.uint32)
+        rc = lib.fr_defl_run_host(self.h, _ptr(a), a.size, _ptr(offs), n, _ptr(comp), _ptr(crc))
+        if rc != FR_OK:
+            raise FrenderError(f"fr_defl_run_host: {lib.fr_defl_last_error(self.h).decode()} (rc={rc})")
+        out = np.empty(int(lib.fr_defl_out_bytes(self.h)), np.uint8)
+        rc = lib.fr_defl_fetch(self.h, _ptr(out), out.size)
+        if rc != FR_OK:
+            raise FrenderError(f"fr_defl_fetch: {lib.fr_defl_last_error(self.h).decode()} (rc={rc})")
+        return comp, crc, out
+
+
+def gzip_frame(crc: int, isize: int) -> tuple:
+    """The header and trailer that make a raw deflate stream a gzip member (RFC 1952; XFL 2 and OS 255
+    as Python's gzip writes them at level 9, mtime 0)."""
+    import struct
+    return b"\x1f\x8b\x08\x00\x00\x00\x00\x00\x02\xff", struct.pack("<II", crc & 0xFFFFFFFF, isize & 0xFFFFFFFF)
 
 
 def _torch_stream_done(device: int):

@@ -326,6 +326,8 @@ int grid_for(u64 n, int per = 256, int cap = 8192) {
 
 using namespace fr;
 
+fr_defl* fr_defl_create_on(int device, hipStream_t stream);
+
 struct fr_dmx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -359,6 +361,8 @@ struct fr_dmx {
     u8* out[2] = {nullptr, nullptr};
     u64 out_cap[2] = {0, 0};
     u64 out_len[2] = {0, 0};
+    std::vector<u64> hoff[2];  // destination offsets of the routed bytes (host copy)
+    fr_defl* defl[2] = {nullptr, nullptr};  // the writers' compression (fr_deflate.hip), created on first use
 };
 
 #define DK(x)                                                                  \
@@ -401,6 +405,7 @@ void fr_dmx_destroy(fr_dmx* d) {
                  d->tmp, d->cnt, d->base, d->fe};
     for (void* x : p)
         if (x) (void)hipFree(x);
+    for (fr_defl* z : d->defl) fr_defl_destroy(z);
     if (d->stream) (void)hipStreamDestroy(d->stream);
     delete d;
 }
@@ -538,6 +543,8 @@ int fr_dmx_route(fr_dmx* d, int n_dest, uint64_t n_pairs, int64_t* first_error, 
     *error_val = 0;
     for (int k = 0; k < n_dest; ++k) bytes_r1[k] = bytes_r2[k] = 0;
     d->out_len[0] = d->out_len[1] = 0;
+    d->hoff[0].assign((size_t)std::max(n_dest, 0) + 1, 0);
+    d->hoff[1].assign((size_t)std::max(n_dest, 0) + 1, 0);
     if (!P) return FR_OK;
     DK(ensure(&d->fe, d->c_fe, 1));
     unsigned long long* fe = d->fe;
@@ -608,7 +615,31 @@ int fr_dmx_route(fr_dmx* d, int n_dest, uint64_t n_pairs, int64_t* first_error, 
     DK(hipStreamSynchronize(d->stream));
     d->out_len[0] = s1;
     d->out_len[1] = s2;
+    d->hoff[0] = h1;
+    d->hoff[1] = h2;
     return FR_OK;
+}
+
+int fr_dmx_deflate(fr_dmx* d, int mate, int n_dest, uint64_t* comp_bytes, uint32_t* crc32) {
+    if (mate < 0 || mate > 1) return d->err = "mate must be 0 (R1) or 1 (R2)", FR_ERR_INVALID;
+    if (n_dest < 0 || (u64)n_dest + 1 != d->hoff[mate].size())
+        return d->err = "fr_dmx_deflate: n_dest differs from the last fr_dmx_route", FR_ERR_INVALID;
+    DK(hipSetDevice(d->device));
+    if (!d->defl[mate]) {
+        d->defl[mate] = fr_defl_create_on(d->device, d->stream);
+        const char* e = fr_defl_last_error(d->defl[mate]);
+        if (e && *e) return d->err = std::string("fr_dmx_deflate: ") + e, FR_ERR_HIP;
+    }
+    const int rc = fr_defl_run(d->defl[mate], d->out[mate], d->hoff[mate].data(), n_dest, comp_bytes, crc32);
+    if (rc != FR_OK) d->err = std::string("fr_dmx_deflate: ") + fr_defl_last_error(d->defl[mate]);
+    return rc;
+}
+
+int fr_dmx_fetch_deflated(fr_dmx* d, int mate, uint8_t* out, uint64_t len) {
+    if (mate < 0 || mate > 1 || !d->defl[mate]) return d->err = "fr_dmx_fetch_deflated: bad mate or no fr_dmx_deflate", FR_ERR_INVALID;
+    const int rc = fr_defl_fetch(d->defl[mate], out, len);
+    if (rc != FR_OK) d->err = std::string("fr_dmx_fetch_deflated: ") + fr_defl_last_error(d->defl[mate]);
+    return rc;
 }
 
 int fr_dmx_fetch(fr_dmx* d, int mate, uint8_t* out, uint64_t len) {

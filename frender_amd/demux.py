@@ -117,6 +117,31 @@ class _GzMembers:
         self.f.close()
 
 
+class _GzDevice:
+    """A .fq.gz writer of gzip members whose deflate streams the GPU made (fr_dmx_deflate): one member
+    per window, header + stream + (CRC-32, length) trailer.  A file nothing was written to gets one
+    empty member, as gzip.open's writer leaves it."""
+
+    def __init__(self, path: str, level: int):
+        self.f = open(path, "wb")
+        self.level = level
+        self.wrote = False
+
+    def write_member(self, arr: np.ndarray, start: int, end: int, crc: int, isize: int) -> None:
+        if end <= start:
+            return
+        head, tail = _lib.gzip_frame(int(crc), int(isize))
+        self.f.write(head)
+        self.f.write(memoryview(arr)[start:end])
+        self.f.write(tail)
+        self.wrote = True
+
+    def close(self) -> None:
+        if not self.wrote:
+            self.f.write(gzip.compress(b"", compresslevel=9))
+        self.f.close()
+
+
 class _GzFile:
     """gzip.open writer with the same write_from interface (the image has no libdeflate)."""
 
@@ -138,9 +163,18 @@ def out_path(name, out_dir, infix, read) -> str:
     return f"{out_dir}{name}_frender-demux_{infix + '_' if infix else ''}{read}.fq.gz"
 
 
-def open_files(name, out_dir, infix, level):
+_WRITERS = {"gpu": _GzDevice, "libdeflate": _GzMembers, "zlib": _GzFile}
+
+
+def writer_kind(name: str):
+    """The writer class of --gz-writer (libdeflate falls back to zlib where the image has none)."""
+    if name == "libdeflate" and _LD is None:
+        name = "zlib"
+    return _WRITERS[name]
+
+
+def open_files(name, out_dir, infix, level, kind=_GzDevice):
     """frender.py:667-676."""
-    kind = _GzMembers if _LD is not None and os.environ.get("FR_DEMUX_ZLIB", "0") == "0" else _GzFile
     return {read: kind(out_path(name, out_dir, infix, read), level) for read in ("R1", "R2")}
 
 
@@ -276,18 +310,32 @@ def _demux_pair(dmx, pool, gz, i1, i2, read1_file, read2_file, results, route_of
                 if val == _lib.FR_DMX_MISSING:
                     raise SystemExit(f"Couldn't find barcode {code} in supplied frender result file!")
                 raise SystemExit("Unrecognized read type found in supplied frender result file!")
-            o1 = dmx.fetch(0, int(b1.sum()))
-            o2 = dmx.fetch(1, int(b2.sum()))
-            for j in pending:
-                j.result()
-            c1 = np.concatenate([[0], np.cumsum(b1)]).astype(np.int64)
-            c2 = np.concatenate([[0], np.cumsum(b2)]).astype(np.int64)
-            pending = []
-            for k, w in enumerate(writers):
-                if b1[k]:
-                    pending.append(pool.submit(w["R1"].write_from, o1, int(c1[k]), int(c1[k + 1])))
-                if b2[k]:
-                    pending.append(pool.submit(w["R2"].write_from, o2, int(c2[k]), int(c2[k + 1])))
+            if isinstance(writers[0]["R1"], _GzDevice):  # the GPU deflates every destination's bytes
+                z1, k1, o1 = dmx.deflate(0, len(writers))
+                z2, k2, o2 = dmx.deflate(1, len(writers))
+                for j in pending:
+                    j.result()
+                c1 = np.concatenate([[0], np.cumsum(z1)]).astype(np.int64)
+                c2 = np.concatenate([[0], np.cumsum(z2)]).astype(np.int64)
+                pending = []
+                for k, w in enumerate(writers):
+                    if b1[k]:
+                        pending.append(pool.submit(w["R1"].write_member, o1, int(c1[k]), int(c1[k + 1]), k1[k], b1[k]))
+                    if b2[k]:
+                        pending.append(pool.submit(w["R2"].write_member, o2, int(c2[k]), int(c2[k + 1]), k2[k], b2[k]))
+            else:
+                o1 = dmx.fetch(0, int(b1.sum()))
+                o2 = dmx.fetch(1, int(b2.sum()))
+                for j in pending:
+                    j.result()
+                c1 = np.concatenate([[0], np.cumsum(b1)]).astype(np.int64)
+                c2 = np.concatenate([[0], np.cumsum(b2)]).astype(np.int64)
+                pending = []
+                for k, w in enumerate(writers):
+                    if b1[k]:
+                        pending.append(pool.submit(w["R1"].write_from, o1, int(c1[k]), int(c1[k + 1])))
+                    if b2[k]:
+                        pending.append(pool.submit(w["R2"].write_from, o2, int(c2[k]), int(c2[k + 1])))
             # carry the bytes after the routed records
             cut = []
             for m in (0, 1):
@@ -313,6 +361,7 @@ def frender_demux(args, dev=None) -> None:
     undeter = not args.no_undeter
     samples = not args.no_samples
     level = getattr(args, "gz_level", None) or 9  # gzip.open's default, as the reference writes
+    kind = writer_kind(getattr(args, "gz_writer", None) or "gpu")
     infix = args.o
     undeter_name = f"Undetermined{'-ambiguous' if ambiguous else ''}{'-index-hop' if index_hop else ''}"
 
@@ -335,7 +384,7 @@ def frender_demux(args, dev=None) -> None:
     writers = []  # destination id -> writer pair (N ranks: its name; rank 0 writes the files at the end)
 
     def new_writers(name):
-        writers.append(open_files(name, args.d, infix, level) if group is None else name)
+        writers.append(open_files(name, args.d, infix, level, kind) if group is None else name)
         return len(writers) - 1
 
     sample_dest = {sid: new_writers(sid) for sid in ids} if samples else None
@@ -374,7 +423,7 @@ def frender_demux(args, dev=None) -> None:
     window = int(getattr(args, "window", None) or (512 << 20))  # decoded bytes per mate per GPU pass
     if group is not None:
         return _demux_ranks(group, args, dev, pairs, results, route_of, keys[fast], vals[fast], writers, window, level,
-                            infix)
+                            infix, kind)
     dmx = dev or _lib.Demux(_device_index(None))
     pool = ThreadPoolExecutor(max_workers=max(2, min(32, len(writers) * 2)))
     gz = _lib.GzPool([str(f) for pr in pairs for f in pr], threads=4)
@@ -431,7 +480,7 @@ def _mkdir_everywhere(group, path):
         raise PeerFailed()
 
 
-def _demux_ranks(group, args, dev, pairs, results, route_of, keys, vals, names, window, level, infix):
+def _demux_ranks(group, args, dev, pairs, results, route_of, keys, vals, names, window, level, infix, kind):
     import shutil
 
     from .dist import PeerFailed, reduce_min
@@ -449,7 +498,7 @@ def _demux_ranks(group, args, dev, pairs, results, route_of, keys, vals, names, 
         for j, k in enumerate(mine):
             d = os.path.join(parts, str(k))
             os.makedirs(d, exist_ok=True)
-            writers = [open_files(n, d, infix, level) for n in names]
+            writers = [open_files(n, d, infix, level, kind) for n in names]
             try:
                 _demux_pair(dmx, pool, gz, 2 * j, 2 * j + 1, pairs[k][0], pairs[k][1], results, route_of, writers,
                             window)

@@ -334,6 +334,33 @@ int fr_dmx_route(fr_dmx* d, int n_dest, uint64_t n_pairs, int64_t* first_error, 
                  uint64_t* bytes_r1, uint64_t* bytes_r2);
 /* the routed bytes of a mate (destination-major) */
 int fr_dmx_fetch(fr_dmx* d, int mate, uint8_t* out, uint64_t len);
+/* the demux writers' compression on the GPU (replaces the gzip.open(..., "wb") writer pairs of
+ * frender.py:667-676 that frender.py:795-810 write every routed record to): the routed bytes of a mate
+ * (the last fr_dmx_route) become one raw deflate stream (RFC 1951) per destination that has bytes;
+ * comp_bytes[k] = its byte count (0: no bytes routed), crc32[k] = the CRC-32 of destination k's routed
+ * bytes, so that a gzip member is header + stream + (crc32[k], bytes routed).  The streams stay on the
+ * device, destination-major, until fr_dmx_fetch_deflated (the next fr_dmx_deflate of the mate replaces
+ * them). */
+int fr_dmx_deflate(fr_dmx* d, int mate, int n_dest, uint64_t* comp_bytes, uint32_t* crc32);
+int fr_dmx_fetch_deflated(fr_dmx* d, int mate, uint8_t* out, uint64_t len);
+
+/* ---- GPU deflate over any byte ranges (fr_deflate.hip; fr_dmx_deflate runs it on the routed bytes).
+ * Stream s is bytes [offsets[s], offsets[s + 1]) of the device buffer dev_data (4-byte aligned, 16
+ * readable bytes past offsets[n_streams]); every stream becomes one raw deflate stream, no larger than
+ * zlib level 9 makes it on FASTQ-shaped text (64-KiB blocks, each with a dynamic Huffman code over a
+ * cost-minimising parse; a block that would not shrink is stored). */
+typedef struct fr_defl fr_defl;
+fr_defl* fr_defl_create(int device);
+void fr_defl_destroy(fr_defl* z);
+const char* fr_defl_last_error(const fr_defl* z);
+int fr_defl_run(fr_defl* z, const uint8_t* dev_data, const uint64_t* offsets, int n_streams, uint64_t* comp_bytes,
+                uint32_t* crc32);
+/* the same over a host buffer (copied to the device first) */
+int fr_defl_run_host(fr_defl* z, const uint8_t* data, uint64_t len, const uint64_t* offsets, int n_streams,
+                     uint64_t* comp_bytes, uint32_t* crc32);
+/* the last run's streams, concatenated in stream order */
+uint64_t fr_defl_out_bytes(const fr_defl* z);
+int fr_defl_fetch(fr_defl* z, uint8_t* out, uint64_t len);
 
 #ifdef __cplusplus
 }

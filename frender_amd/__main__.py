@@ -53,6 +53,7 @@ def main(argv=None):
                         "--gz-level)")
     d.add_argument("--gpus", type=int, default=1,
                    help="GPUs (one process each; file pairs are dealt to them, rank 0 writes the outputs)")
+    d.add_argument("--stage-times", action="store_true", help="print the demux's seconds per stage (stderr)")
     d.add_argument("files", nargs="+", help="Fastq file, list of fastq files, or directory path")
     d.set_defaults(cmd="demux")
     args = parser.parse_args(argv)

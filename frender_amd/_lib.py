@@ -116,6 +116,7 @@ _SIGS = {
                                   C.c_int, C.c_int, C.c_int]),
     # native inflate (row f-2)
     "fr_gz_open": (P, [C.POINTER(C.c_char_p), C.c_int, C.c_int]),
+    "fr_gz_open_ahead": (P, [C.POINTER(C.c_char_p), C.c_int, C.c_int, C.c_int]),
     "fr_gz_feed": (C.c_int, [P, C.c_int, P]),
     "fr_gz_next": (C.c_int, [P, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]),
     "fr_gz_feed_part": (C.c_int, [P, C.c_int, P, C.c_int64, C.c_int, C.c_int, C.c_uint64, C.POINTER(C.c_uint64)]),
@@ -268,11 +269,14 @@ class GzPool:
     """Native inflate of a scan's .gz files (fr_gz_*): `threads` host threads inflate the listed
     files in order ahead of the consumer; feed(i, ctx) hands file i's bytes to ctx.feed."""
 
-    def __init__(self, paths, threads: int = 1):
+    def __init__(self, paths, threads: int = 1, ahead: int = None):
+        """`ahead`: files inflating at once (default `threads`); the other threads split big
+        single-member files (fr_gz_open_ahead)."""
         self.paths = [str(p) for p in paths]
         enc = [os.fsencode(p) for p in self.paths]
         arr = (C.c_char_p * max(len(enc), 1))(*enc)
-        self.h = lib.fr_gz_open(arr, len(enc), max(1, int(threads)))
+        threads = max(1, int(threads))
+        self.h = lib.fr_gz_open_ahead(arr, len(enc), threads, max(1, int(ahead or threads)))
         if not self.h:
             raise FrenderError("fr_gz_open returned NULL")
 

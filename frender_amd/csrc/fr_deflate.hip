@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -41,7 +42,8 @@ using namespace frd;
 constexpr uint32_t TPB = 256;
 constexpr uint32_t NPASS = 4;
 constexpr uint32_t NB = 1u << HBITS;
-constexpr uint64_t SCR_BYTES = (uint64_t)BLOCK * 4 + (uint64_t)BLOCK * 2 + (uint64_t)NSUB * (SUB + 1) * 4 + 256;
+constexpr uint64_t SCR_BYTES = (uint64_t)BLOCK * 4 + (uint64_t)BLOCK * 2 + 256;
+static_assert(NSUB * 256 <= NB * WAYS / 2, "the parse rings live in the matchfinder table");
 
 struct DJob {
     uint64_t start;  // first input byte (offset into the data buffer)
@@ -56,7 +58,7 @@ struct DefShared {
         uint16_t tab[NB * WAYS];  // matchfinder buckets (positions mod 65536, relative to the history start)
         uint32_t stage[NB * WAYS / 2];  // then the block's output bits
     };
-    uint16_t bh[TPB];  // this batch's hashes (0xFFFF: none)
+    alignas(8) uint16_t bh[TPB];  // this batch's hashes (0xFFFF: none)
     uint32_t bhist[256];
     uint32_t llf[NLL];
     uint32_t df[NDIST];
@@ -77,6 +79,26 @@ __device__ __forceinline__ uint32_t ld32u(const uint8_t* p) {
     const uint32_t* q = (const uint32_t*)(a & ~(uintptr_t)3);
     return __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(a & 3));
 }
+
+#ifdef FRD_PROF
+__device__ unsigned long long g_prof[8];
+#define PROF_MARK(k)                                                            \
+    do {                                                                        \
+        if (t == 0) {                                                           \
+            const unsigned long long now_ = wall_clock64();                     \
+            atomicAdd(&g_prof[k], now_ - prof_t);                               \
+            prof_t = now_;                                                      \
+        }                                                                       \
+    } while (0)
+#else
+#define PROF_MARK(k) \
+    do {             \
+    } while (0)
+#endif
+
+struct Ld32 {
+    __device__ uint32_t operator()(const uint8_t* p) const { return ld32u(p); }
+};
 
 struct LdsOr {
     __device__ void operator()(uint32_t* p, uint32_t v) const {
@@ -125,7 +147,10 @@ __global__ __launch_bounds__(TPB, 2) void deflate_blocks(const uint8_t* __restri
     }
     uint32_t* m = (uint32_t*)(scratch + (uint64_t)blockIdx.x * SCR_BYTES);
     uint16_t* choice = (uint16_t*)(m + BLOCK);
-    uint32_t* best = (uint32_t*)(choice + BLOCK);
+    const Lay ly{m, choice};
+#ifdef FRD_PROF
+    unsigned long long prof_t = wall_clock64();
+#endif
     for (uint32_t j = blockIdx.x; j < n_jobs; j += gridDim.x) {
         const DJob job = jobs[j];
         const uint32_t len = job.len, hist = job.hist, ntot = hist + len;
@@ -154,35 +179,32 @@ __global__ __launch_bounds__(TPB, 2) void deflate_blocks(const uint8_t* __restri
                     uint32_t dds[WAYS + 1];
                     for (uint32_t s = 0; s < WAYS; ++s) dds[s] = (r - S.tab[h * WAYS + s]) & 0xFFFF;
                     dds[WAYS] = 0;
-                    for (uint32_t u = t; u-- > 0;)
-                        if (S.bh[u] == h) {
-                            dds[WAYS] = t - u;
-                            break;
-                        }
-                    const uint8_t* p = hsp + r;
-                    for (uint32_t s = 0; s <= WAYS; ++s) {
-                        const uint32_t dd = dds[s];
-                        if (dd == 0 || dd > WIN || dd > r) continue;
-                        const uint8_t* c = p - dd;
-                        if (ld32u(c) != w) continue;
-                        uint32_t l = 4;
-                        while (l < maxlen) {
-                            const uint32_t x = ld32u(p + l) ^ ld32u(c + l);
-                            if (x) {
-                                l += (uint32_t)__builtin_ctz(x) >> 3;
+                    {  // the latest earlier lane of the batch with the same hash, four hashes per LDS read
+                        const uint64_t hh = (uint64_t)h * 0x0001000100010001ull;
+                        const uint64_t* bw = (const uint64_t*)S.bh;
+                        for (int wi = ((int)t - 1) >> 2; wi >= 0; --wi) {
+                            const uint64_t v = bw[wi] ^ hh;
+                            uint32_t u = ~0u;
+                            for (int q = 3; q >= 0; --q)
+                                if ((uint32_t)(4 * wi + q) < t && ((v >> (16 * q)) & 0xFFFF) == 0) {
+                                    u = 4 * wi + q;
+                                    break;
+                                }
+                            if (u != ~0u) {
+                                dds[WAYS] = t - u;
                                 break;
                             }
-                            l += 4;
                         }
-                        l = min(l, maxlen);
-                        if (l > bl || (l == bl && dd < bd)) bl = l, bd = dd;
                     }
+                    best_match<WAYS + 1>(hsp + r, w, dds, r, maxlen, Ld32{}, bl, bd);
                 }
-                m[r - hist] = bl >= MINM ? (bl | (bd << 16)) : 0u;
+                ly.rec(r - hist) = mpack(hsp[r], bl >= MINM ? bl : 0u, bd);
             }
             __syncthreads();
             if (h != 0xFFFF) S.tab[h * WAYS + (t >> 6)] = (uint16_t)r;
         }
+        __syncthreads();
+        PROF_MARK(0);
         // ---- crc32 of the block: 1-KiB slices, folded by lane 0
         const uint32_t nsub = (len + SUB - 1) / SUB;
         if (t < nsub) {
@@ -215,21 +237,24 @@ __global__ __launch_bounds__(TPB, 2) void deflate_blocks(const uint8_t* __restri
                 crc ^= S.lane_v[s];
             }
         }
+        PROF_MARK(1);
         // ---- parse passes
         for (uint32_t pass = 0; pass < NPASS; ++pass) {
             for (uint32_t i = t; i < NLL; i += TPB) S.llf[i] = 0;
             if (t < NDIST) S.df[t] = 0;
             if (t < nsub) {
                 const uint32_t a = t * SUB, b = min(len, a + SUB);
-                parse_range(blk, a, b, m, choice, best + t * (SUB + 1), S.cost);
+                parse_range(a, b, ly, Ring{S.stage + t * 256, t & 63}, S.cost);
             }
             __syncthreads();
+            PROF_MARK(2);
             if (t == 0) S.llf[256] = 1;
             if (t < nsub) {
                 const uint32_t a = t * SUB, b = min(len, a + SUB);
-                count_range(blk, a, b, m, choice, S.llf, S.df, LdsAdd{});
+                count_range(a, b, ly, S.llf, S.df, LdsAdd{});
             }
             __syncthreads();
+            PROF_MARK(3);
             if (t == 64) {
                 huff_gather(S.df, NDIST, S.hwd);
                 huff_sort(S.hwd);
@@ -237,6 +262,7 @@ __global__ __launch_bounds__(TPB, 2) void deflate_blocks(const uint8_t* __restri
             }
             ll_lengths(S, t);
             __syncthreads();
+            PROF_MARK(4);
             if (pass + 1 < NPASS) {
                 costs_from_lengths(S.cost, S.T.ll_len, S.T.d_len, 15, t, t + 1);
                 if (t + TPB <= MAXM) costs_from_lengths(S.cost, S.T.ll_len, S.T.d_len, 15, t + TPB, t + TPB + 1);
@@ -268,6 +294,7 @@ __global__ __launch_bounds__(TPB, 2) void deflate_blocks(const uint8_t* __restri
             S.misc[4] = 0;
         }
         __syncthreads();
+        PROF_MARK(5);
         const uint32_t nbytes = S.misc[2];
         uint8_t* out = stage_out + (uint64_t)j * OUT_STRIDE;
         if (S.misc[0]) {
@@ -275,7 +302,7 @@ __global__ __launch_bounds__(TPB, 2) void deflate_blocks(const uint8_t* __restri
             for (uint32_t i = t; i < nw + 1; i += TPB) S.stage[i] = 0;
             if (t < nsub) {
                 const uint32_t a = t * SUB, b = min(len, a + SUB);
-                S.lane_v[t] = (uint32_t)range_bits(blk, a, b, m, choice, S.T);
+                S.lane_v[t] = (uint32_t)range_bits(a, b, ly, S.T);
             }
             __syncthreads();
             if (t == 0) {
@@ -291,7 +318,7 @@ __global__ __launch_bounds__(TPB, 2) void deflate_blocks(const uint8_t* __restri
                 const uint32_t a = t * SUB, b = min(len, a + SUB);
                 BitW bw;
                 bw.init(S.stage, S.lane_off[t]);
-                write_range(blk, a, b, m, choice, S.T, bw, LdsOr{});
+                write_range(a, b, ly, S.T, bw, LdsOr{});
                 bw.flush(LdsOr{});
             }
             if (t == TPB - 1) {
@@ -328,6 +355,7 @@ __global__ __launch_bounds__(TPB, 2) void deflate_blocks(const uint8_t* __restri
             out_crc[j] = crc;
         }
         __syncthreads();
+        PROF_MARK(6);
     }
 }
 
@@ -458,7 +486,7 @@ int fr_defl_run(fr_defl* z, const uint8_t* dev_data, const uint64_t* offsets, in
                 uint32_t* crc32_out) {
     if (!z->scratch) return FR_ERR_HIP;
     if (n_streams < 0 || (n_streams && !offsets)) return z->err = "fr_defl_run: bad stream list", FR_ERR_INVALID;
-    if (((uintptr_t)dev_data & 3u) != 0) return z->err = "fr_defl_run: data must be 4-byte aligned", FR_ERR_INVALID;
+    if (((uintptr_t)dev_data & 15u) != 0) return z->err = "fr_defl_run: data must be 16-byte aligned", FR_ERR_INVALID;
     DF(hipSetDevice(z->device));
     z->hjobs.clear();
     for (int s = 0; s < n_streams; ++s) {
@@ -490,6 +518,17 @@ int fr_defl_run(fr_defl* z, const uint8_t* dev_data, const uint64_t* offsets, in
         hipLaunchKernelGGL(deflate_blocks, dim3(g), dim3(TPB), 0, z->stream, dev_data, z->jobs, (uint32_t)nj, z->stage,
                            z->blen, z->bcrc, z->scratch, z->shift);
         DF(hipGetLastError());
+#ifdef FRD_PROF
+        {
+            unsigned long long pr[8];
+            DF(hipStreamSynchronize(z->stream));
+            DF(hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_prof), sizeof pr));
+            fprintf(stderr, "FRD_PROF wall ticks (100 MHz) summed over WGs: match %llu crc+cost %llu parse %llu count %llu huff %llu tables %llu emit %llu\n",
+                    pr[0], pr[1], pr[2], pr[3], pr[4], pr[5], pr[6]);
+            unsigned long long zero[8] = {0};
+            DF(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), zero, sizeof zero));
+        }
+#endif
         DF(hipMemsetAsync(z->blen + nj, 0, 4, z->stream));
         size_t tb = 0;
         DF(rocprim::exclusive_scan(nullptr, tb, z->blen, z->boff, (uint64_t)0, (size_t)nj + 1,

@@ -8,6 +8,7 @@
 // than zlib -9's on the demux shapes (tests/test_deflate_host.py, tests/test_gpu_deflate.py).
 #pragma once
 #include <stdint.h>
+#include <string.h>
 
 #if defined(__HIPCC__)
 #define FRD_HD __host__ __device__ inline
@@ -195,41 +196,180 @@ FRD_HD uint32_t dist_cost(const Costs& c, uint32_t d) {
     return c.dist[code];
 }
 
-// Backward cost-minimising parse of [a, b) (block-relative).  m[i] = longest match at i
-// (len | dist << 16, len 0 when none); choice[i] = 0 (literal) or the match length taken at i.
-// best[] holds b - a + 1 entries.  Matches end at b: a lane's sub-range is parsed on its own.
-FRD_HD void parse_range(const uint8_t* blk, uint32_t a, uint32_t b, const uint32_t* m, uint16_t* choice,
-                        uint32_t* best, const Costs& c) {
-    best[b - a] = 0;
-    for (uint32_t i = b; i-- > a;) {
-        uint32_t bc = best[i + 1 - a] + c.lit[blk[i]];
-        uint32_t ch = 0;
-        const uint32_t mi = m[i];
-        uint32_t L = mi & 0xFFFF;
-        if (L > b - i) L = b - i;
-        if (L >= MINM) {
-            const uint32_t dc = dist_cost(c, mi >> 16);
-            const uint32_t* bb = best + (i - a);
-            if (L <= 64) {
-                for (uint32_t l = MINM; l <= L; ++l) {
-                    const uint32_t x = c.len[l] + dc + bb[l];
-                    if (x < bc) bc = x, ch = l;
-                }
+// Per-position record of the matchfinder: the byte, the longest match's length (0: none) and distance
+FRD_HD uint32_t mpack(uint32_t byte, uint32_t len, uint32_t dist) {
+    return byte | (len << 8) | (len ? (dist - 1) << 17 : 0u);
+}
+FRD_HD uint32_t m_byte(uint32_t v) { return v & 255; }
+FRD_HD uint32_t m_len(uint32_t v) { return (v >> 8) & 511; }
+FRD_HD uint32_t m_dist(uint32_t v) { return (v >> 17) + 1; }
+
+// The longest of the candidate matches at p (distances dds[0..nc), 0 = none; the 4 bytes at p are w),
+// ties to the nearer; every surviving candidate is extended in the same 8-byte step, so a step costs
+// one round of independent loads.  ld(q) = the 4 bytes at q (unaligned).
+template <uint32_t NC, class LD>
+FRD_HD void best_match(const uint8_t* p, uint32_t w, const uint32_t* dds, uint32_t r, uint32_t maxlen, LD ld,
+                       uint32_t& bl, uint32_t& bd) {
+    constexpr uint32_t nc = NC;
+    uint32_t len[NC];
+    uint32_t alive = 0;
+#pragma unroll
+    for (uint32_t s = 0; s < nc; ++s) {
+        len[s] = 0;
+        const uint32_t dd = dds[s];
+        if (dd == 0 || dd > WIN || dd > r) continue;
+        if (ld(p - dd) == w) {
+            alive |= 1u << s;
+            len[s] = 4;
+        }
+    }
+    for (uint32_t l = 4; alive && l < maxlen; l += 8) {
+        const uint32_t p0 = ld(p + l), p1 = ld(p + l + 4);
+#pragma unroll
+        for (uint32_t s = 0; s < nc; ++s) {
+            if (!(alive >> s & 1)) continue;
+            const uint8_t* c = p - dds[s] + l;
+            const uint32_t x0 = ld(c) ^ p0, x1 = ld(c + 4) ^ p1;
+            if (x0) {
+                len[s] = l + ((uint32_t)__builtin_ctz(x0) >> 3);
+                alive &= ~(1u << s);
+            } else if (x1) {
+                len[s] = l + 4 + ((uint32_t)__builtin_ctz(x1) >> 3);
+                alive &= ~(1u << s);
             } else {
-                for (uint32_t l = MINM; l <= 36; ++l) {
-                    const uint32_t x = c.len[l] + dc + bb[l];
-                    if (x < bc) bc = x, ch = l;
-                }
-                for (uint32_t l = L - 32; l <= L; ++l) {
-                    const uint32_t x = c.len[l] + dc + bb[l];
-                    if (x < bc) bc = x, ch = l;
-                }
+                len[s] = l + 8;
             }
         }
-        best[i - a] = bc;
-        choice[i] = (uint16_t)ch;
+    }
+    bl = 0, bd = 0;
+#pragma unroll
+    for (uint32_t s = 0; s < nc; ++s) {
+        const uint32_t l = len[s] < maxlen ? len[s] : maxlen;
+        if (l > bl || (l == bl && l && dds[s] < bd)) bl = l, bd = dds[s];
     }
 }
+
+// 16-byte loads and stores of the per-lane arrays (16-byte aligned chunks)
+FRD_HD void ld16(const void* p, uint32_t* w) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint4 v = *(const uint4*)p;
+    w[0] = v.x, w[1] = v.y, w[2] = v.z, w[3] = v.w;
+#else
+    memcpy(w, p, 16);
+#endif
+}
+FRD_HD void st16(void* p, const uint32_t* w) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    *(uint4*)p = make_uint4(w[0], w[1], w[2], w[3]);
+#else
+    memcpy(p, w, 16);
+#endif
+}
+
+// The per-position arrays of a block (matchfinder records, parse choices) are laid out lane-major
+// by 16-byte chunk: the chunks of one chunk index for the NSUB lanes sit side by side, so the lanes'
+// loads in step are contiguous.  lane = i / SUB, k = i % SUB.
+struct Lay {
+    uint32_t* m;
+    uint16_t* ch;
+    FRD_HD uint32_t* mchunk(uint32_t i) const { return m + ((((i % SUB) >> 2) * NSUB + i / SUB) << 2); }
+    FRD_HD uint16_t* cchunk(uint32_t i) const { return ch + ((((i % SUB) >> 3) * NSUB + i / SUB) << 3); }
+    FRD_HD uint32_t& rec(uint32_t i) const { return mchunk(i)[i & 3]; }
+};
+
+// The parse's costs-to-end of the next 256 positions: a ring (256 words per lane; the kernel
+// swizzles a lane's slots by its lane number so that lanes marching in step hit distinct LDS banks)
+struct Ring {
+    uint32_t* base;
+    uint32_t sw;
+    FRD_HD uint32_t& at(uint32_t k) const { return base[(k & 255) ^ sw]; }
+};
+constexpr uint32_t PARSE_MAXL = 255;  // the ring holds best[i + 1 .. i + 255]: longer matches are cut
+
+// Backward cost-minimising parse of [a, b) (block-relative; a a multiple of 8).  m[i] = mpack record
+// of i; choice[i] = 0 (literal) or the match length taken at i, written 8 at a time (a chunk past b
+// is overwritten: no lane owns those positions).  Matches end at b: a lane's sub-range is parsed on
+// its own.  m is read 4 positions per load, the next chunk one chunk ahead.  The lengths tried at a
+// match: all of 4..10, or 4..8 and the last three of a longer one (trying every length changed the
+// FASTQ shapes' streams by < 0.01%).
+FRD_HD void parse_range(uint32_t a, uint32_t b, const Lay& ly, const Ring& best, const Costs& c) {
+    if (b <= a) return;
+    best.at(b - a) = 0;
+    uint32_t cur[4], nxt[4] = {0, 0, 0, 0}, wbuf[4] = {0, 0, 0, 0};
+    uint32_t cc = (b - 1) >> 2, wc = (b - 1) >> 3;
+    ld16(ly.mchunk(4 * cc), cur);
+    if (cc > (a >> 2)) ld16(ly.mchunk(4 * (cc - 1)), nxt);
+    for (uint32_t i = b; i-- > a;) {
+        if ((i >> 2) != cc) {
+            cc = i >> 2;
+            for (int q = 0; q < 4; ++q) cur[q] = nxt[q];
+            if (cc > (a >> 2)) ld16(ly.mchunk(4 * (cc - 1)), nxt);
+        }
+        if ((i >> 3) != wc) {
+            st16(ly.cchunk(8 * wc), wbuf);
+            for (int q = 0; q < 4; ++q) wbuf[q] = 0;
+            wc = i >> 3;
+        }
+        const uint32_t k = i - a;
+        const uint32_t mi = cur[i & 3];
+        uint32_t bc = best.at(k + 1) + c.lit[m_byte(mi)];
+        uint32_t ch = 0;
+        uint32_t L = m_len(mi);
+        if (L > b - i) L = b - i;
+        if (L > PARSE_MAXL) L = PARSE_MAXL;
+        if (L >= MINM) {
+            const uint32_t dc = dist_cost(c, m_dist(mi));
+            auto span = [&](uint32_t lo, uint32_t hi) {  // lengths lo..hi in increasing order
+                uint32_t l = lo;
+                for (; l + 8 <= hi + 1; l += 8) {
+                    uint32_t v[8];
+#pragma unroll
+                    for (uint32_t q = 0; q < 8; ++q) v[q] = c.len[l + q] + best.at(k + l + q);
+#pragma unroll
+                    for (uint32_t q = 0; q < 8; ++q) {
+                        const uint32_t x = v[q] + dc;
+                        if (x < bc) bc = x, ch = l + q;
+                    }
+                }
+                for (; l <= hi; ++l) {
+                    const uint32_t x = c.len[l] + dc + best.at(k + l);
+                    if (x < bc) bc = x, ch = l;
+                }
+            };
+            if (L <= 10) {  // lengths 4..10 and, of a longer match, 4..8 and its last three
+                span(MINM, L);
+            } else {
+                span(MINM, 8);
+                span(L - 2, L);
+            }
+        }
+        best.at(k) = bc;
+        wbuf[(i >> 1) & 3] |= ch << ((i & 1) * 16);
+    }
+    st16(ly.cchunk(8 * wc), wbuf);
+}
+
+// Forward walk of a lane's parse: choices 8 and records 4 per load
+struct Fwd {
+    Lay ly;
+    uint32_t cc, mc;
+    uint32_t cw[4], mw[4];
+    FRD_HD Fwd(const Lay& l) : ly(l), cc(~0u), mc(~0u) {}
+    FRD_HD uint32_t choice(uint32_t i) {
+        if ((i >> 3) != cc) {
+            cc = i >> 3;
+            ld16(ly.cchunk(i), cw);
+        }
+        return (cw[(i >> 1) & 3] >> ((i & 1) * 16)) & 0xFFFF;
+    }
+    FRD_HD uint32_t rec(uint32_t i) {
+        if ((i >> 2) != mc) {
+            mc = i >> 2;
+            ld16(ly.mchunk(i), mw);
+        }
+        return mw[i & 3];
+    }
+};
 
 // Bit writer into zeroed 32-bit words: every word is ORed in (the GPU's lanes share edge words)
 struct BitW {
@@ -352,19 +492,19 @@ FRD_HD void write_header(const Tables& t, bool final_block, BitW& bw, OR orf) {
 }
 
 // body bits of [a, b) under the parse in choice[] and the final tables
-FRD_HD uint64_t range_bits(const uint8_t* blk, uint32_t a, uint32_t b, const uint32_t* m, const uint16_t* choice,
-                           const Tables& t) {
+FRD_HD uint64_t range_bits(uint32_t a, uint32_t b, const Lay& ly, const Tables& t) {
     uint64_t bits = 0;
+    Fwd f(ly);
     for (uint32_t i = a; i < b;) {
-        const uint32_t ch = choice[i];
+        const uint32_t ch = f.choice(i), v = f.rec(i);
         if (ch >= MINM) {
             uint32_t idx, eb, ev, dcode, deb, dev;
             len_code(ch, idx, eb, ev);
-            dist_code(m[i] >> 16, dcode, deb, dev);
+            dist_code(m_dist(v), dcode, deb, dev);
             bits += t.ll_len[257 + idx] + eb + t.d_len[dcode] + deb;
             i += ch;
         } else {
-            bits += t.ll_len[blk[i]];
+            bits += t.ll_len[m_byte(v)];
             ++i;
         }
     }
@@ -372,21 +512,21 @@ FRD_HD uint64_t range_bits(const uint8_t* blk, uint32_t a, uint32_t b, const uin
 }
 
 template <class OR>
-FRD_HD void write_range(const uint8_t* blk, uint32_t a, uint32_t b, const uint32_t* m, const uint16_t* choice,
-                        const Tables& t, BitW& bw, OR orf) {
+FRD_HD void write_range(uint32_t a, uint32_t b, const Lay& ly, const Tables& t, BitW& bw, OR orf) {
+    Fwd f(ly);
     for (uint32_t i = a; i < b;) {
-        const uint32_t ch = choice[i];
+        const uint32_t ch = f.choice(i), v = f.rec(i);
         if (ch >= MINM) {
             uint32_t idx, eb, ev, dcode, deb, dev;
             len_code(ch, idx, eb, ev);
-            dist_code(m[i] >> 16, dcode, deb, dev);
+            dist_code(m_dist(v), dcode, deb, dev);
             bw.put(t.ll_code[257 + idx], t.ll_len[257 + idx], orf);
             if (eb) bw.put(ev, eb, orf);
             bw.put(t.d_code[dcode], t.d_len[dcode], orf);
             if (deb) bw.put(dev, deb, orf);
             i += ch;
         } else {
-            bw.put(t.ll_code[blk[i]], t.ll_len[blk[i]], orf);
+            bw.put(t.ll_code[m_byte(v)], t.ll_len[m_byte(v)], orf);
             ++i;
         }
     }
@@ -394,19 +534,19 @@ FRD_HD void write_range(const uint8_t* blk, uint32_t a, uint32_t b, const uint32
 
 // symbol counts of [a, b) under the parse in choice[]
 template <class ADD>
-FRD_HD void count_range(const uint8_t* blk, uint32_t a, uint32_t b, const uint32_t* m, const uint16_t* choice,
-                        uint32_t* llf, uint32_t* df, ADD add) {
+FRD_HD void count_range(uint32_t a, uint32_t b, const Lay& ly, uint32_t* llf, uint32_t* df, ADD add) {
+    Fwd f(ly);
     for (uint32_t i = a; i < b;) {
-        const uint32_t ch = choice[i];
+        const uint32_t ch = f.choice(i), v = f.rec(i);
         if (ch >= MINM) {
             uint32_t idx, eb, ev, dcode, deb, dev;
             len_code(ch, idx, eb, ev);
-            dist_code(m[i] >> 16, dcode, deb, dev);
+            dist_code(m_dist(v), dcode, deb, dev);
             add(llf + 257 + idx);
             add(df + dcode);
             i += ch;
         } else {
-            add(llf + blk[i]);
+            add(llf + m_byte(v));
             ++i;
         }
     }

@@ -131,6 +131,7 @@ struct GzFile {
 struct fr_gz {
     std::vector<GzFile> files;
     int threads = 1;
+    int ahead = 1;         // files inflating at once (fr_gz_open: threads; fr_gz_open_ahead: fewer)
     int busy = 0;          // threads inflating now (workers + BGZF helpers), <= threads
     size_t whole_used = 0; // bytes of whole-file buffers held now (<= WHOLE_BUDGET)
     size_t block = 16u << 20;
@@ -181,7 +182,7 @@ constexpr size_t LD_MAX_OUT = 1ull << 30;    // decoded bytes it may produce
 constexpr size_t BGZF_MAX_IN = 1ull << 30;   // BGZF files: compressed bytes for the parallel path
 constexpr size_t BGZF_MAX_BLOCK = 65536;     // the format's bound on a member's size and ISIZE
 constexpr size_t BGZF_WINDOW = 64ull << 20;  // decoded bytes per parallel BGZF window
-constexpr size_t WHOLE_BUDGET = 3ull << 30;  // whole-file buffers (input + output) held at once per pool
+constexpr size_t WHOLE_BUDGET = 6ull << 30;  // whole-file buffers (input + output) held at once per pool
 constexpr size_t PGZ_MIN_IN = 16ull << 20;   // single-member files from this compressed size decode in parallel
 constexpr size_t PGZ_CHUNK_MIN = 2ull << 20;  // compressed bytes per parallel chunk (about 4 per thread)
 constexpr size_t PGZ_CHUNK_MAX = 32ull << 20;
@@ -313,7 +314,9 @@ bool inflate_member_parallel(fr_gz* g, GzFile& f, const Bytes& in) {
         size_t b;
         ~Hold() { give_budget(g, b); }
     } hold{g, est};
-    const int nh = take_threads(g, g->threads - 1);
+    // every idle thread (fr_gz_open), or the file's share threads / files_ahead (fr_gz_open_ahead)
+    const int share = g->ahead >= g->threads ? g->threads : std::max(2, g->threads / g->ahead);
+    const int nh = take_threads(g, share - 1);
     struct Threads {
         fr_gz* g;
         int k;
@@ -581,7 +584,7 @@ void worker(fr_gz* g) {
         {
             std::unique_lock<std::mutex> lk(g->m);
             g->cv.wait(lk, [&] {
-                return g->stop || (g->next < (int)g->files.size() && g->next < g->consume + g->threads &&
+                return g->stop || (g->next < (int)g->files.size() && g->next < g->consume + g->ahead &&
                                    g->busy < g->threads);
             });
             if (g->stop) return;
@@ -601,17 +604,22 @@ void worker(fr_gz* g) {
 
 extern "C" {
 
-fr_gz* fr_gz_open(const char* const* paths, int n_files, int threads) {
+fr_gz* fr_gz_open_ahead(const char* const* paths, int n_files, int threads, int files_ahead) {
     fr_gz* g = new fr_gz();
     g->files.resize(n_files > 0 ? n_files : 0);
     for (int i = 0; i < n_files; ++i) g->files[i].path = paths[i];
     g->threads = threads < 1 ? 1 : threads;
+    g->ahead = std::max(1, std::min(files_ahead, g->threads));
     // files inflating ahead of the consumer may buffer up to 2 GiB of decoded blocks in all, so a
     // worker is not parked behind a short queue while the consumer is still on an earlier file
-    g->depth = std::max<size_t>(3, (2ull << 30) / ((size_t)g->threads * g->block));
-    const int nw = std::min(g->threads, std::max(n_files, 1));
+    g->depth = std::max<size_t>(3, (2ull << 30) / ((size_t)g->ahead * g->block));
+    const int nw = std::min(g->ahead, std::max(n_files, 1));
     for (int k = 0; k < nw; ++k) g->workers.emplace_back(worker, g);
     return g;
+}
+
+fr_gz* fr_gz_open(const char* const* paths, int n_files, int threads) {
+    return fr_gz_open_ahead(paths, n_files, threads, threads);
 }
 
 const char* fr_gz_error(const fr_gz* g) { return g ? g->err.c_str() : "null inflate pool"; }

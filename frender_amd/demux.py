@@ -11,9 +11,12 @@ from __future__ import annotations
 
 import csv
 import gzip
+import json
 import os
 import re
+import sys
 import threading
+import time
 from concurrent.futures import ThreadPoolExecutor
 from pathlib import Path
 
@@ -262,6 +265,9 @@ def _line_at(data: bytes, start: int) -> bytes:
     return data[start:] if e < 0 else data[start:e]
 
 
+STAGE_TIMES = {}  # seconds per stage of _demux_pair's windows (demux --stage-times prints them)
+
+
 def _demux_pair(dmx, pool, gz, i1, i2, read1_file, read2_file, results, route_of, writers, window):
     """One R1/R2 pair in record-aligned windows: the GPU indexes both windows, the complete
     record pairs are routed, and the bytes after the last routed record carry into the next
@@ -271,8 +277,11 @@ def _demux_pair(dmx, pool, gz, i1, i2, read1_file, read2_file, results, route_of
     bufs = [b"", b""]
     eof = [False, False]
     pending = []  # the previous window's gzip jobs: overlap with this window's inflate and GPU work
+    st = STAGE_TIMES
+    clock = time.perf_counter
     try:
         while True:
+            t0 = clock()
             for m in (0, 1):
                 parts = [bufs[m]]
                 size = len(bufs[m])
@@ -285,7 +294,9 @@ def _demux_pair(dmx, pool, gz, i1, i2, read1_file, read2_file, results, route_of
                     parts.append(c)
                     size += len(c)
                 bufs[m] = b"".join(parts)
+            t1 = clock()
             n = [dmx.load(0, bufs[0]), dmx.load(1, bufs[1])]
+            t2 = clock()
             # the last record of a window may continue in the next one unless its file ended
             done = [n[m] if eof[m] else max(n[m] - 1, 0) for m in (0, 1)]
             n_pairs = min(done)
@@ -304,6 +315,7 @@ def _demux_pair(dmx, pool, gz, i1, i2, read1_file, read2_file, results, route_of
                     dest.append(_lib.FR_DMX_MISSING if row is None else route_of(row))
                 dmx.patch(ex, np.array(dest, dtype=np.int32))
             first, val, b1, b2 = dmx.route(len(writers), n_pairs)
+            t3 = clock()
             if first >= 0:
                 s, _ = dmx.records(1, [first])
                 code = _line_at(bufs[1], int(s[0])).split(b":")[-1].decode("utf-8")
@@ -313,6 +325,7 @@ def _demux_pair(dmx, pool, gz, i1, i2, read1_file, read2_file, results, route_of
             if isinstance(writers[0]["R1"], _GzDevice):  # the GPU deflates every destination's bytes
                 z1, k1, o1 = dmx.deflate(0, len(writers))
                 z2, k2, o2 = dmx.deflate(1, len(writers))
+                t4 = clock()
                 for j in pending:
                     j.result()
                 c1 = np.concatenate([[0], np.cumsum(z1)]).astype(np.int64)
@@ -326,6 +339,7 @@ def _demux_pair(dmx, pool, gz, i1, i2, read1_file, read2_file, results, route_of
             else:
                 o1 = dmx.fetch(0, int(b1.sum()))
                 o2 = dmx.fetch(1, int(b2.sum()))
+                t4 = clock()
                 for j in pending:
                     j.result()
                 c1 = np.concatenate([[0], np.cumsum(b1)]).astype(np.int64)
@@ -336,6 +350,11 @@ def _demux_pair(dmx, pool, gz, i1, i2, read1_file, read2_file, results, route_of
                         pending.append(pool.submit(w["R1"].write_from, o1, int(c1[k]), int(c1[k + 1])))
                     if b2[k]:
                         pending.append(pool.submit(w["R2"].write_from, o2, int(c2[k]), int(c2[k + 1])))
+            t5 = clock()
+            for k, v in (("inflate+join", t1 - t0), ("load+index", t2 - t1), ("route", t3 - t2), ("deflate/fetch", t4 - t3),
+                         ("wait writers", t5 - t4)):
+                st[k] = st.get(k, 0.0) + v
+            st["windows"] = st.get("windows", 0) + 1
             # carry the bytes after the routed records
             cut = []
             for m in (0, 1):
@@ -426,7 +445,8 @@ def frender_demux(args, dev=None) -> None:
                             infix, kind)
     dmx = dev or _lib.Demux(_device_index(None))
     pool = ThreadPoolExecutor(max_workers=max(2, min(32, len(writers) * 2)))
-    gz = _lib.GzPool([str(f) for pr in pairs for f in pr], threads=4)
+    # with the GPU compressing, the host's cores inflate (a big single-member file in parallel)
+    gz = _lib.GzPool([str(f) for pr in pairs for f in pr], threads=_inflate_threads(kind), ahead=4)
     try:
         dmx.set_table(keys[fast], vals[fast])
         for k, (read1_file, read2_file) in enumerate(pairs):
@@ -440,6 +460,8 @@ def frender_demux(args, dev=None) -> None:
                 f.close()
         if dev is None:
             dmx.close()
+        if getattr(args, "stage_times", False):
+            print(json.dumps({k: round(v, 3) for k, v in STAGE_TIMES.items()}), file=sys.stderr)
 
 
 # ---- demux --gpus N ------------------------------------------------------------------------------
@@ -450,6 +472,16 @@ def frender_demux(args, dev=None) -> None:
 # concatenation is a valid gzip stream whose text is the concatenation of the pairs' texts: the
 # reference's file content.  The first failing pair (in pair order) decides the error, raised by the
 # rank that met it, after rank 0 has written the pairs up to it.
+
+def _inflate_threads(kind) -> int:
+    """Inflate threads of the demux's GzPool: 4 beside host compressors; with the GPU writers, the
+    process's CPUs up to 16.  The pool inflates 4 files at once (this pair's mates and the next
+    pair's), each big single-member file split over its share of the threads."""
+    if kind is not _GzDevice:
+        return 4
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 4)
+    return max(4, min(16, n))
+
 
 def _device_index(group) -> int:
     """This rank's GPU: LOCAL_RANK, folded onto the visible GPUs for gloo rehearsals on one GPU."""
@@ -492,7 +524,7 @@ def _demux_ranks(group, args, dev, pairs, results, route_of, keys, vals, names, 
     failed, exc = len(pairs), None
     try:
         # opened inside the try: a rank whose pool or device fails still joins the collectives below
-        gz = _lib.GzPool([str(f) for k in mine for f in pairs[k]], threads=4)
+        gz = _lib.GzPool([str(f) for k in mine for f in pairs[k]], threads=_inflate_threads(kind), ahead=4)
         dmx = _lib.Demux(_device_index(group))
         dmx.set_table(keys, vals)
         for j, k in enumerate(mine):

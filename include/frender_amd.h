@@ -155,6 +155,9 @@ int fr_feed(fr_ctx* ctx, const uint8_t* data, uint64_t len);
  * caller re-reads the file with Python's gzip to raise the reference's exception). */
 typedef struct fr_gz fr_gz;
 fr_gz* fr_gz_open(const char* const* paths, int n_files, int threads);
+/* the same with at most files_ahead files inflating at once: the other threads help split the big
+ * single-member files among them (the demux reads a file pair at a time) */
+fr_gz* fr_gz_open_ahead(const char* const* paths, int n_files, int threads, int files_ahead);
 int fr_gz_feed(fr_gz* g, int i, fr_ctx* ctx);
 /* The consumer-side alternative to fr_gz_feed (demux reads R1 and R2 in lockstep): the next decoded
  * block of file i.  *data / *len stay valid until the next fr_gz_next or fr_gz_close on the pool;

@@ -43,6 +43,7 @@ uint32_t encode_block(const uint8_t* buf, uint64_t start, uint32_t len, uint32_t
                       const Params& P, std::vector<uint32_t>& m, std::vector<uint16_t>& choice,
                       std::vector<uint32_t>& best) {
     const uint8_t* blk = buf + start;
+    const Lay ly{m.data(), choice.data()};
     const uint64_t hs = start - hist;
     const uint32_t ntot = hist + len;
     static uint16_t tab[(1u << HBITS) * WAYS];
@@ -59,7 +60,7 @@ uint32_t encode_block(const uint8_t* buf, uint64_t start, uint32_t len, uint32_t
             if (r >= hist) bhist[buf[p]]++;
             const bool valid = r + HLEN <= ntot;
             if (!valid) {
-                if (r >= hist) m[r - hist] = 0;
+                if (r >= hist) ly.rec(r - hist) = mpack(buf[p], 0, 0);
                 continue;
             }
             const uint32_t w = load32u(buf + p);
@@ -67,33 +68,17 @@ uint32_t encode_block(const uint8_t* buf, uint64_t start, uint32_t len, uint32_t
             hsh[t] = h;
             if (r < hist) continue;
             const uint32_t maxlen = (ntot - r) < MAXM ? (ntot - r) : MAXM;
-            uint32_t bl = 0, bd = 0;
-            uint32_t cand[WAYS + 1];
-            for (uint32_t s = 0; s < WAYS; ++s) cand[s] = tab[h * WAYS + s];
-            cand[WAYS] = r;  // none
+            uint32_t dds[WAYS + 1];
+            for (uint32_t s = 0; s < WAYS; ++s) dds[s] = (r - tab[h * WAYS + s]) & 0xFFFF;
+            dds[WAYS] = 0;
             for (uint32_t u = t; u-- > 0;)  // the latest earlier lane of the batch with the same hash
                 if (hsh[u] == h) {
-                    cand[WAYS] = base + u;
+                    dds[WAYS] = t - u;
                     break;
                 }
-            for (uint32_t s = 0; s <= WAYS; ++s) {
-                const uint32_t dd = (r - cand[s]) & 0xFFFF;
-                if (dd == 0 || dd > WIN || dd > r) continue;
-                const uint8_t* c = buf + p - dd;
-                if (load32u(c) != w) continue;
-                uint32_t l = 4;
-                while (l < maxlen) {
-                    const uint32_t x = load32u(buf + p + l) ^ load32u(c + l);
-                    if (x) {
-                        l += (uint32_t)__builtin_ctz(x) >> 3;
-                        break;
-                    }
-                    l += 4;
-                }
-                if (l > maxlen) l = maxlen;
-                if (l > bl || (l == bl && dd < bd)) bl = l, bd = dd;
-            }
-            m[r - hist] = bl >= MINM ? (bl | (bd << 16)) : 0;
+            uint32_t bl, bd;
+            best_match<WAYS + 1>(buf + p, w, dds, r, maxlen, load32u, bl, bd);
+            ly.rec(r - hist) = mpack(buf[p], bl >= MINM ? bl : 0, bd);
         }
         for (uint32_t t = 0; t < TPB; ++t)
             if (hsh[t] != ~0u) tab[hsh[t] * WAYS + t * WAYS / TPB] = (uint16_t)(base + t);
@@ -120,14 +105,14 @@ uint32_t encode_block(const uint8_t* buf, uint64_t start, uint32_t len, uint32_t
     for (int pass = 0; pass < P.passes; ++pass) {
         for (uint32_t s = 0; s < nsub; ++s) {
             const uint32_t a = s * SUB, b = (s + 1) * SUB < len ? (s + 1) * SUB : len;
-            parse_range(blk, a, b, m.data(), choice.data(), best.data() + s * (SUB + 1), c);
+            parse_range(a, b, ly, Ring{best.data(), 0}, c);
         }
         memset(llf, 0, sizeof llf);
         memset(df, 0, sizeof df);
         llf[256] = 1;
         for (uint32_t s = 0; s < nsub; ++s) {
             const uint32_t a = s * SUB, b = (s + 1) * SUB < len ? (s + 1) * SUB : len;
-            count_range(blk, a, b, m.data(), choice.data(), llf, df, add);
+            count_range(a, b, ly, llf, df, add);
         }
         huff_gather(llf, NLL, hw);
         huff_sort(hw);
@@ -164,10 +149,10 @@ uint32_t encode_block(const uint8_t* buf, uint64_t start, uint32_t len, uint32_t
         uint64_t off = hdr;
         for (uint32_t s = 0; s < nsub; ++s) {
             const uint32_t a = s * SUB, b = (s + 1) * SUB < len ? (s + 1) * SUB : len;
-            const uint64_t nb = range_bits(blk, a, b, m.data(), choice.data(), T);
+            const uint64_t nb = range_bits(a, b, ly, T);
             BitW lw;
             lw.init(words, off);
-            write_range(blk, a, b, m.data(), choice.data(), T, lw, orf);
+            write_range(a, b, ly, T, lw, orf);
             lw.flush(orf);
             off += nb;
         }
@@ -209,9 +194,9 @@ uint64_t frd_host_deflate(const uint8_t* in, uint64_t n, uint8_t* out, uint64_t 
     for (uint64_t i = 0; i < n; ++i) cr = crc_tab[(cr ^ in[i]) & 255] ^ (cr >> 8);
     *crc = ~cr;
     Params P{passes, len_init, dist_init};
-    std::vector<uint32_t> m(BLOCK + 8);
-    std::vector<uint16_t> choice(BLOCK + 8);
-    std::vector<uint32_t> best(NSUB * (SUB + 1));
+    std::vector<uint32_t> m(BLOCK);
+    std::vector<uint16_t> choice(BLOCK);
+    std::vector<uint32_t> best(256);
     std::vector<uint8_t> padded(n + 16, 0);
     if (n) memcpy(padded.data(), in, n);
     std::vector<uint8_t> blkout(OUT_STRIDE);

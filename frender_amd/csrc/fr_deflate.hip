@@ -40,7 +40,7 @@ namespace {
 using namespace frd;
 
 constexpr uint32_t TPB = 256;
-constexpr uint32_t NPASS = 4;
+constexpr uint32_t NPASS = 3;
 constexpr uint32_t NB = 1u << HBITS;
 constexpr uint64_t SCR_BYTES = (uint64_t)BLOCK * 4 + (uint64_t)BLOCK * 2 + 256;
 static_assert(NSUB * 256 <= NB * WAYS / 2, "the parse rings live in the matchfinder table");
@@ -59,6 +59,7 @@ struct DefShared {
         uint32_t stage[NB * WAYS / 2];  // then the block's output bits
     };
     alignas(8) uint16_t bh[TPB];  // this batch's hashes (0xFFFF: none)
+    uint32_t seen[2][2][128];     // per batch parity: hashes (>> 1) seen once / again in the batch
     uint32_t bhist[256];
     uint32_t llf[NLL];
     uint32_t df[NDIST];
@@ -158,6 +159,8 @@ __global__ __launch_bounds__(TPB, 2) void deflate_blocks(const uint8_t* __restri
         const uint8_t* hsp = blk - hist;
         for (uint32_t i = t; i < NB * WAYS / 2; i += TPB) S.stage[i] = 0;
         S.bhist[t] = 0;
+        S.seen[t >> 7][0][t & 127] = 0;
+        S.seen[t >> 7][1][t & 127] = 0;
         __syncthreads();
         // ---- matchfinder
         for (uint32_t base = 0; base < ntot; base += TPB) {
@@ -171,7 +174,13 @@ __global__ __launch_bounds__(TPB, 2) void deflate_blocks(const uint8_t* __restri
                 }
             }
             S.bh[t] = (uint16_t)h;
+            const uint32_t par = (base / TPB) & 1;
+            if (h != 0xFFFF) {
+                const uint32_t bit = 1u << ((h >> 1) & 31), wi = h >> 6;
+                if (atomicOr(&S.seen[par][0][wi], bit) & bit) atomicOr(&S.seen[par][1][wi], bit);
+            }
             __syncthreads();
+            S.seen[par ^ 1][t >> 7][t & 127] = 0;  // the other parity's maps, for the next batch
             if (r >= hist && r < ntot) {
                 uint32_t bl = 0, bd = 0;
                 if (h != 0xFFFF) {
@@ -179,22 +188,23 @@ __global__ __launch_bounds__(TPB, 2) void deflate_blocks(const uint8_t* __restri
                     uint32_t dds[WAYS + 1];
                     for (uint32_t s = 0; s < WAYS; ++s) dds[s] = (r - S.tab[h * WAYS + s]) & 0xFFFF;
                     dds[WAYS] = 0;
-                    {  // the latest earlier lane of the batch with the same hash, four hashes per LDS read
+                    if (S.seen[par][1][h >> 6] >> ((h >> 1) & 31) & 1) {
+                        // another lane of the batch may share the hash: the latest earlier one,
+                        // sixteen hashes (four independent LDS reads) per step
                         const uint64_t hh = (uint64_t)h * 0x0001000100010001ull;
                         const uint64_t* bw = (const uint64_t*)S.bh;
-                        for (int wi = ((int)t - 1) >> 2; wi >= 0; --wi) {
-                            const uint64_t v = bw[wi] ^ hh;
-                            uint32_t u = ~0u;
-                            for (int q = 3; q >= 0; --q)
-                                if ((uint32_t)(4 * wi + q) < t && ((v >> (16 * q)) & 0xFFFF) == 0) {
-                                    u = 4 * wi + q;
+                        uint32_t u = ~0u;
+                        for (int g = ((int)t - 1) >> 4; g >= 0 && u == ~0u; --g) {
+                            uint64_t v[4];
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) v[q] = bw[4 * g + q] ^ hh;
+                            for (int e = 15; e >= 0; --e)
+                                if ((uint32_t)(16 * g + e) < t && ((v[e >> 2] >> (16 * (e & 3))) & 0xFFFF) == 0) {
+                                    u = 16 * g + e;
                                     break;
                                 }
-                            if (u != ~0u) {
-                                dds[WAYS] = t - u;
-                                break;
-                            }
                         }
+                        if (u != ~0u) dds[WAYS] = t - u;
                     }
                     best_match<WAYS + 1>(hsp + r, w, dds, r, maxlen, Ld32{}, bl, bd);
                 }
@@ -219,9 +229,9 @@ __global__ __launch_bounds__(TPB, 2) void deflate_blocks(const uint8_t* __restri
             for (uint32_t l = t; l <= MAXM; l += TPB) {
                 uint32_t idx = 0, eb = 0, ev;
                 if (l >= 3) len_code(l, idx, eb, ev);
-                S.cost.len[l] = l < 3 ? 0 : (uint16_t)(CF * (3 + eb));
+                S.cost.len[l] = l < 3 ? 0 : (uint16_t)(CF * (2 + eb));
             }
-            if (t < NDIST) S.cost.dist[t] = (uint16_t)(CF * (3 + dist_ebits(t)));
+            if (t < NDIST) S.cost.dist[t] = (uint16_t)(CF * (2 + dist_ebits(t)));
         }
         __syncthreads();
         uint32_t crc = 0;
@@ -496,7 +506,7 @@ int fr_defl_run(fr_defl* z, const uint8_t* dev_data, const uint64_t* offsets, in
             DJob j{};
             j.start = x;
             j.len = (uint32_t)std::min<uint64_t>(BLOCK, b - x);
-            j.hist = (uint32_t)std::min<uint64_t>(WIN, x - a);
+            j.hist = (uint32_t)std::min<uint64_t>(HIST, x - a);
             j.last = x + BLOCK >= b;
             z->hjobs.push_back(j);
         }

@@ -19,7 +19,8 @@
 namespace frd {
 
 constexpr uint32_t BLOCK = 1u << 16;   // input bytes per deflate block (one workgroup)
-constexpr uint32_t WIN = 32768;        // deflate window: history a block may reference
+constexpr uint32_t WIN = 32768;        // deflate window
+constexpr uint32_t HIST = WIN;         // bytes of its stream before a block that the block may reference
 #ifndef FRD_SUB
 #define FRD_SUB 1024
 #endif
@@ -249,20 +250,38 @@ FRD_HD void best_match(const uint8_t* p, uint32_t w, const uint32_t* dds, uint32
     }
 }
 
+// Four words held in registers (a named struct, never indexed: an array indexed by a variable would
+// live in scratch memory)
+struct Q4 {
+    uint32_t v0, v1, v2, v3;
+};
+FRD_HD uint32_t sel4(const Q4& a, uint32_t j) {  // by shifts: a select of fields is turned back into an index
+    const uint64_t lo = (uint64_t)a.v1 << 32 | a.v0, hi = (uint64_t)a.v3 << 32 | a.v2;
+    return (uint32_t)(((j & 2) ? hi : lo) >> ((j & 1) * 32));
+}
+FRD_HD void or4(Q4& a, uint32_t j, uint32_t v) {
+    a.v0 |= j == 0 ? v : 0u;
+    a.v1 |= j == 1 ? v : 0u;
+    a.v2 |= j == 2 ? v : 0u;
+    a.v3 |= j == 3 ? v : 0u;
+}
+
 // 16-byte loads and stores of the per-lane arrays (16-byte aligned chunks)
-FRD_HD void ld16(const void* p, uint32_t* w) {
+FRD_HD Q4 ld16(const void* p) {
 #if defined(__HIP_DEVICE_COMPILE__)
     const uint4 v = *(const uint4*)p;
-    w[0] = v.x, w[1] = v.y, w[2] = v.z, w[3] = v.w;
+    return Q4{v.x, v.y, v.z, v.w};
 #else
-    memcpy(w, p, 16);
+    Q4 q;
+    memcpy(&q, p, 16);
+    return q;
 #endif
 }
-FRD_HD void st16(void* p, const uint32_t* w) {
+FRD_HD void st16(void* p, const Q4& q) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    *(uint4*)p = make_uint4(w[0], w[1], w[2], w[3]);
+    *(uint4*)p = make_uint4(q.v0, q.v1, q.v2, q.v3);
 #else
-    memcpy(p, w, 16);
+    memcpy(p, &q, 16);
 #endif
 }
 
@@ -295,24 +314,29 @@ constexpr uint32_t PARSE_MAXL = 255;  // the ring holds best[i + 1 .. i + 255]: 
 FRD_HD void parse_range(uint32_t a, uint32_t b, const Lay& ly, const Ring& best, const Costs& c) {
     if (b <= a) return;
     best.at(b - a) = 0;
-    uint32_t cur[4], nxt[4] = {0, 0, 0, 0}, wbuf[4] = {0, 0, 0, 0};
-    uint32_t cc = (b - 1) >> 2, wc = (b - 1) >> 3;
-    ld16(ly.mchunk(4 * cc), cur);
-    if (cc > (a >> 2)) ld16(ly.mchunk(4 * (cc - 1)), nxt);
+    // records 4 per load, three chunks (12 positions) ahead of the one in use
+    const Q4 z{0, 0, 0, 0};
+    Q4 q0, q1 = z, q2 = z, q3 = z, wbuf = z;
+    const uint32_t c0 = a >> 2;
+    uint32_t cc = (b - 1) >> 2, wc = (b - 1) >> 3, next_best = 0;
+    q0 = ld16(ly.mchunk(4 * cc));
+    if (cc >= c0 + 1) q1 = ld16(ly.mchunk(4 * (cc - 1)));
+    if (cc >= c0 + 2) q2 = ld16(ly.mchunk(4 * (cc - 2)));
+    if (cc >= c0 + 3) q3 = ld16(ly.mchunk(4 * (cc - 3)));
     for (uint32_t i = b; i-- > a;) {
         if ((i >> 2) != cc) {
             cc = i >> 2;
-            for (int q = 0; q < 4; ++q) cur[q] = nxt[q];
-            if (cc > (a >> 2)) ld16(ly.mchunk(4 * (cc - 1)), nxt);
+            q0 = q1, q1 = q2, q2 = q3;
+            if (cc >= c0 + 3) q3 = ld16(ly.mchunk(4 * (cc - 3)));
         }
         if ((i >> 3) != wc) {
             st16(ly.cchunk(8 * wc), wbuf);
-            for (int q = 0; q < 4; ++q) wbuf[q] = 0;
+            wbuf = z;
             wc = i >> 3;
         }
         const uint32_t k = i - a;
-        const uint32_t mi = cur[i & 3];
-        uint32_t bc = best.at(k + 1) + c.lit[m_byte(mi)];
+        const uint32_t mi = sel4(q0, i & 3);
+        uint32_t bc = next_best + c.lit[m_byte(mi)];  // best(k + 1) is the previous step's result
         uint32_t ch = 0;
         uint32_t L = m_len(mi);
         if (L > b - i) L = b - i;
@@ -344,30 +368,35 @@ FRD_HD void parse_range(uint32_t a, uint32_t b, const Lay& ly, const Ring& best,
             }
         }
         best.at(k) = bc;
-        wbuf[(i >> 1) & 3] |= ch << ((i & 1) * 16);
+        next_best = bc;
+        or4(wbuf, (i >> 1) & 3, ch << ((i & 1) * 16));
     }
     st16(ly.cchunk(8 * wc), wbuf);
 }
 
 // Forward walk of a lane's parse: choices 8 and records 4 per load
-struct Fwd {
+struct Fwd {  // the next chunk of each array is loaded when the walk enters one (chunks stay in the lane)
     Lay ly;
-    uint32_t cc, mc;
-    uint32_t cw[4], mw[4];
-    FRD_HD Fwd(const Lay& l) : ly(l), cc(~0u), mc(~0u) {}
+    uint32_t end, cc, mc;
+    Q4 cw, cn, mw, mn;
+    FRD_HD Fwd(const Lay& l, uint32_t b) : ly(l), end(b), cc(0xFFFFFFF0u), mc(0xFFFFFFF0u) {}  // no chunk yet
     FRD_HD uint32_t choice(uint32_t i) {
-        if ((i >> 3) != cc) {
-            cc = i >> 3;
-            ld16(ly.cchunk(i), cw);
+        const uint32_t c = i >> 3;
+        if (c != cc) {
+            cw = c == cc + 1 ? cn : ld16(ly.cchunk(i));
+            cc = c;
+            if (8 * (c + 1) < end) cn = ld16(ly.cchunk(8 * (c + 1)));
         }
-        return (cw[(i >> 1) & 3] >> ((i & 1) * 16)) & 0xFFFF;
+        return (sel4(cw, (i >> 1) & 3) >> ((i & 1) * 16)) & 0xFFFF;
     }
     FRD_HD uint32_t rec(uint32_t i) {
-        if ((i >> 2) != mc) {
-            mc = i >> 2;
-            ld16(ly.mchunk(i), mw);
+        const uint32_t c = i >> 2;
+        if (c != mc) {
+            mw = c == mc + 1 ? mn : ld16(ly.mchunk(i));
+            mc = c;
+            if (4 * (c + 1) < end) mn = ld16(ly.mchunk(4 * (c + 1)));
         }
-        return mw[i & 3];
+        return sel4(mw, i & 3);
     }
 };
 
@@ -494,7 +523,7 @@ FRD_HD void write_header(const Tables& t, bool final_block, BitW& bw, OR orf) {
 // body bits of [a, b) under the parse in choice[] and the final tables
 FRD_HD uint64_t range_bits(uint32_t a, uint32_t b, const Lay& ly, const Tables& t) {
     uint64_t bits = 0;
-    Fwd f(ly);
+    Fwd f(ly, b);
     for (uint32_t i = a; i < b;) {
         const uint32_t ch = f.choice(i), v = f.rec(i);
         if (ch >= MINM) {
@@ -513,7 +542,7 @@ FRD_HD uint64_t range_bits(uint32_t a, uint32_t b, const Lay& ly, const Tables& 
 
 template <class OR>
 FRD_HD void write_range(uint32_t a, uint32_t b, const Lay& ly, const Tables& t, BitW& bw, OR orf) {
-    Fwd f(ly);
+    Fwd f(ly, b);
     for (uint32_t i = a; i < b;) {
         const uint32_t ch = f.choice(i), v = f.rec(i);
         if (ch >= MINM) {
@@ -535,7 +564,7 @@ FRD_HD void write_range(uint32_t a, uint32_t b, const Lay& ly, const Tables& t, 
 // symbol counts of [a, b) under the parse in choice[]
 template <class ADD>
 FRD_HD void count_range(uint32_t a, uint32_t b, const Lay& ly, uint32_t* llf, uint32_t* df, ADD add) {
-    Fwd f(ly);
+    Fwd f(ly, b);
     for (uint32_t i = a; i < b;) {
         const uint32_t ch = f.choice(i), v = f.rec(i);
         if (ch >= MINM) {

@@ -71,7 +71,10 @@ uint32_t encode_block(const uint8_t* buf, uint64_t start, uint32_t len, uint32_t
             uint32_t dds[WAYS + 1];
             for (uint32_t s = 0; s < WAYS; ++s) dds[s] = (r - tab[h * WAYS + s]) & 0xFFFF;
             dds[WAYS] = 0;
-            for (uint32_t u = t; u-- > 0;)  // the latest earlier lane of the batch with the same hash
+#ifndef FRD_INTRA_LO
+#define FRD_INTRA_LO(t) 0
+#endif
+            for (uint32_t u = t; u-- > FRD_INTRA_LO(t);)  // the latest earlier lane of the batch with the same hash
                 if (hsh[u] == h) {
                     dds[WAYS] = t - u;
                     break;
@@ -205,7 +208,7 @@ uint64_t frd_host_deflate(const uint8_t* in, uint64_t n, uint8_t* out, uint64_t 
     for (uint64_t b = 0; b < nb; ++b) {
         const uint64_t s = b * BLOCK;
         const uint32_t len = (uint32_t)(n - s < BLOCK ? n - s : BLOCK);
-        const uint32_t hist = (uint32_t)(s < WIN ? s : WIN);
+        const uint32_t hist = (uint32_t)(s < HIST ? s : HIST);
         const uint32_t k = encode_block(padded.data(), s, len, hist, b + 1 == nb, blkout.data(), P, m, choice, best);
         if (!k || o + k > cap) return 0;
         memcpy(out + o, blkout.data(), k);

@@ -26,10 +26,10 @@ def build_host(tmp_dir) -> ctypes.CDLL:
 
 
 def host_deflate(lib, data: bytes) -> tuple:
-    """(raw deflate stream, crc32) with the kernel's settings: 4 passes, pass-1 length/distance 3 bits."""
+    """(raw deflate stream, crc32) with the kernel's settings: 3 passes, pass-1 length/distance 2 bits."""
     out = ctypes.create_string_buffer(len(data) + len(data) // 64 + 1024)
     crc = ctypes.c_uint32()
-    k = lib.frd_host_deflate(data, len(data), out, len(out), 4, 3, 3, ctypes.byref(crc))
+    k = lib.frd_host_deflate(data, len(data), out, len(out), 3, 2, 2, ctypes.byref(crc))
     assert k, "host build: output bound or bit accounting failed"
     return out.raw[:k], crc.value
 

@@ -77,7 +77,7 @@ def parse():
     ap.add_argument("--tuning", default="",
                     help="A/B runs only: fr_tuning fields for the bench's context, e.g. 'log_min=0,chunk_tiles=400' "
                          "(results never change; a tuned run reports them in config.tuning)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r04.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r05.json"),
                     help="per-launch HBM bytes of the tally kernel from rocprofv3 PMC (scripts/make_traffic.py); "
                          "used only when taken on this source tree and this launch shape, else traffic is null")
     return ap.parse_args()

@@ -146,6 +146,7 @@ _SIGS = {
     "fr_dmx_patch": (C.c_int, [P, P, P, C.c_uint64]),
     "fr_dmx_route": (C.c_int, [P, C.c_int, C.c_uint64, C.POINTER(C.c_int64), C.POINTER(C.c_int32), P, P]),
     "fr_dmx_fetch": (C.c_int, [P, C.c_int, P, C.c_uint64]),
+    "fr_dmx_load_parts": (C.c_int, [P, C.c_int, P, P, C.c_int, C.POINTER(C.c_uint64)]),
     "fr_dmx_deflate": (C.c_int, [P, C.c_int, C.c_int, P, P]),
     "fr_dmx_fetch_deflated": (C.c_int, [P, C.c_int, P, C.c_uint64]),
     "fr_defl_create": (P, [C.c_int]),
@@ -429,6 +430,14 @@ class Demux:
         a = np.frombuffer(data, dtype=np.uint8)
         n = C.c_uint64()
         self._ck(lib.fr_dmx_load(self.h, mate, _ptr(a), a.size, C.byref(n)), "fr_dmx_load")
+        return n.value
+
+    def load_parts(self, mate: int, parts) -> int:
+        """load() of the concatenation of a list of bytes objects, without joining them on the host."""
+        ptrs = (C.c_void_p * max(len(parts), 1))(*[C.cast(C.c_char_p(p), C.c_void_p) for p in parts])
+        lens = np.array([len(p) for p in parts] or [0], dtype=np.uint64)
+        n = C.c_uint64()
+        self._ck(lib.fr_dmx_load_parts(self.h, mate, ptrs, _ptr(lens), len(parts), C.byref(n)), "fr_dmx_load_parts")
         return n.value
 
     def load_device(self, mate: int, dev_ptr: int, nbytes: int) -> int:

@@ -489,6 +489,21 @@ int fr_dmx_load(fr_dmx* d, int mate, const uint8_t* data, uint64_t len, uint64_t
     return dmx_index_mate(d, mate, d->data[mate], len, n_records);
 }
 
+int fr_dmx_load_parts(fr_dmx* d, int mate, const uint8_t* const* parts, const uint64_t* lens, int n_parts,
+                      uint64_t* n_records) {
+    if (mate < 0 || mate > 1 || n_parts < 0) return d->err = "mate must be 0 (R1) or 1 (R2)", FR_ERR_INVALID;
+    DK(hipSetDevice(d->device));
+    u64 len = 0;
+    for (int k = 0; k < n_parts; ++k) len += lens[k];
+    DK(ensure(&d->data[mate], d->cap[mate], len + 16));
+    u64 off = 0;
+    for (int k = 0; k < n_parts; ++k) {
+        if (lens[k]) DK(hipMemcpyAsync(d->data[mate] + off, parts[k], lens[k], hipMemcpyHostToDevice, d->stream));
+        off += lens[k];
+    }
+    return dmx_index_mate(d, mate, d->data[mate], len, n_records);
+}
+
 int fr_dmx_load_device(fr_dmx* d, int mate, const uint8_t* dev_data, uint64_t len, uint64_t* n_records) {
     if (mate < 0 || mate > 1) return d->err = "mate must be 0 (R1) or 1 (R2)", FR_ERR_INVALID;
     if (((uintptr_t)dev_data & 15u) != 0) return d->err = "device data must be 16-byte aligned", FR_ERR_INVALID;

@@ -260,9 +260,35 @@ def read_text(path) -> bytes:
     return b"".join(text_chunks(path))
 
 
-def _line_at(data: bytes, start: int) -> bytes:
-    e = data.find(b"\n", start)
-    return data[start:] if e < 0 else data[start:e]
+def _line_at(parts, start: int) -> bytes:
+    """The line that starts at byte `start` of the concatenation of `parts` (without its '\n')."""
+    for k, p in enumerate(parts):
+        if start >= len(p):
+            start -= len(p)
+            continue
+        e = p.find(b"\n", start)
+        if e >= 0:
+            return p[start:e]
+        out = [p[start:]]
+        break
+    else:
+        return b""
+    for q in parts[k + 1:]:
+        e = q.find(b"\n")
+        if e >= 0:
+            out.append(q[:e])
+            break
+        out.append(q)
+    return b"".join(out)
+
+
+def _tail(parts, start: int) -> list:
+    """The bytes of the concatenation of `parts` from `start` on, as parts (no copy of whole parts)."""
+    for k, p in enumerate(parts):
+        if start < len(p):
+            return ([p[start:]] if start else [p]) + parts[k + 1:]
+        start -= len(p)
+    return []
 
 
 STAGE_TIMES = {}  # seconds per stage of _demux_pair's windows (demux --stage-times prints them)
@@ -274,7 +300,7 @@ def _demux_pair(dmx, pool, gz, i1, i2, read1_file, read2_file, results, route_of
     window.  Pairing stops when either mate runs out of records (zip, frender.py:777).  The mates
     inflate on the native pool gz (files i1, i2)."""
     streams = [text_chunks(read1_file, gz, i1), text_chunks(read2_file, gz, i2)]
-    bufs = [b"", b""]
+    bufs = [[], []]  # each mate's window as a list of decoded blocks (never joined on the host)
     eof = [False, False]
     pending = []  # the previous window's gzip jobs: overlap with this window's inflate and GPU work
     st = STAGE_TIMES
@@ -283,19 +309,17 @@ def _demux_pair(dmx, pool, gz, i1, i2, read1_file, read2_file, results, route_of
         while True:
             t0 = clock()
             for m in (0, 1):
-                parts = [bufs[m]]
-                size = len(bufs[m])
+                size = sum(len(p) for p in bufs[m])
                 while size < window and not eof[m]:
                     try:
                         c = next(streams[m])
                     except StopIteration:
                         eof[m] = True
                         break
-                    parts.append(c)
+                    bufs[m].append(c)
                     size += len(c)
-                bufs[m] = b"".join(parts)
             t1 = clock()
-            n = [dmx.load(0, bufs[0]), dmx.load(1, bufs[1])]
+            n = [dmx.load_parts(0, bufs[0]), dmx.load_parts(1, bufs[1])]
             t2 = clock()
             # the last record of a window may continue in the next one unless its file ended
             done = [n[m] if eof[m] else max(n[m] - 1, 0) for m in (0, 1)]
@@ -356,14 +380,12 @@ def _demux_pair(dmx, pool, gz, i1, i2, read1_file, read2_file, results, route_of
                 st[k] = st.get(k, 0.0) + v
             st["windows"] = st.get("windows", 0) + 1
             # carry the bytes after the routed records
-            cut = []
             for m in (0, 1):
                 if n_pairs < n[m]:
                     s, _ = dmx.records(m, [n_pairs])
-                    cut.append(int(s[0]))
+                    bufs[m] = _tail(bufs[m], int(s[0]))
                 else:
-                    cut.append(len(bufs[m]))
-            bufs = [bufs[0][cut[0]:], bufs[1][cut[1]:]]
+                    bufs[m] = []
             if (eof[0] and n_pairs == n[0]) or (eof[1] and n_pairs == n[1]):
                 break
     finally:

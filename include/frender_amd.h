@@ -321,6 +321,9 @@ const char* fr_dmx_last_error(const fr_dmx* d);
 int fr_dmx_set_table(fr_dmx* d, const uint64_t* keys, const int32_t* vals, uint64_t n);
 /* mate 0 = R1, 1 = R2 (R2 also resolves every record's destination); returns the record count */
 int fr_dmx_load(fr_dmx* d, int mate, const uint8_t* data, uint64_t len, uint64_t* n_records);
+/* the same over the concatenation of n_parts host buffers (a window without a host-side join) */
+int fr_dmx_load_parts(fr_dmx* d, int mate, const uint8_t* const* parts, const uint64_t* lens, int n_parts,
+                      uint64_t* n_records);
 /* the same over bytes already resident in HBM (16-byte aligned; used in place until the next load) */
 int fr_dmx_load_device(fr_dmx* d, int mate, const uint8_t* dev_data, uint64_t len, uint64_t* n_records);
 /* byte span [start, end) of the given records of a mate (host error messages, exotic codes) */

@@ -106,7 +106,7 @@ def main():
             for r in rows(src + "/prof_trace/**/*kernel_trace.csv") if r["Kernel_Name"].startswith(KERNEL)]
     full = [d for d in durs if durs and d >= 0.7 * max(durs)]
     out = {
-        "round": int(os.environ.get("ROUND", "4")),
+        "round": int(os.environ.get("ROUND", "5")),
         "rocprof_full_launch_ms": round(sum(full) / len(full), 4) if full else None,
         "rocprof_full_launches": len(full),
         "tree_hash": source_tree_hash(),

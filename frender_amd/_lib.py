@@ -266,6 +266,28 @@ class GzError(FrenderError):
     """A .gz input the native inflate could not read (the caller replays it with Python's gzip)."""
 
 
+def inflate_ahead(paths, threads: int, budget: int = 2 << 30) -> int:
+    """Files a pool should inflate at once: as many as `threads` while their decoded sizes fit the pool's
+    2-GiB block budget, fewer for big files (whose decode then splits over the idle threads: a consumer
+    that reads the files in order otherwise waits on one thread per file).  A file's decoded size is its
+    gzip trailer's ISIZE, or 4 x its size when the trailer is smaller than the file (multi-member)."""
+    big = 0
+    for p in paths:
+        try:
+            with open(p, "rb") as f:
+                f.seek(0, os.SEEK_END)
+                n = f.tell()
+                f.seek(max(n - 4, 0))
+                isize = int.from_bytes(f.read(4), "little")
+        except OSError:
+            continue
+        big = max(big, isize if isize >= n else 4 * n)
+    if big <= 0:
+        return max(1, threads)
+    ahead = max(2, min(threads, budget // big)) if threads >= 2 else 1
+    return max(1, min(ahead, len(paths)))  # one file: every thread splits it
+
+
 class GzPool:
     """Native inflate of a scan's .gz files (fr_gz_*): `threads` host threads inflate the listed
     files in order ahead of the consumer; feed(i, ctx) hands file i's bytes to ctx.feed."""

@@ -397,6 +397,7 @@ def _demux_pair(dmx, pool, gz, i1, i2, read1_file, read2_file, results, route_of
 
 def frender_demux(args, dev=None) -> None:
     """frender.py:733-814 with the per-record loop on the GPU."""
+    t_start = time.perf_counter()
     index_hop = not args.no_index_hop
     ambiguous = not args.no_ambiguous
     undeter = not args.no_undeter
@@ -468,13 +469,17 @@ def frender_demux(args, dev=None) -> None:
     dmx = dev or _lib.Demux(_device_index(None))
     pool = ThreadPoolExecutor(max_workers=max(2, min(32, len(writers) * 2)))
     # with the GPU compressing, the host's cores inflate (a big single-member file in parallel)
-    gz = _lib.GzPool([str(f) for pr in pairs for f in pr], threads=_inflate_threads(kind), ahead=4)
+    paths = [str(f) for pr in pairs for f in pr]
+    nt = _inflate_threads(kind)
+    gz = _lib.GzPool(paths, threads=nt, ahead=_lib.inflate_ahead(paths, nt))
     try:
         dmx.set_table(keys[fast], vals[fast])
+        STAGE_TIMES["setup"] = time.perf_counter() - t_start  # results, writers, device table, pool
         for k, (read1_file, read2_file) in enumerate(pairs):
             print(f"Demultiplexing {read1_file.name}...")
             _demux_pair(dmx, pool, gz, 2 * k, 2 * k + 1, read1_file, read2_file, results, route_of, writers, window)
     finally:
+        t_end = time.perf_counter()
         gz.close()
         pool.shutdown(wait=True)
         for w in writers:
@@ -482,6 +487,8 @@ def frender_demux(args, dev=None) -> None:
                 f.close()
         if dev is None:
             dmx.close()
+        STAGE_TIMES["finish"] = time.perf_counter() - t_end  # last writes, closes
+        STAGE_TIMES["total"] = time.perf_counter() - t_start
         if getattr(args, "stage_times", False):
             print(json.dumps({k: round(v, 3) for k, v in STAGE_TIMES.items()}), file=sys.stderr)
 
@@ -497,8 +504,9 @@ def frender_demux(args, dev=None) -> None:
 
 def _inflate_threads(kind) -> int:
     """Inflate threads of the demux's GzPool: 4 beside host compressors; with the GPU writers, the
-    process's CPUs up to 16.  The pool inflates 4 files at once (this pair's mates and the next
-    pair's), each big single-member file split over its share of the threads."""
+    process's CPUs up to 16.  The pool inflates as many files at once as fit its block budget (4 of
+    the config-5 shape's 443-MB mates: this pair's and the next), each big single-member file split
+    over its share of the threads."""
     if kind is not _GzDevice:
         return 4
     n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 4)
@@ -546,7 +554,9 @@ def _demux_ranks(group, args, dev, pairs, results, route_of, keys, vals, names, 
     failed, exc = len(pairs), None
     try:
         # opened inside the try: a rank whose pool or device fails still joins the collectives below
-        gz = _lib.GzPool([str(f) for k in mine for f in pairs[k]], threads=_inflate_threads(kind), ahead=4)
+        paths = [str(f) for k in mine for f in pairs[k]]
+        nt = _inflate_threads(kind)
+        gz = _lib.GzPool(paths, threads=nt, ahead=_lib.inflate_ahead(paths, nt))
         dmx = _lib.Demux(_device_index(group))
         dmx.set_table(keys, vals)
         for j, k in enumerate(mine):

@@ -441,7 +441,8 @@ def sharded_tally(dist, ctx, files, sample, cores):
     try:
         ctx.reset()
         streamed = [k for k in range(len(mine)) if k not in bgzf and not (flags[mine[k][0]].any())]
-        pool = _lib.GzPool([files[mine[k][0]] for k in streamed], threads=max(1, int(cores)))
+        paths = [files[mine[k][0]] for k in streamed]
+        pool = _lib.GzPool(paths, threads=max(1, int(cores)), ahead=_lib.inflate_ahead(paths, max(1, int(cores))))
         slot = {k: j for j, k in enumerate(streamed)}
         for k, (fi, part, nparts) in enumerate(mine):
             if k not in bgzf and k not in slot:

@@ -121,7 +121,8 @@ def scan_files(ctx, files, indices, sample, cores, on_file=None, after_file=None
     reference's "Tallying barcodes from ..." line), after_file(i, records, new barcodes) once it is
     tallied.  Returns {i: (records, new barcodes)}."""
     out = {}
-    pool = _lib.GzPool([files[i] for i in indices], threads=max(1, int(cores)))
+    paths = [files[i] for i in indices]
+    pool = _lib.GzPool(paths, threads=max(1, int(cores)), ahead=_lib.inflate_ahead(paths, max(1, int(cores))))
     try:
         for k, fi in enumerate(indices):
             path = files[fi]

@@ -197,3 +197,29 @@ def test_parallel_single_member_errors(tmp_path, big_text, damage):
     else:
         assert decoded([p], 6) == [exp]
     assert _lib.gz_parallel_members() == before  # never the parallel decoder's output
+
+
+def test_inflate_ahead(tmp_path):
+    """Files inflating at once: all of them while their decoded sizes (gzip ISIZE) fit the 2-GiB block
+    budget, fewer for big ones, never more than the files, one file gets every thread."""
+    import gzip
+    import struct
+
+    from frender_amd import _lib
+
+    def fake(name, isize, comp=64):  # a file whose trailer claims `isize` decoded bytes
+        p = tmp_path / name
+        p.write_bytes(b"\x1f\x8b" + b"\0" * (comp - 6) + struct.pack("<I", isize))
+        return str(p)
+
+    small = [fake(f"s{i}.gz", 200 << 20) for i in range(8)]
+    assert _lib.inflate_ahead(small, 8) == 8
+    big = [fake(f"b{i}.gz", 443 << 20) for i in range(32)]
+    assert _lib.inflate_ahead(big, 16) == 4
+    assert _lib.inflate_ahead(big, 8) == 4
+    assert _lib.inflate_ahead([fake("huge.gz", 1800 << 20)], 16) == 1
+    assert _lib.inflate_ahead(big[:2], 16) == 2
+    assert _lib.inflate_ahead(big, 1) == 1
+    real = tmp_path / "real.gz"
+    real.write_bytes(gzip.compress(b"@r 1:N:0:AC+GT\nA\n+\nF\n" * 1000))
+    assert _lib.inflate_ahead([str(real)] * 3, 4) == 3

@@ -131,7 +131,7 @@ def main():
         "source": f"profiles/{tag}_pmc_chunk_kernel.csv (rocprofv3 --pmc FETCH_SIZE, then --pmc WRITE_SIZE, "
                   f"separate runs of bench.py {os.environ.get('PROF_ARGS', '--steps 5 --warmup 1 --no-cpu')})",
     }
-    with open(os.path.join(prof, os.environ.get("TRAFFIC_JSON", "traffic_r04.json")), "w") as fh:
+    with open(os.path.join(prof, os.environ.get("TRAFFIC_JSON", "traffic_r05.json")), "w") as fh:
         json.dump(out, fh, indent=1)
     print(json.dumps(out, indent=1))
 

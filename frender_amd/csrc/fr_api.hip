@@ -42,6 +42,8 @@ static void pinned_copy(u8* dst, const u8* src, u64 n) {
 
 struct fr_ctx {
     int device = 0;
+    GSlot* snap = nullptr;         // a speculative device feed's rollback copy of the table (kept between feeds)
+    u64 snap_cap = 0;
     hipStream_t stream = nullptr;  // tally / classify / table kernels
     hipStream_t copy = nullptr;    // H2D of host feeds
     std::string err;
@@ -772,7 +774,8 @@ void fr_destroy(fr_ctx* ctx) {
                    ctx->d_keys, ctx->d_counts, ctx->d_first, ctx->d_keys_s, ctx->d_counts_s,
                    ctx->d_first_s, ctx->d_pos, ctx->d_perm, ctx->d_rank, ctx->d_counter, ctx->d_temp, ctx->d_bins, ctx->d_binbase, ctx->d_arr, ctx->d_rows, ctx->d_pres_u,
                    ctx->d_pres_f, ctx->d_pres_c, ctx->d_m1, ctx->d_m2, ctx->d_row, ctx->d_rm2, ctx->d_rrow, ctx->d_cls, ctx->d_rcls,
-                   ctx->d_errw, ctx->d_errf, ctx->d_nbr, ctx->cold, ctx->rare, ctx->chunk_info, ctx->log, ctx->log_sub, ctx->log_temp};
+                   ctx->d_errw, ctx->d_errf, ctx->d_nbr, ctx->cold, ctx->rare, ctx->chunk_info, ctx->log, ctx->log_sub, ctx->log_temp,
+                   ctx->snap};
     for (void* p : dev)
         if (p) (void)hipFree(p);
     if (ctx->h_st) (void)hipHostFree(ctx->h_st);
@@ -1083,8 +1086,18 @@ int fr_feed_device(fr_ctx* ctx, const uint8_t* dev_data, uint64_t len) {
     const bool empty = saved.n_keys == 0 && saved.n_overflow == 0;
     const bool spec = ctx->spec_ok && ctx->max_records == 0 && saved.n_overflow == 0;
     GSlot* snap = nullptr;
-    if (spec && !empty) {
-        CK(dalloc(&snap, snap_slots));
+    if (spec && !empty) {  // the copy's buffer stays with the context: a feed per file would pay a synchronising free
+        if (ctx->snap_cap < snap_slots) {
+            if (ctx->snap) {
+                CK(hipStreamSynchronize(ctx->stream));
+                CK(hipFree(ctx->snap));
+                ctx->snap = nullptr;
+            }
+            ctx->snap_cap = 0;
+            CK(dalloc(&ctx->snap, snap_slots));
+            ctx->snap_cap = snap_slots;
+        }
+        snap = ctx->snap;
         CK(hipMemcpyAsync(snap, ctx->tab.slots, snap_slots * sizeof(GSlot), hipMemcpyDeviceToDevice, ctx->stream));
     }
     // Equal ranges of at most chunk_bytes: one launch (one set of ramps and tail) for the bench's 7.4 GB,
@@ -1150,10 +1163,6 @@ int fr_feed_device(fr_ctx* ctx, const uint8_t* dev_data, uint64_t len) {
         if (!room_bad) ctx->spec_replays++;
     }
     ctx->grow_sync = false;
-    if (snap) {
-        CK(hipStreamSynchronize(ctx->stream));
-        CK(hipFree(snap));
-    }
     if (rc) return rc;
     ctx->feed_keys = ctx->h_st->n_keys - saved.n_keys;
     ctx->feed_logged = ctx->h_st->log_commits != saved.log_commits;  // read_state above: exact

@@ -8,6 +8,14 @@ from datetime import datetime, timezone
 from .dist import launch_ranks
 
 
+def _single_process():
+    """One process, one GPU: the library loads without PyTorch (frender_amd/_runtime.py), unless something in
+    this process imported it already."""
+    from . import _runtime
+    if "torch" not in sys.modules:
+        _runtime.USE_TORCH = False
+
+
 def main(argv=None):
     parser = argparse.ArgumentParser(prog="frender_amd")
     sub = parser.add_subparsers()
@@ -62,6 +70,7 @@ def main(argv=None):
             return launch_ranks(args.gpus, sys.argv[1:] if argv is None else list(argv))
         if int(os.environ.get("WORLD_SIZE", "1")) > 1:
             return run_rank(args)
+        _single_process()
         from .scan import frender_scan
         frender_scan(args)
         return 0
@@ -74,6 +83,7 @@ def main(argv=None):
             return launch_ranks(args.gpus, child)
         if int(os.environ.get("WORLD_SIZE", "1")) > 1:
             return run_rank(args)
+        _single_process()
         from .demux import frender_demux
         frender_demux(args)
         return 0

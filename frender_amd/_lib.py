@@ -15,10 +15,14 @@ import os
 
 import numpy as np
 
-try:  # one HIP runtime per process (see module doc)
-    import torch  # noqa: F401
-except Exception:  # pragma: no cover - torch is plumbing only
-    torch = None
+from . import _runtime
+
+torch = None
+if _runtime.USE_TORCH:  # one HIP runtime per process (see module doc)
+    try:
+        import torch  # noqa: F401
+    except Exception:  # pragma: no cover - torch is plumbing only
+        torch = None
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FRENDER_HIP_LIB", os.path.join(HERE, "libfrender_hip.so"))

@@ -419,7 +419,7 @@ struct fr_defl {
     uint64_t* boff = nullptr;
     uint8_t *stage = nullptr, *out = nullptr, *scratch = nullptr, *in = nullptr;
     void* tmp = nullptr;
-    uint64_t c_jobs = 0, c_stage = 0, c_out = 0, c_tmp = 0, c_in = 0;
+    uint64_t c_jobs = 0, c_blen = 0, c_bcrc = 0, c_boff = 0, c_stage = 0, c_out = 0, c_tmp = 0, c_in = 0;
     uint64_t out_len = 0;
     std::vector<DJob> hjobs;
     std::vector<uint32_t> hlen, hcrc;
@@ -516,12 +516,9 @@ int fr_defl_run(fr_defl* z, const uint8_t* dev_data, const uint64_t* offsets, in
     z->out_len = 0;
     if (nj) {
         DF(grow(&z->jobs, z->c_jobs, nj));
-        uint64_t c_blen = z->c_jobs;
-        DF(grow(&z->blen, c_blen, z->c_jobs + 1));
-        uint64_t c_bcrc = z->c_jobs;
-        DF(grow(&z->bcrc, c_bcrc, z->c_jobs + 1));
-        uint64_t c_boff = z->c_jobs;
-        DF(grow(&z->boff, c_boff, z->c_jobs + 1));
+        DF(grow(&z->blen, z->c_blen, nj + 1));  // grow-only: a window's buffers serve the next ones
+        DF(grow(&z->bcrc, z->c_bcrc, nj + 1));
+        DF(grow(&z->boff, z->c_boff, nj + 1));
         DF(grow(&z->stage, z->c_stage, nj * OUT_STRIDE));
         DF(hipMemcpyAsync(z->jobs, z->hjobs.data(), nj * sizeof(DJob), hipMemcpyHostToDevice, z->stream));
         const uint32_t g = (uint32_t)std::min<uint64_t>(nj, (uint64_t)z->grid);

@@ -308,34 +308,23 @@ constexpr uint32_t PARSE_MAXL = 255;  // the ring holds best[i + 1 .. i + 255]: 
 // Backward cost-minimising parse of [a, b) (block-relative; a a multiple of 8).  m[i] = mpack record
 // of i; choice[i] = 0 (literal) or the match length taken at i, written 8 at a time (a chunk past b
 // is overwritten: no lane owns those positions).  Matches end at b: a lane's sub-range is parsed on
-// its own.  m is read 4 positions per load, the next chunk one chunk ahead.  The lengths tried at a
-// match: all of 4..10, or 4..8 and the last three of a longer one (trying every length changed the
-// FASTQ shapes' streams by < 0.01%).
+// its own.  m is read 4 positions per load, three chunks (12 positions) ahead of the one in use, into
+// four register slots that keep their roles (the walk is unrolled by four chunks: rotating the slots
+// by copies made every position wait for the load in flight; a store in the position loop made the
+// compiler wait for every load before it).  The lengths tried at a match: all of
+// 4..10, or 4..8 and the last three of a longer one (trying every length changed the FASTQ shapes'
+// streams by < 0.01%).
 FRD_HD void parse_range(uint32_t a, uint32_t b, const Lay& ly, const Ring& best, const Costs& c) {
     if (b <= a) return;
     best.at(b - a) = 0;
-    // records 4 per load, three chunks (12 positions) ahead of the one in use
-    const Q4 z{0, 0, 0, 0};
-    Q4 q0, q1 = z, q2 = z, q3 = z, wbuf = z;
+    Q4 wbuf{0, 0, 0, 0};
     const uint32_t c0 = a >> 2;
-    uint32_t cc = (b - 1) >> 2, wc = (b - 1) >> 3, next_best = 0;
-    q0 = ld16(ly.mchunk(4 * cc));
-    if (cc >= c0 + 1) q1 = ld16(ly.mchunk(4 * (cc - 1)));
-    if (cc >= c0 + 2) q2 = ld16(ly.mchunk(4 * (cc - 2)));
-    if (cc >= c0 + 3) q3 = ld16(ly.mchunk(4 * (cc - 3)));
-    for (uint32_t i = b; i-- > a;) {
-        if ((i >> 2) != cc) {
-            cc = i >> 2;
-            q0 = q1, q1 = q2, q2 = q3;
-            if (cc >= c0 + 3) q3 = ld16(ly.mchunk(4 * (cc - 3)));
-        }
-        if ((i >> 3) != wc) {
-            st16(ly.cchunk(8 * wc), wbuf);
-            wbuf = z;
-            wc = i >> 3;
-        }
+    uint32_t cc = (b - 1) >> 2, next_best = 0, i = b;
+    // chunk cc - d, or the range's first chunk past it (loaded, never used: every slot loads)
+    auto ldc = [&](uint32_t d) { return ld16(ly.mchunk(4 * (cc >= c0 + d ? cc - d : c0))); };
+    Q4 qa = ldc(0), qb = ldc(1), qc = ldc(2), qd = ldc(3);
+    auto pos = [&](uint32_t mi) {  // position i (already decremented) with its record mi
         const uint32_t k = i - a;
-        const uint32_t mi = sel4(q0, i & 3);
         uint32_t bc = next_best + c.lit[m_byte(mi)];  // best(k + 1) is the previous step's result
         uint32_t ch = 0;
         uint32_t L = m_len(mi);
@@ -370,35 +359,67 @@ FRD_HD void parse_range(uint32_t a, uint32_t b, const Lay& ly, const Ring& best,
         best.at(k) = bc;
         next_best = bc;
         or4(wbuf, (i >> 1) & 3, ch << ((i & 1) * 16));
+    };
+    auto chunk = [&](Q4& q) {  // the positions of chunk cc left, then q takes chunk cc - 4
+        for (const uint32_t lo = 4 * cc; i > lo;) {
+            --i;
+            pos(sel4(q, i & 3));
+        }
+        if (!(cc & 1)) {  // the choices of 8 positions (outside the loop above, which stays free of
+            st16(ly.cchunk(4 * cc), wbuf);  // memory operations: no wait for the slots' loads there)
+            wbuf = Q4{0, 0, 0, 0};
+        }
+        if (cc == c0) return false;
+        q = ldc(4);
+        --cc;
+        return true;
+    };
+    while (cc >= c0 + 4) {  // four chunks with no exit among them (the compiler's waits stay counted)
+        chunk(qa), chunk(qb), chunk(qc), chunk(qd);
     }
-    st16(ly.cchunk(8 * wc), wbuf);
+    (void)(chunk(qa) && chunk(qb) && chunk(qc) && chunk(qd));  // the last 1..4
 }
 
-// Forward walk of a lane's parse: choices 8 and records 4 per load
-struct Fwd {  // the next chunk of each array is loaded when the walk enters one (chunks stay in the lane)
-    Lay ly;
-    uint32_t end, cc, mc;
-    Q4 cw, cn, mw, mn;
-    FRD_HD Fwd(const Lay& l, uint32_t b) : ly(l), end(b), cc(0xFFFFFFF0u), mc(0xFFFFFFF0u) {}  // no chunk yet
-    FRD_HD uint32_t choice(uint32_t i) {
-        const uint32_t c = i >> 3;
-        if (c != cc) {
-            cw = c == cc + 1 ? cn : ld16(ly.cchunk(i));
-            cc = c;
-            if (8 * (c + 1) < end) cn = ld16(ly.cchunk(8 * (c + 1)));
-        }
-        return (sel4(cw, (i >> 1) & 3) >> ((i & 1) * 16)) & 0xFFFF;
-    }
-    FRD_HD uint32_t rec(uint32_t i) {
-        const uint32_t c = i >> 2;
-        if (c != mc) {
-            mw = c == mc + 1 ? mn : ld16(ly.mchunk(i));
-            mc = c;
-            if (4 * (c + 1) < end) mn = ld16(ly.mchunk(4 * (c + 1)));
-        }
-        return sel4(mw, i & 3);
-    }
+// Forward walk of a lane's parse: sym(ch, v) for each symbol of [a, b) in order (ch the choice, v the
+// record at its start; a a multiple of 8).  The walk goes through the positions in groups of 8 (two
+// record chunks and one choice chunk, loaded three groups ahead) and visits the symbols that start in
+// each: the next symbol's position never waits on a load (following the choices from load to load made
+// every step a memory round trip).  Four group slots keep their roles, as in parse_range.
+struct Grp {
+    Q4 r0, r1, c;
 };
+template <class SYM>
+FRD_HD void walk(uint32_t a, uint32_t b, const Lay& ly, SYM sym) {
+    if (b <= a) return;
+    const uint32_t gl = (b - 1) >> 3;
+    uint32_t g = a >> 3, nxt = a;
+    auto ldg = [&](uint32_t d, Grp& q) {  // group g + d, or the lane's last group past it
+        const uint32_t x = 8 * (g + d <= gl ? g + d : gl);
+        q.r0 = ld16(ly.mchunk(x));
+        q.r1 = ld16(ly.mchunk(x + 4));
+        q.c = ld16(ly.cchunk(x));
+    };
+    Grp ga, gb, gc, gd;
+    ldg(0, ga), ldg(1, gb), ldg(2, gc), ldg(3, gd);
+    auto group = [&](Grp& q) {  // the symbols that start in group g, then q takes group g + 4
+        const uint32_t hi = 8 * g + 8 < b ? 8 * g + 8 : b;
+        while (nxt < hi) {
+            const uint32_t i = nxt;
+            const uint32_t ch = (sel4(q.c, (i >> 1) & 3) >> ((i & 1) * 16)) & 0xFFFF;
+            const uint32_t v0 = sel4(q.r0, i & 3), v1 = sel4(q.r1, i & 3), v = (i & 4) ? v1 : v0;
+            nxt = i + (ch >= MINM ? ch : 1);
+            sym(ch, v);
+        }
+        if (g == gl) return false;
+        ldg(4, q);
+        ++g;
+        return true;
+    };
+    while (g + 4 <= gl) {  // four groups with no exit among them
+        group(ga), group(gb), group(gc), group(gd);
+    }
+    (void)(group(ga) && group(gb) && group(gc) && group(gd));  // the last 1..4
+}
 
 // Bit writer into zeroed 32-bit words: every word is ORed in (the GPU's lanes share edge words)
 struct BitW {
@@ -523,28 +544,22 @@ FRD_HD void write_header(const Tables& t, bool final_block, BitW& bw, OR orf) {
 // body bits of [a, b) under the parse in choice[] and the final tables
 FRD_HD uint64_t range_bits(uint32_t a, uint32_t b, const Lay& ly, const Tables& t) {
     uint64_t bits = 0;
-    Fwd f(ly, b);
-    for (uint32_t i = a; i < b;) {
-        const uint32_t ch = f.choice(i), v = f.rec(i);
+    walk(a, b, ly, [&](uint32_t ch, uint32_t v) {
         if (ch >= MINM) {
             uint32_t idx, eb, ev, dcode, deb, dev;
             len_code(ch, idx, eb, ev);
             dist_code(m_dist(v), dcode, deb, dev);
             bits += t.ll_len[257 + idx] + eb + t.d_len[dcode] + deb;
-            i += ch;
         } else {
             bits += t.ll_len[m_byte(v)];
-            ++i;
         }
-    }
+    });
     return bits;
 }
 
 template <class OR>
 FRD_HD void write_range(uint32_t a, uint32_t b, const Lay& ly, const Tables& t, BitW& bw, OR orf) {
-    Fwd f(ly, b);
-    for (uint32_t i = a; i < b;) {
-        const uint32_t ch = f.choice(i), v = f.rec(i);
+    walk(a, b, ly, [&](uint32_t ch, uint32_t v) {
         if (ch >= MINM) {
             uint32_t idx, eb, ev, dcode, deb, dev;
             len_code(ch, idx, eb, ev);
@@ -553,32 +568,26 @@ FRD_HD void write_range(uint32_t a, uint32_t b, const Lay& ly, const Tables& t, 
             if (eb) bw.put(ev, eb, orf);
             bw.put(t.d_code[dcode], t.d_len[dcode], orf);
             if (deb) bw.put(dev, deb, orf);
-            i += ch;
         } else {
             bw.put(t.ll_code[m_byte(v)], t.ll_len[m_byte(v)], orf);
-            ++i;
         }
-    }
+    });
 }
 
 // symbol counts of [a, b) under the parse in choice[]
 template <class ADD>
 FRD_HD void count_range(uint32_t a, uint32_t b, const Lay& ly, uint32_t* llf, uint32_t* df, ADD add) {
-    Fwd f(ly, b);
-    for (uint32_t i = a; i < b;) {
-        const uint32_t ch = f.choice(i), v = f.rec(i);
+    walk(a, b, ly, [&](uint32_t ch, uint32_t v) {
         if (ch >= MINM) {
             uint32_t idx, eb, ev, dcode, deb, dev;
             len_code(ch, idx, eb, ev);
             dist_code(m_dist(v), dcode, deb, dev);
             add(llf + 257 + idx);
             add(df + dcode);
-            i += ch;
         } else {
             add(llf + m_byte(v));
-            ++i;
         }
-    }
+    });
 }
 
 // parse costs from code lengths (a symbol the tables do not hold costs `absent` bits)

@@ -466,12 +466,18 @@ def frender_demux(args, dev=None) -> None:
     if group is not None:
         return _demux_ranks(group, args, dev, pairs, results, route_of, keys[fast], vals[fast], writers, window, level,
                             infix, kind)
-    dmx = dev or _lib.Demux(_device_index(None))
-    pool = ThreadPoolExecutor(max_workers=max(2, min(32, len(writers) * 2)))
-    # with the GPU compressing, the host's cores inflate (a big single-member file in parallel)
+    # with the GPU compressing, the host's cores inflate (a big single-member file in parallel); the
+    # pool's workers start at once, so the first blocks decode while the device context comes up
     paths = [str(f) for pr in pairs for f in pr]
     nt = _inflate_threads(kind)
     gz = _lib.GzPool(paths, threads=nt, ahead=_lib.inflate_ahead(paths, nt))
+    STAGE_TIMES["setup: results, writers"] = time.perf_counter() - t_start
+    try:
+        dmx = dev or _lib.Demux(_device_index(None))
+    except BaseException:
+        gz.close()
+        raise
+    pool = ThreadPoolExecutor(max_workers=max(2, min(32, len(writers) * 2)))
     try:
         dmx.set_table(keys[fast], vals[fast])
         STAGE_TIMES["setup"] = time.perf_counter() - t_start  # results, writers, device table, pool
@@ -485,8 +491,10 @@ def frender_demux(args, dev=None) -> None:
         for w in writers:
             for f in w.values():
                 f.close()
+        t_files = time.perf_counter()
         if dev is None:
             dmx.close()
+        STAGE_TIMES["finish: files"] = t_files - t_end
         STAGE_TIMES["finish"] = time.perf_counter() - t_end  # last writes, closes
         STAGE_TIMES["total"] = time.perf_counter() - t_start
         if getattr(args, "stage_times", False):

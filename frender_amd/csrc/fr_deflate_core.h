@@ -332,28 +332,19 @@ FRD_HD void parse_range(uint32_t a, uint32_t b, const Lay& ly, const Ring& best,
         if (L > PARSE_MAXL) L = PARSE_MAXL;
         if (L >= MINM) {
             const uint32_t dc = dist_cost(c, m_dist(mi));
-            auto span = [&](uint32_t lo, uint32_t hi) {  // lengths lo..hi in increasing order
-                uint32_t l = lo;
-                for (; l + 8 <= hi + 1; l += 8) {
-                    uint32_t v[8];
+            // eight lengths in increasing order, all read at once (no per-lane loop): 4..8, then 9..11
+            // (those up to L) or L-2..L
+            const uint32_t up = L <= 10 ? 0u : L - 11;
+            uint32_t v[8];
 #pragma unroll
-                    for (uint32_t q = 0; q < 8; ++q) v[q] = c.len[l + q] + best.at(k + l + q);
+            for (uint32_t q = 0; q < 8; ++q) {
+                const uint32_t l = 4 + q + (q >= 5 ? up : 0u);
+                v[q] = c.len[l] + best.at(k + l);
+            }
 #pragma unroll
-                    for (uint32_t q = 0; q < 8; ++q) {
-                        const uint32_t x = v[q] + dc;
-                        if (x < bc) bc = x, ch = l + q;
-                    }
-                }
-                for (; l <= hi; ++l) {
-                    const uint32_t x = c.len[l] + dc + best.at(k + l);
-                    if (x < bc) bc = x, ch = l;
-                }
-            };
-            if (L <= 10) {  // lengths 4..10 and, of a longer match, 4..8 and its last three
-                span(MINM, L);
-            } else {
-                span(MINM, 8);
-                span(L - 2, L);
+            for (uint32_t q = 0; q < 8; ++q) {
+                const uint32_t l = 4 + q + (q >= 5 ? up : 0u), x = v[q] + dc;
+                if (l <= L && x < bc) bc = x, ch = l;
             }
         }
         best.at(k) = bc;

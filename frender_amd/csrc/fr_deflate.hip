@@ -60,6 +60,7 @@ struct DefShared {
     };
     alignas(8) uint16_t bh[TPB];  // this batch's hashes (0xFFFF: none)
     uint32_t seen[2][2][128];     // per batch parity: hashes (>> 1) seen once / again in the batch
+    uint32_t first[256];          // per hash & 255: batch << 8 | 255 - the batch's first lane with it (max)
     uint32_t bhist[256];
     uint32_t llf[NLL];
     uint32_t df[NDIST];
@@ -82,7 +83,7 @@ __device__ __forceinline__ uint32_t ld32u(const uint8_t* p) {
 }
 
 #ifdef FRD_PROF
-__device__ unsigned long long g_prof[8];
+__device__ unsigned long long g_prof[12];
 #define PROF_MARK(k)                                                            \
     do {                                                                        \
         if (t == 0) {                                                           \
@@ -91,9 +92,13 @@ __device__ unsigned long long g_prof[8];
             prof_t = now_;                                                      \
         }                                                                       \
     } while (0)
+#define PROF_SUB(k) const unsigned long long k = wall_clock64()
 #else
 #define PROF_MARK(k) \
     do {             \
+    } while (0)
+#define PROF_SUB(k) \
+    do {            \
     } while (0)
 #endif
 
@@ -161,9 +166,14 @@ __global__ __launch_bounds__(TPB, 2) void deflate_blocks(const uint8_t* __restri
         S.bhist[t] = 0;
         S.seen[t >> 7][0][t & 127] = 0;
         S.seen[t >> 7][1][t & 127] = 0;
+        S.first[t] = 0;
         __syncthreads();
         // ---- matchfinder
+#ifdef FRD_PROF
+        unsigned long long ps[3] = {0, 0, 0};  // lane 0's batch segments: to the first barrier, to the second, the rest
+#endif
         for (uint32_t base = 0; base < ntot; base += TPB) {
+            PROF_SUB(pq0);
             const uint32_t r = base + t;
             uint32_t h = 0xFFFF, w = 0;
             if (r < ntot) {
@@ -178,8 +188,10 @@ __global__ __launch_bounds__(TPB, 2) void deflate_blocks(const uint8_t* __restri
             if (h != 0xFFFF) {
                 const uint32_t bit = 1u << ((h >> 1) & 31), wi = h >> 6;
                 if (atomicOr(&S.seen[par][0][wi], bit) & bit) atomicOr(&S.seen[par][1][wi], bit);
+                atomicMax(&S.first[h & 255], (base / TPB + 1) << 8 | (TPB - 1 - t));
             }
             __syncthreads();
+            PROF_SUB(pq1);
             S.seen[par ^ 1][t >> 7][t & 127] = 0;  // the other parity's maps, for the next batch
             if (r >= hist && r < ntot) {
                 uint32_t bl = 0, bd = 0;
@@ -188,21 +200,36 @@ __global__ __launch_bounds__(TPB, 2) void deflate_blocks(const uint8_t* __restri
                     uint32_t dds[WAYS + 1];
                     for (uint32_t s = 0; s < WAYS; ++s) dds[s] = (r - S.tab[h * WAYS + s]) & 0xFFFF;
                     dds[WAYS] = 0;
-                    if (S.seen[par][1][h >> 6] >> ((h >> 1) & 31) & 1) {
+                    // the lanes of the batch with this hash are at or after the first lane with its low
+                    // byte: a lane that is that first one, or whose hash the batch holds once, has none
+                    const uint32_t lo = TPB - 1 - (S.first[h & 255] & 255);
+                    if (lo < t && (S.seen[par][1][h >> 6] >> ((h >> 1) & 31) & 1)) {
                         // another lane of the batch may share the hash: the latest earlier one,
-                        // sixteen hashes (four independent LDS reads) per step
+                        // sixteen hashes (four independent LDS reads) per step; a word's fields equal
+                        // to h are found at once (zero-field flags: a flag above a zero field may be a
+                        // borrow's, but a flagged word holds a zero field, its highest is the lane)
                         const uint64_t hh = (uint64_t)h * 0x0001000100010001ull;
                         const uint64_t* bw = (const uint64_t*)S.bh;
                         uint32_t u = ~0u;
-                        for (int g = ((int)t - 1) >> 4; g >= 0 && u == ~0u; --g) {
+                        for (int g = ((int)t - 1) >> 4; g >= (int)(lo >> 4) && u == ~0u; --g) {
                             uint64_t v[4];
 #pragma unroll
                             for (int q = 0; q < 4; ++q) v[q] = bw[4 * g + q] ^ hh;
-                            for (int e = 15; e >= 0; --e)
-                                if ((uint32_t)(16 * g + e) < t && ((v[e >> 2] >> (16 * (e & 3))) & 0xFFFF) == 0) {
-                                    u = 16 * g + e;
-                                    break;
+                            const int rem = (int)t - 16 * g;  // the group's lanes below t
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) {
+                                const int nb = rem - 4 * q;  // fields of word q below t
+                                uint64_t z = (v[q] - 0x0001000100010001ull) & ~v[q] & 0x8000800080008000ull;
+                                z = nb >= 4 ? z : nb <= 0 ? 0ull : z & ((1ull << (16 * nb)) - 1ull);
+                                if (z) {
+                                    const uint64_t x = v[q];
+                                    const uint32_t f = (nb > 3 && !(x >> 48)) ? 3u
+                                                       : (nb > 2 && !((x >> 32) & 0xFFFF)) ? 2u
+                                                       : (nb > 1 && !((x >> 16) & 0xFFFF)) ? 1u
+                                                                                            : 0u;
+                                    u = 16 * g + 4 * q + f;
                                 }
+                            }
                         }
                         if (u != ~0u) dds[WAYS] = t - u;
                     }
@@ -211,8 +238,16 @@ __global__ __launch_bounds__(TPB, 2) void deflate_blocks(const uint8_t* __restri
                 ly.rec(r - hist) = mpack(hsp[r], bl >= MINM ? bl : 0u, bd);
             }
             __syncthreads();
+            PROF_SUB(pq2);
             if (h != 0xFFFF) S.tab[h * WAYS + (t >> 6)] = (uint16_t)r;
+#ifdef FRD_PROF
+            ps[0] += pq1 - pq0, ps[1] += pq2 - pq1, ps[2] += wall_clock64() - pq2;
+#endif
         }
+#ifdef FRD_PROF
+        if (t == 0)
+            for (int q = 0; q < 3; ++q) atomicAdd(&g_prof[8 + q], ps[q]);
+#endif
         __syncthreads();
         PROF_MARK(0);
         // ---- crc32 of the block: 1-KiB slices, folded by lane 0
@@ -527,12 +562,12 @@ int fr_defl_run(fr_defl* z, const uint8_t* dev_data, const uint64_t* offsets, in
         DF(hipGetLastError());
 #ifdef FRD_PROF
         {
-            unsigned long long pr[8];
+            unsigned long long pr[12];
             DF(hipStreamSynchronize(z->stream));
             DF(hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_prof), sizeof pr));
-            fprintf(stderr, "FRD_PROF wall ticks (100 MHz) summed over WGs: match %llu crc+cost %llu parse %llu count %llu huff %llu tables %llu emit %llu\n",
-                    pr[0], pr[1], pr[2], pr[3], pr[4], pr[5], pr[6]);
-            unsigned long long zero[8] = {0};
+            fprintf(stderr, "FRD_PROF wall ticks (100 MHz) summed over WGs: match %llu crc+cost %llu parse %llu count %llu huff %llu tables %llu emit %llu | match batches: to barrier 1 %llu, to barrier 2 %llu, rest %llu\n",
+                    pr[0], pr[1], pr[2], pr[3], pr[4], pr[5], pr[6], pr[8], pr[9], pr[10]);
+            unsigned long long zero[12] = {0};
             DF(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), zero, sizeof zero));
         }
 #endif

@@ -246,23 +246,34 @@ def pack_lower(s: str) -> int:
 FR_DMX_MISSING, FR_DMX_BADTYPE, FR_DMX_EXOTIC = -1, -2, -3
 
 
+_PACK_LUT = np.zeros(128, dtype=np.uint8)
+for _i, _c in enumerate("ACGTN+"):
+    _PACK_LUT[ord(_c)] = _i + 1
+
+
 def pack_fast(codes) -> tuple:
-    """Codes over {A,C,G,T,N,+} of 1..21 chars -> (3-bit packed keys, mask of the packable codes)."""
-    keys = np.zeros(len(codes), dtype=np.uint64)
-    ok = np.zeros(len(codes), dtype=bool)
-    sym = {"A": 1, "C": 2, "G": 3, "T": 4, "N": 5, "+": 6}
-    for i, c in enumerate(codes):
-        if not 1 <= len(c) <= 21:
-            continue
-        v = 0
-        for j, ch in enumerate(c):
-            s = sym.get(ch)
-            if s is None:
-                break
-            v |= s << (3 * j)
-        else:
-            keys[i] = v
-            ok[i] = True
+    """Codes over {A,C,G,T,N,+} of 1..21 chars -> (3-bit packed keys, mask of the packable codes):
+    character j of a code is bits 3j..3j+2 (A=1 C=2 G=3 T=4 N=5 +=6).  Vectorised over the codes (a
+    per-character loop took 1.4 s for a 300k-row results file)."""
+    n = len(codes)
+    keys = np.zeros(n, dtype=np.uint64)
+    ok = np.zeros(n, dtype=bool)
+    if not n:
+        return keys, ok
+    lens = np.fromiter((len(c) for c in codes), dtype=np.int64, count=n)
+    sel = np.nonzero((lens >= 1) & (lens <= 21))[0]
+    if not sel.size:
+        return keys, ok
+    cp = np.array([codes[i] for i in sel.tolist()], dtype="<U21").view(np.uint32).reshape(-1, 21)
+    # 0: not in the alphabet, or padding; one row per character position
+    sym = np.ascontiguousarray(np.where(cp < 128, _PACK_LUT[np.minimum(cp, 127)], np.uint8(0)).T)
+    nvalid = np.count_nonzero(sym, axis=0)
+    good = nvalid == lens[sel]  # every character in the alphabet (padding is 0: it never counts)
+    packed = np.zeros(sel.size, dtype=np.uint64)
+    for j in range(21):
+        packed |= sym[j].astype(np.uint64) << np.uint64(3 * j)
+    keys[sel[good]] = packed[good]
+    ok[sel[good]] = True
     return keys, ok
 
 

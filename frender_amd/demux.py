@@ -10,6 +10,7 @@ errors and gzips each destination's bytes into its writer pair (threads: zlib re
 from __future__ import annotations
 
 import csv
+import gc
 import gzip
 import json
 import os
@@ -49,7 +50,15 @@ def parse_results_file(result_file, strict: bool = False) -> dict:
         else:
             assert top == RESULTS_HEADER, f"${result_file} does not appear to be a valid frender result file!"
             ti, si = 5, 6
-        return {line[0] + "+" + line[1]: (line[ti], line[si]) for line in rd}
+        # (a scan's results file holds a row per distinct code: hundreds of thousands of tuples, which
+        # the cyclic collector would walk again and again while the dict grows)
+        enabled = gc.isenabled()
+        gc.disable()
+        try:
+            return {line[0] + "+" + line[1]: (line[ti], line[si]) for line in rd}
+        finally:
+            if enabled:
+                gc.enable()
 
 
 def _load_libdeflate():
@@ -487,14 +496,17 @@ def frender_demux(args, dev=None) -> None:
     finally:
         t_end = time.perf_counter()
         gz.close()
+        t_gz = time.perf_counter()
         pool.shutdown(wait=True)
+        STAGE_TIMES["finish: inflate pool"] = t_gz - t_end
+        STAGE_TIMES["finish: writer pool"] = time.perf_counter() - t_gz
         for w in writers:
             for f in w.values():
                 f.close()
         t_files = time.perf_counter()
         if dev is None:
             dmx.close()
-        STAGE_TIMES["finish: files"] = t_files - t_end
+        STAGE_TIMES["finish: files"] = t_files - t_end - STAGE_TIMES["finish: inflate pool"] - STAGE_TIMES["finish: writer pool"]
         STAGE_TIMES["finish"] = time.perf_counter() - t_end  # last writes, closes
         STAGE_TIMES["total"] = time.perf_counter() - t_start
         if getattr(args, "stage_times", False):

@@ -102,8 +102,20 @@ __device__ unsigned long long g_prof[12];
     } while (0)
 #endif
 
+// best_match's loads of a block's window: one buffer load of the dwords that hold the 12 bytes at p
+// (the candidates' loads are scattered, so the memory pipeline's cost is per instruction; a buffer
+// load takes dword-aligned multi-dword reads, and reads past the window's 16 readable bytes return 0)
 struct Ld32 {
-    __device__ uint32_t operator()(const uint8_t* p) const { return ld32u(p); }
+    const uint8_t* base;
+    __amdgpu_buffer_rsrc_t rs;
+    __device__ Ld32(const uint8_t* b, uint32_t bytes)
+        : base(b), rs(__builtin_amdgcn_make_buffer_rsrc((void*)b, (short)0, (int)bytes, 0x00020000)) {}
+    __device__ W12 w12(const uint8_t* p) const {
+        const uint32_t o = (uint32_t)(p - base), s = o & 3u;
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, o & ~3u, 0, 0);
+        return W12{__builtin_amdgcn_alignbyte(v[1], v[0], s), __builtin_amdgcn_alignbyte(v[2], v[1], s),
+                   __builtin_amdgcn_alignbyte(v[3], v[2], s)};
+    }
 };
 
 struct LdsOr {
@@ -162,6 +174,7 @@ __global__ __launch_bounds__(TPB, 2) void deflate_blocks(const uint8_t* __restri
         const uint32_t len = job.len, hist = job.hist, ntot = hist + len;
         const uint8_t* blk = data + job.start;
         const uint8_t* hsp = blk - hist;
+        const Ld32 win(hsp, ntot + 16);  // (the data's 16 readable bytes past the end: fr_defl_run)
         for (uint32_t i = t; i < NB * WAYS / 2; i += TPB) S.stage[i] = 0;
         S.bhist[t] = 0;
         S.seen[t >> 7][0][t & 127] = 0;
@@ -233,7 +246,7 @@ __global__ __launch_bounds__(TPB, 2) void deflate_blocks(const uint8_t* __restri
                         }
                         if (u != ~0u) dds[WAYS] = t - u;
                     }
-                    best_match<WAYS + 1>(hsp + r, w, dds, r, maxlen, Ld32{}, bl, bd);
+                    best_match<WAYS + 1>(hsp + r, w, dds, r, maxlen, win, bl, bd);
                 }
                 ly.rec(r - hist) = mpack(hsp[r], bl >= MINM ? bl : 0u, bd);
             }

@@ -206,40 +206,50 @@ FRD_HD uint32_t m_len(uint32_t v) { return (v >> 8) & 511; }
 FRD_HD uint32_t m_dist(uint32_t v) { return (v >> 17) + 1; }
 
 // The longest of the candidate matches at p (distances dds[0..nc), 0 = none; the 4 bytes at p are w),
-// ties to the nearer; every surviving candidate is extended in the same 8-byte step, so a step costs
-// one round of independent loads.  ld(q) = the 4 bytes at q (unaligned).
+// ties to the nearer; every surviving candidate is compared 12 bytes a step in the same round, so a
+// step costs one round of independent loads (the first round also tests the 4 bytes a candidate must
+// share).  ld.w12(q) = the 12 bytes at q as three little-endian words (unaligned; reads stay within 16
+// bytes past the block's end).
+struct W12 {
+    uint32_t a, b, c;
+};
 template <uint32_t NC, class LD>
 FRD_HD void best_match(const uint8_t* p, uint32_t w, const uint32_t* dds, uint32_t r, uint32_t maxlen, LD ld,
                        uint32_t& bl, uint32_t& bd) {
     constexpr uint32_t nc = NC;
     uint32_t len[NC];
     uint32_t alive = 0;
+    // first mismatch among the 12 bytes at l (x: the xor of the two reads); 12 when none
+    auto diff = [](const W12& x) -> uint32_t {
+        return x.a ? (uint32_t)__builtin_ctz(x.a) >> 3
+               : x.b ? 4 + ((uint32_t)__builtin_ctz(x.b) >> 3)
+               : x.c ? 8 + ((uint32_t)__builtin_ctz(x.c) >> 3)
+                     : 12u;
+    };
+    {
+        const W12 pw = ld.w12(p);
+        (void)w;
 #pragma unroll
-    for (uint32_t s = 0; s < nc; ++s) {
-        len[s] = 0;
-        const uint32_t dd = dds[s];
-        if (dd == 0 || dd > WIN || dd > r) continue;
-        if (ld(p - dd) == w) {
-            alive |= 1u << s;
-            len[s] = 4;
+        for (uint32_t s = 0; s < nc; ++s) {
+            len[s] = 0;
+            const uint32_t dd = dds[s];
+            if (dd == 0 || dd > WIN || dd > r) continue;
+            const W12 cw = ld.w12(p - dd);
+            const W12 x{cw.a ^ pw.a, cw.b ^ pw.b, cw.c ^ pw.c};
+            if (x.a & 0xFFFFFFFFu) continue;  // the first 4 bytes differ: no match
+            len[s] = diff(x);
+            if (len[s] == 12) alive |= 1u << s;
         }
     }
-    for (uint32_t l = 4; alive && l < maxlen; l += 8) {
-        const uint32_t p0 = ld(p + l), p1 = ld(p + l + 4);
+    for (uint32_t l = 12; alive && l < maxlen; l += 12) {
+        const W12 pw = ld.w12(p + l);
 #pragma unroll
         for (uint32_t s = 0; s < nc; ++s) {
             if (!(alive >> s & 1)) continue;
-            const uint8_t* c = p - dds[s] + l;
-            const uint32_t x0 = ld(c) ^ p0, x1 = ld(c + 4) ^ p1;
-            if (x0) {
-                len[s] = l + ((uint32_t)__builtin_ctz(x0) >> 3);
-                alive &= ~(1u << s);
-            } else if (x1) {
-                len[s] = l + 4 + ((uint32_t)__builtin_ctz(x1) >> 3);
-                alive &= ~(1u << s);
-            } else {
-                len[s] = l + 8;
-            }
+            const W12 cw = ld.w12(p - dds[s] + l);
+            const uint32_t k = diff(W12{cw.a ^ pw.a, cw.b ^ pw.b, cw.c ^ pw.c});
+            len[s] = l + k;
+            if (k < 12) alive &= ~(1u << s);
         }
     }
     bl = 0, bd = 0;

@@ -24,6 +24,14 @@ uint32_t load32u(const uint8_t* p) {
     return v;
 }
 
+struct HostLd {  // best_match's loads
+    W12 w12(const uint8_t* p) const {
+        W12 v;
+        memcpy(&v, p, 12);
+        return v;
+    }
+};
+
 uint32_t crc_tab[256];
 void crc_init() {
     for (uint32_t i = 0; i < 256; ++i) {
@@ -80,7 +88,7 @@ uint32_t encode_block(const uint8_t* buf, uint64_t start, uint32_t len, uint32_t
                     break;
                 }
             uint32_t bl, bd;
-            best_match<WAYS + 1>(buf + p, w, dds, r, maxlen, load32u, bl, bd);
+            best_match<WAYS + 1>(buf + p, w, dds, r, maxlen, HostLd{}, bl, bd);
             ly.rec(r - hist) = mpack(buf[p], bl >= MINM ? bl : 0, bd);
         }
         for (uint32_t t = 0; t < TPB; ++t)

@@ -276,6 +276,15 @@ FRD_HD void or4(Q4& a, uint32_t j, uint32_t v) {
     a.v3 |= j == 3 ? v : 0u;
 }
 
+// the compiler waits here for q's loads (an empty use of its registers)
+FRD_HD void ready(const Q4& q) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" ::"v"(q.v0), "v"(q.v1), "v"(q.v2), "v"(q.v3));
+#else
+    (void)q;
+#endif
+}
+
 // 16-byte loads and stores of the per-lane arrays (16-byte aligned chunks)
 FRD_HD Q4 ld16(const void* p) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -332,7 +341,6 @@ FRD_HD void parse_range(uint32_t a, uint32_t b, const Lay& ly, const Ring& best,
     uint32_t cc = (b - 1) >> 2, next_best = 0, i = b;
     // chunk cc - d, or the range's first chunk past it (loaded, never used: every slot loads)
     auto ldc = [&](uint32_t d) { return ld16(ly.mchunk(4 * (cc >= c0 + d ? cc - d : c0))); };
-    Q4 qa = ldc(0), qb = ldc(1), qc = ldc(2), qd = ldc(3);
     auto pos = [&](uint32_t mi) {  // position i (already decremented) with its record mi
         const uint32_t k = i - a;
         uint32_t bc = next_best + c.lit[m_byte(mi)];  // best(k + 1) is the previous step's result
@@ -361,24 +369,39 @@ FRD_HD void parse_range(uint32_t a, uint32_t b, const Lay& ly, const Ring& best,
         next_best = bc;
         or4(wbuf, (i >> 1) & 3, ch << ((i & 1) * 16));
     };
-    auto chunk = [&](Q4& q) {  // the positions of chunk cc left, then q takes chunk cc - 4
+    auto run = [&](const Q4& q) {  // the positions of chunk cc left (a loop free of memory operations)
         for (const uint32_t lo = 4 * cc; i > lo;) {
             --i;
             pos(sel4(q, i & 3));
         }
-        if (!(cc & 1)) {  // the choices of 8 positions (outside the loop above, which stays free of
-            st16(ly.cchunk(4 * cc), wbuf);  // memory operations: no wait for the slots' loads there)
-            wbuf = Q4{0, 0, 0, 0};
-        }
-        if (cc == c0) return false;
-        q = ldc(4);
-        --cc;
-        return true;
     };
-    while (cc >= c0 + 4) {  // four chunks with no exit among them (the compiler's waits stay counted)
-        chunk(qa), chunk(qb), chunk(qc), chunk(qd);
+    auto flush = [&]() {  // after an even chunk: the choices of its 8 positions
+        st16(ly.cchunk(4 * cc), wbuf);
+        wbuf = Q4{0, 0, 0, 0};
+    };
+    if (!(cc & 1)) {  // an even first chunk on its own: the loop below starts at an odd one
+        run(ldc(0));
+        flush();
+        if (cc == c0) return;
+        --cc;
     }
-    (void)(chunk(qa) && chunk(qb) && chunk(qc) && chunk(qd));  // the last 1..4
+    // Chunks cc (odd) .. cc - 3 in the four slots; each slot takes the chunk four below when its chunk
+    // is done.  Before a store the next two chunks' slots are waited for: a load used while a store is
+    // in flight makes the compiler wait for every load, the newest ones too.
+    Q4 qa = ldc(0), qb = ldc(1), qc = ldc(2), qd = ldc(3);
+    while (cc >= c0 + 4) {
+        run(qa), qa = ldc(4), --cc;
+        run(qb), ready(qc), ready(qd), flush(), qb = ldc(4), --cc;
+        run(qc), qc = ldc(4), --cc;
+        run(qd), ready(qa), ready(qb), flush(), qd = ldc(4), --cc;
+    }
+    // the last two or four chunks (c0 is even)
+    run(qa), --cc;
+    run(qb), flush();
+    if (cc == c0) return;
+    --cc;
+    run(qc), --cc;
+    run(qd), flush();
 }
 
 // Forward walk of a lane's parse: sym(ch, v) for each symbol of [a, b) in order (ch the choice, v the

@@ -292,7 +292,12 @@ class _Skip(Exception):
 
 
 def world_group():
-    """torch.distributed when this process is one rank of N > 1, else None."""
+    """torch.distributed when this process is one rank of N > 1, else None.  A process that has not
+    imported torch has no process group: the single-GPU commands do not pay the import here."""
+    import sys
+
+    if "torch" not in sys.modules:
+        return None
     try:
         import torch.distributed as dist
     except Exception:  # pragma: no cover

@@ -544,7 +544,8 @@ inline size_t find_start(const uint8_t* s, size_t n, size_t from, size_t to) {
 
 // ---- the member ------------------------------------------------------------------------------------
 // A gzip member's deflate data starting at s[0] (the file's remaining bytes s[0, n)), decoded by
-// `threads` threads in chunks of chunk_bytes compressed bytes.  On success `pieces` holds the decoded
+// `threads` threads in chunks of chunk_bytes compressed bytes.  Buffers in `pieces` on entry are
+// reused for the chunks' output (their capacity; the caller's recycled pieces).  On success `pieces` holds the decoded
 // bytes in order (each piece one chunk's output), dend = the deflate data's byte length (the trailer
 // follows), crc / total = the output's CRC-32 and length.  False on any failure (the caller decodes the
 // file with zlib from its start).
@@ -563,7 +564,12 @@ inline bool inflate_parallel(const uint8_t* s, size_t n, int threads, size_t chu
         ch[k].s = s;
         ch[k].n = n;
         ch[k].first = k == 0;
+        if (k < pieces.size()) {  // a buffer the caller passed in: the chunk's output reuses its capacity
+            ch[k].tail = std::move(pieces[k]);
+            ch[k].tail.clear();
+        }
     }
+    pieces.clear();
     auto pool = [&](const std::function<void()>& fn, size_t items) {
         std::vector<std::thread> ts;
         for (int t = 1; t < (int)std::min<size_t>((size_t)std::max(threads, 1), items); ++t) ts.emplace_back(fn);

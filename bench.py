@@ -112,6 +112,12 @@ def table_checksum(ctx, U):
     return int(h.sum().item())
 
 
+def reads_idx2(args, sheet):
+    """idx2 as the synthetic reads carry it: with --rc the samples of synth.CFG3_RC_NAMES read rc(idx2)."""
+    from frender_amd import synth
+    return synth.read_idx2(sheet, synth.CFG3_RC_NAMES if args.rc else None)
+
+
 def load_traffic(path, tree, per_launch_bytes, samples, index_len, combinatorial):
     """(HBM bytes per launch, note, VALU dict) from a PMC traffic file (scripts/make_traffic.py), or
     (None, why, None): a file measured on another source tree (frender_amd._lib.source_tree_hash) or
@@ -254,7 +260,7 @@ def cpu_baseline(args, ctx, sheet, reclen):
     n = args.cpu_reads
     cores = args.cpu_cores
     dev = ctx.device_alloc(n * reclen + 64)
-    ctx.synth_device(dev, 0, n, args.read_len, 1, sheet.idx1, sheet.idx2)
+    ctx.synth_device(dev, 0, n, args.read_len, 1, sheet.idx1, reads_idx2(args, sheet))
     data = ctx.copy_to_host(dev, n * reclen)
     ctx.device_free(dev)
     cuts = [n * i // cores for i in range(cores + 1)]
@@ -508,7 +514,9 @@ def main():
     ctx = _lib.Context(device=local, chunk_bytes=(args.launch_gib << 30) - (1 << 20), table_slots=1 << 22,
                        tuning=tuning or None)
     buf = ctx.device_alloc(nbytes + 64)
-    ctx.synth_device(buf, rank * n, n, args.read_len, 1, sheet.idx1, sheet.idx2)
+    # with --rc the reads of synth.CFG3_RC_NAMES carry rc(idx2) (the sheet is unchanged), so the per-name
+    # call flips those samples and pass B classifies against the rewritten idx2 list (tests/golden/cfg3_pin.json)
+    ctx.synth_device(buf, rank * n, n, args.read_len, 1, sheet.idx1, reads_idx2(args, sheet))
     names, nid = _sheet_names(sheet.ids)
     merge_cbs = device_callbacks(ctx)
     wire = "cpu" if args.dist_backend == "gloo" else "cuda"  # where small collectives' tensors live

@@ -53,8 +53,9 @@ def main(argv=None):
     d.add_argument("-r", metavar="result_file", required=True, help="REQUIRED: frender scan result file")
     d.add_argument("--strict-header", action="store_true",
                    help="reject a results file in scan's own column order, as frender.py does (default: accept it)")
-    d.add_argument("--gz-level", type=int, default=9,
-                   help="gzip level of the host writers (the reference writes gzip.open's default, 9)")
+    d.add_argument("--gz-level", type=int, default=None,
+                   help="gzip level of the host writers (default 9: the reference writes gzip.open's default); "
+                        "the gpu writer has no levels (its streams are no larger than level 9's)")
     d.add_argument("--gz-writer", choices=("gpu", "libdeflate", "zlib"), default="gpu",
                    help="who compresses the outputs: gpu (default: the routed bytes are deflated on the GPU, "
                         "no larger than zlib level 9 makes them on FASTQ), libdeflate or zlib (host threads at "

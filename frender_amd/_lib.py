@@ -159,6 +159,7 @@ _SIGS = {
     "fr_defl_run": (C.c_int, [P, P, P, C.c_int, P, P]),
     "fr_defl_run_host": (C.c_int, [P, P, C.c_uint64, P, C.c_int, P, P]),
     "fr_defl_out_bytes": (C.c_uint64, [P]),
+    "fr_defl_stored_fallbacks": (C.c_uint64, [P]),
     "fr_defl_fetch": (C.c_int, [P, P, C.c_uint64]),
 }
 for _name, (_res, _args) in _SIGS.items():
@@ -285,7 +286,9 @@ def inflate_ahead(paths, threads: int, budget: int = 2 << 30) -> int:
     """Files a pool should inflate at once: as many as `threads` while their decoded sizes fit the pool's
     2-GiB block budget, fewer for big files (whose decode then splits over the idle threads: a consumer
     that reads the files in order otherwise waits on one thread per file).  A file's decoded size is its
-    gzip trailer's ISIZE, or 4 x its size when the trailer is smaller than the file (multi-member)."""
+    gzip trailer's ISIZE (the decoded length mod 2^32) lifted by whole 2^32 steps toward 4 x its size, as
+    the native pool sizes it (fr_gz.cpp lift_isize): exact for a member of up to 4 GiB decoded, and a
+    big member whose ISIZE wrapped, or a multi-member file's small last ISIZE, is not taken at its word."""
     big = 0
     for p in paths:
         try:
@@ -296,7 +299,8 @@ def inflate_ahead(paths, threads: int, budget: int = 2 << 30) -> int:
                 isize = int.from_bytes(f.read(4), "little")
         except OSError:
             continue
-        big = max(big, isize if isize >= n else 4 * n)
+        want = 4 * n
+        big = max(big, isize + (((want - isize + (1 << 31)) >> 32) << 32 if want > isize else 0))
     if big <= 0:
         return max(1, threads)
     ahead = max(2, min(threads, budget // big)) if threads >= 2 else 1

@@ -349,15 +349,11 @@ __global__ __launch_bounds__(TPB, 2) void deflate_blocks(const uint8_t* __restri
             S.misc[1] = hdr;
             S.misc[2] = (uint32_t)(dyn ? dyn_bytes : stored_bytes);
             S.misc[3] = (uint32_t)(ebits - S.T.ll_len[256]);
-            S.misc[4] = 0;
         }
         __syncthreads();
         PROF_MARK(5);
-        const uint32_t nbytes = S.misc[2];
         uint8_t* out = stage_out + (uint64_t)j * OUT_STRIDE;
         if (S.misc[0]) {
-            const uint32_t nw = (nbytes + 3) / 4;
-            for (uint32_t i = t; i < nw + 1; i += TPB) S.stage[i] = 0;
             if (t < nsub) {
                 const uint32_t a = t * SUB, b = min(len, a + SUB);
                 S.lane_v[t] = (uint32_t)range_bits(a, b, ly, S.T);
@@ -369,8 +365,20 @@ __global__ __launch_bounds__(TPB, 2) void deflate_blocks(const uint8_t* __restri
                     S.lane_off[s] = off;
                     off += S.lane_v[s];
                 }
-                if (off != S.misc[3]) S.misc[4] = 1;  // the lanes' bits must add up to the counted body
+                // the lanes' bits must add up to the counted body; if they do not, the block is stored
+                // (always a valid encoding of its bytes) and counted in out_crc[n_jobs]
+                if (off != S.misc[3]) {
+                    S.misc[0] = 0;
+                    S.misc[2] = len + 5 * ((len + 65534) / 65535);
+                    atomicAdd(&out_crc[n_jobs], 1u);
+                }
             }
+            __syncthreads();
+        }
+        const uint32_t nbytes = S.misc[2];
+        if (S.misc[0]) {
+            const uint32_t nw = (nbytes + 3) / 4;
+            for (uint32_t i = t; i < nw + 1; i += TPB) S.stage[i] = 0;
             __syncthreads();
             if (t < nsub) {
                 const uint32_t a = t * SUB, b = min(len, a + SUB);
@@ -409,7 +417,7 @@ __global__ __launch_bounds__(TPB, 2) void deflate_blocks(const uint8_t* __restri
             }
         }
         if (t == 0) {
-            out_len[j] = S.misc[4] ? 0xFFFFFFFFu : nbytes;
+            out_len[j] = nbytes;
             out_crc[j] = crc;
         }
         __syncthreads();
@@ -469,6 +477,7 @@ struct fr_defl {
     void* tmp = nullptr;
     uint64_t c_jobs = 0, c_blen = 0, c_bcrc = 0, c_boff = 0, c_stage = 0, c_out = 0, c_tmp = 0, c_in = 0;
     uint64_t out_len = 0;
+    uint64_t fallbacks = 0;  // blocks stored because their bit accounting did not add up (diagnostics)
     std::vector<DJob> hjobs;
     std::vector<uint32_t> hlen, hcrc;
     uint32_t shift64k[1024];
@@ -569,6 +578,7 @@ int fr_defl_run(fr_defl* z, const uint8_t* dev_data, const uint64_t* offsets, in
         DF(grow(&z->boff, z->c_boff, nj + 1));
         DF(grow(&z->stage, z->c_stage, nj * OUT_STRIDE));
         DF(hipMemcpyAsync(z->jobs, z->hjobs.data(), nj * sizeof(DJob), hipMemcpyHostToDevice, z->stream));
+        DF(hipMemsetAsync(z->bcrc + nj, 0, 4, z->stream));  // the kernel counts its stored fallbacks here
         const uint32_t g = (uint32_t)std::min<uint64_t>(nj, (uint64_t)z->grid);
         hipLaunchKernelGGL(deflate_blocks, dim3(g), dim3(TPB), 0, z->stream, dev_data, z->jobs, (uint32_t)nj, z->stage,
                            z->blen, z->bcrc, z->scratch, z->shift);
@@ -594,8 +604,10 @@ int fr_defl_run(fr_defl* z, const uint8_t* dev_data, const uint64_t* offsets, in
         z->hlen.resize(nj);
         z->hcrc.resize(nj);
         DF(hipMemcpyAsync(z->hlen.data(), z->blen, nj * 4, hipMemcpyDeviceToHost, z->stream));
-        DF(hipMemcpyAsync(z->hcrc.data(), z->bcrc, nj * 4, hipMemcpyDeviceToHost, z->stream));
+        z->hcrc.resize(nj + 1);
+        DF(hipMemcpyAsync(z->hcrc.data(), z->bcrc, (nj + 1) * 4, hipMemcpyDeviceToHost, z->stream));
         DF(hipStreamSynchronize(z->stream));
+        z->fallbacks += z->hcrc[nj];
         uint64_t total = 0;
         for (uint64_t k = 0; k < nj; ++k) {
             if (z->hlen[k] > OUT_STRIDE) return z->err = "fr_defl_run: a block's bit accounting failed", FR_ERR_DEVICE;
@@ -635,6 +647,7 @@ int fr_defl_run_host(fr_defl* z, const uint8_t* data, uint64_t len, const uint64
 }
 
 uint64_t fr_defl_out_bytes(const fr_defl* z) { return z ? z->out_len : 0; }
+uint64_t fr_defl_stored_fallbacks(const fr_defl* z) { return z ? z->fallbacks : 0; }
 
 int fr_defl_fetch(fr_defl* z, uint8_t* out, uint64_t len) {
     if (len > z->out_len) return z->err = "fr_defl_fetch: more bytes than the last run produced", FR_ERR_INVALID;

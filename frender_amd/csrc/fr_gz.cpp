@@ -285,6 +285,14 @@ bool bgzf_decode(fr_gz* g, const Libdeflate* ld, const Bytes& in, const std::vec
     return ok;
 }
 
+// a member's decoded size from its trailer's ISIZE (decoded length mod 2^32): lifted by whole 2^32 steps
+// toward 4x the compressed size csize (exact for a single member of up to 4 GiB decoded)
+inline uint64_t lift_isize(uint64_t isize, uint64_t csize) {
+    const uint64_t want = 4 * csize;
+    const uint64_t m = want > isize ? (want - isize + (1ull << 31)) >> 32 : 0;
+    return isize + (m << 32);
+}
+
 // hold `bytes` of the pool's whole-file budget (false: it does not fit now; stream instead)
 bool take_budget(fr_gz* g, size_t bytes) {
     std::lock_guard<std::mutex> lk(g->m);
@@ -319,9 +327,12 @@ bool inflate_member_parallel(fr_gz* g, GzFile& f, const Bytes& in) {
         }
     if (flg & 2) h += 2;  // FHCRC
     if (h + 8 >= n) return false;
-    // the trailer's ISIZE sizes the output budget (exact up to 4 GiB decoded; otherwise 4x the input)
-    const size_t hint = le32(&in[n - 4]);
-    const size_t est = hint >= n ? hint : 4 * n;
+    // the trailer's ISIZE (decoded length mod 2^32) lifted by whole 2^32 steps toward 4x the input sizes
+    // the output budget: exact for a member of up to 4 GiB decoded, and a 1-GiB member of FASTQ (4-6 GiB
+    // decoded) is not sized by its wrapped ISIZE.  The decode stops once its chunks outgrow the budget.
+    // (a trailer under n bytes is no trailer: NUL padding ends the file; then 4x the input)
+    const size_t lifted = (size_t)lift_isize(le32(&in[n - 4]), n);
+    const size_t est = lifted >= n ? lifted : 4 * n;
     if (!take_budget(g, est)) return false;
     struct Hold {
         fr_gz* g;
@@ -342,12 +353,17 @@ bool inflate_member_parallel(fr_gz* g, GzFile& f, const Bytes& in) {
     std::vector<Bytes> pieces;  // on the way in: buffers for the chunks' output, from the cache
     for (size_t k = 0, K = (n - h + chunk - 1) / chunk; k < K; ++k) pieces.push_back(buf_cache().take(est / K + 1));
     frpz::Result r;
-    bool ok = frpz::inflate_parallel<Bytes>(in.data() + h, n - h, T, chunk, pieces, r);
-    // the member's trailer (CRC-32, ISIZE), then nothing but NUL padding: one clean member
+    // the member's trailer (CRC-32, ISIZE), then nothing but NUL padding: one clean member.  The tail
+    // test runs inside, right after the stitch (a concatenated multi-member file stops there, before the
+    // window, resolve and CRC phases), and the decode gives up once its output passes est.
+    bool ok = frpz::inflate_parallel<Bytes>(in.data() + h, n - h, T, chunk, pieces, r, est, true);
+    // the decode is done: the helper threads go back to the pool before the queueing below, which
+    // waits on the consumer
+    give_threads(g, held.k);
+    held.k = 0;
     if (ok) {
         const size_t t = h + r.dend;
         ok = t + 8 <= n && le32(&in[t]) == r.crc && le32(&in[t + 4]) == (uint32_t)r.total;
-        for (size_t q = t + 8; ok && q < n; ++q) ok = in[q] == 0;
     }
     if (!ok) {
         for (auto& b : pieces) buf_cache().give(std::move(b));
@@ -827,9 +843,7 @@ uint64_t fr_gz_size_hint(const char* path) {
     const bool ok = fseek(fp, -4, SEEK_END) == 0 && fread(t, 1, 4, fp) == 4;
     fclose(fp);
     if (!ok) return 4 * csize;
-    const uint64_t isize = le32(t), want = 4 * csize;
-    const uint64_t m = want > isize ? (want - isize + (1ull << 31)) >> 32 : 0;
-    return isize + (m << 32);
+    return lift_isize(le32(t), csize);
 }
 
 int fr_gz_part_bounds(const char* path, int nparts, uint64_t hint, uint64_t* bounds) {
@@ -1113,10 +1127,11 @@ bool part_extend(fr_gz_part* p, uint64_t want) {
     return true;
 }
 
-// byte at decoded offset x (-1 past the file's end); data must cover it
+// byte at decoded offset x (-1 past the file's end); data must cover it.  -2 when it does not (an
+// internal error the caller reports as FR_ERR_IO: callers extend first, so it is never expected)
 inline int part_byte(const fr_gz_part* p, uint64_t x) {
     if (x >= p->total) return -1;
-    if (x < p->dbase || x - p->dbase >= p->data.size()) abort();  // callers extend first: never read past data
+    if (x < p->dbase || x - p->dbase >= p->data.size()) return -2;
     return p->data[x - p->dbase];
 }
 
@@ -1130,6 +1145,7 @@ bool part_cut(fr_gz_part* p, uint64_t x, uint64_t L, uint64_t& cut) {
     if (!part_extend(p, x + 1)) return false;
     const int prev = part_byte(p, x - 1);
     const int cur = part_byte(p, x);
+    if (prev == -2 || cur == -2) return false;
     bool start = prev == '\n' || (prev == '\r' && cur != '\n');
     uint64_t q = x, lines = L;
     for (;;) {
@@ -1143,6 +1159,7 @@ bool part_cut(fr_gz_part* p, uint64_t x, uint64_t L, uint64_t& cut) {
         }
         if (q + 2 > p->dbase + p->data.size() && !part_extend(p, q + 2 + (1u << 16))) return false;
         const int c = part_byte(p, q), nx = part_byte(p, q + 1);
+        if (c == -2 || nx == -2) return false;
         start = false;
         if (c == '\n' || (c == '\r' && nx != '\n')) {
             ++lines;

@@ -42,6 +42,23 @@ namespace fr {
 #define FR_CSTAMP(i) do { } while (0)
 #endif
 
+#if defined(FR_STAMPS) && FR_STAMPS == 4  // diagnostic builds only: where a wave's walk time goes (walk_wave's
+// steps, DevState::stamp: 0 the next tile's VMEM wait, 1 LDS copy + classify, 2 rare drain + bitmaps, 3 header
+// parse, 4 walk steps counted, 5 whole-kernel wave cycles, 6 walk calls)
+#define FR_WSTAMP_DECL u64 wst_[4] = {0, 0, 0, 0}; u64 wq_ = __builtin_amdgcn_s_memtime();
+#define FR_WSTAMP(i) do { const u64 n_ = __builtin_amdgcn_s_memtime(); wst_[i] += n_ - wq_; wq_ = n_; } while (0)
+#define FR_WSTAMP_RESET() do { wq_ = __builtin_amdgcn_s_memtime(); } while (0)
+#define FR_WSTAMP_FLUSH(steps) do { if ((threadIdx.x & 63) == 0) { \
+    for (int i_ = 0; i_ < 4; ++i_) atomicAdd((unsigned long long*)&a.st->stamp[i_], (unsigned long long)wst_[i_]); \
+    atomicAdd((unsigned long long*)&a.st->stamp[4], (unsigned long long)(steps)); \
+    atomicAdd((unsigned long long*)&a.st->stamp[6], 1ull); } } while (0)
+#else
+#define FR_WSTAMP_DECL
+#define FR_WSTAMP(i) do { } while (0)
+#define FR_WSTAMP_RESET() do { } while (0)
+#define FR_WSTAMP_FLUSH(steps) do { } while (0)
+#endif
+
 #ifdef FR_DEBUG_PRINT  // diagnostic builds only: trace the tally kernel's chunk loop (workgroup 0, lane 0 of each wave)
 #define FR_TRACE(...) do { if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) printf(__VA_ARGS__); } while (0)
 #else
@@ -259,6 +276,7 @@ struct ScanShared {
 typedef u32 u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) u32 lds_u32;
 typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
+typedef __attribute__((address_space(3))) u64 lds_u64;
 
 __device__ __forceinline__ u64 make_ord(const ScanArgs& a, u64 off_in_range) {
     return ((u64)a.file_tag << ORD_SHIFT) | (a.file_offset + off_in_range);
@@ -295,14 +313,17 @@ __device__ __forceinline__ void lds_insert(ScanShared& sh, const ScanArgs& a, u6
 #pragma unroll 2
     for (int pr = 0; pr < LPROBE; ++pr) {
         // volatile through an explicit LDS pointer: a volatile access through a generic pointer
-        // keeps its flat form (flat loads wait on vmcnt(0), i.e. on every outstanding HBM op)
-        const u32x4 sl = *(const volatile lds_u32x4*)&sh.ls[h];
+        // keeps its flat form (flat loads wait on vmcnt(0), i.e. on every outstanding HBM op).  The key
+        // count is read in the same round as the slot (a new key's claim then costs no extra round trip)
+        u32x4 sl = *(const lds_u32x4*)&sh.ls[h];
+        u32 nk = *(const lds_u32*)&sh.nkeys;
+        asm volatile("" : "+v"(sl), "+v"(nk) :: "memory");  // both loads in one round, not moved or reused
         u64 k = ((u64)sl.y << 32) | sl.x;
         u32 mino = sl.w;
         if (k == 0) {
             // a full LDS table stops claiming slots: the code goes to the cold list; the codes
             // already resident (the hot ones arrive first) keep aggregating here
-            if (*(const volatile lds_u32*)&sh.nkeys >= a.flush_at) break;
+            if (nk >= a.flush_at) break;
             const u64 old = atomicCAS((unsigned long long*)&sh.ls[h].key, 0ull, (unsigned long long)key);
             if (old == 0) {
                 atomicAdd(&sh.nkeys, 1u);
@@ -1312,18 +1333,30 @@ __device__ __forceinline__ u64 window64(u64 x0, u64 x1, u32 b) { return (x0 >> b
 // fallback (the first ' ' or the token end lies 64 or more bytes on, or the token starts past the
 // staged bytes).
 __device__ __forceinline__ int locate_code(const ScanShared& sh, u32 wid, u32 p, u32 bl, u32& start, u32& n) {
+    // One LDS round for both windows: the token start q < p + 64 lies in word w or w + 1, so words w .. w + 2
+    // hold everything either window reads (the loads go out together, before any branch; w <= 63 keeps
+    // w + 2 inside the SEGS + 2 words).  Round 4 read the second window's words after the first window's
+    // test: two dependent LDS round trips per header, each a bitmap pair at a time (four waits).
+    const u32 w = min(p >> 6, (u32)SEGS - 1u), b = p & 63u;
+    const lds_u64* S = (const lds_u64*)&sh.bsp[wid][w];
+    const lds_u64* E = (const lds_u64*)&sh.beol[wid][w];
+    const lds_u64* C = (const lds_u64*)&sh.bcol[wid][w];
+    u64 s0 = S[0], s1 = S[1], s2 = S[2], e0 = E[0], e1 = E[1], c0 = C[0], c1 = C[1], c2 = C[2];
+    // all eight in registers here: the compiler would otherwise sink each load into the branch that uses
+    // it (one wait per load again)
+    asm volatile("" : "+v"(s0), "+v"(s1), "+v"(s2), "+v"(e0), "+v"(e1), "+v"(c0), "+v"(c1), "+v"(c2));
     if (p >= bl) return 2;
-    const u32 w = p >> 6, b = p & 63u;
-    const u64 se = window64(sh.bsp[wid][w], sh.bsp[wid][w + 1], b);
-    const u64 eo = window64(sh.beol[wid][w], sh.beol[wid][w + 1], b);
+    const u64 se = window64(s0, s1, b);
+    const u64 eo = window64(e0, e1, b);
     const u32 f1 = ctz64x(se);
     const u32 q = p + f1 + 1u;
     if (f1 >= 64u) return 2;
     if (ctz64x(eo) == f1) return 1;
     if (q >= bl) return 2;
-    const u32 w2 = q >> 6, b2 = q & 63u;
-    const u64 se2 = window64(sh.bsp[wid][w2], sh.bsp[wid][w2 + 1], b2);
-    const u64 co2 = window64(sh.bcol[wid][w2], sh.bcol[wid][w2 + 1], b2);
+    const bool nxt = (q >> 6) != w;  // the token starts in word w + 1
+    const u32 b2 = q & 63u;
+    const u64 se2 = window64(nxt ? s1 : s0, nxt ? s2 : s1, b2);
+    const u64 co2 = window64(nxt ? c1 : c0, nxt ? c2 : c1, b2);
     const u32 f2 = ctz64x(se2);
     if (f2 >= 64u) return 2;
     const int hc = hsb64x(co2 & ((1ull << f2) - 1ull));  // the last ':' of the token, < 0 none
@@ -1460,7 +1493,13 @@ __device__ __forceinline__ u64 walk_wave(ScanShared& sh, const ScanArgs& a0, u32
     SegRegs r;
     if (tb < te) seg_load(a, tb, r, lane);
     lds_u32x4* mine = (lds_u32x4*)(&sh.raw[wid][0]) + lane * (SEG / 16);
+    FR_WSTAMP_DECL
     for (u32 t = tb; t < te; ++t) {
+#if defined(FR_STAMPS) && FR_STAMPS == 4
+        FR_WSTAMP_RESET();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        FR_WSTAMP(0);
+#endif
         // the previous tile's parse is done with the LDS copy (program order)
 #pragma unroll
         for (int k = 0; k < SEG / 16; ++k) {
@@ -1474,6 +1513,7 @@ __device__ __forceinline__ u64 walk_wave(ScanShared& sh, const ScanArgs& a0, u32
             const u32x4 v = *(const volatile lds_u32x4*)&mine[k];
             return make_uint4(v.x, v.y, v.z, v.w);
         }, lane);
+        FR_WSTAMP(1);
         if (sc.hi) rare_push(sh, a, (t - ct) * TSTEP + lane * SEG, 4u,
                              min((u32)min((u64)TSTEP, a.len - (u64)t * TSTEP) - lane * SEG, (u32)SEG), 0u);
         const u32 tail = *(const volatile lds_u32*)&sh.rq_tail[wid];
@@ -1488,9 +1528,12 @@ __device__ __forceinline__ u64 walk_wave(ScanShared& sh, const ScanArgs& a0, u32
         // (a speculation buffer that overflowed mid-walk, sh.spec_bad, is not checked per tile: the chunk is
         // redone exactly and everything its walk buffered is discarded, so parsing on is harmless; the check
         // was an LDS round trip per tile)
+        FR_WSTAMP(2);
         if (parse && !(ABLATE & 1u)) parse_own_headers(sh, a, t, ct, sc, L0 + lines, lane, wid);
         lines += sc.wtot;
+        FR_WSTAMP(3);
     }
+    FR_WSTAMP_FLUSH(te > tb ? te - tb : 0u);
     lds_fence();
     const u32 tail = *(const volatile lds_u32*)&sh.rq_tail[wid];
     if (tail != done) drain_rare(sh, a, wid, done, tail, lane);
@@ -1634,7 +1677,7 @@ __global__ __launch_bounds__(WG, FR_OCC) void chunk_kernel(ScanArgs args) {
     const Geom g = hv ? Geom{a.chunk_tiles_h, a.mid_chunks_h, a.num_chunks_h, a.ramp_down_g_h}
                       : Geom{a.chunk_tiles, a.mid_chunks, a.num_chunks, a.ramp_down_g};
     const bool limited = a.max_records > 0;
-#if defined(FR_STAMPS) && FR_STAMPS == 1
+#if defined(FR_STAMPS) && (FR_STAMPS == 1 || FR_STAMPS == 4)
     const u64 k0_ = __builtin_amdgcn_s_memtime();
 #endif
     FR_STAMP_DECL
@@ -1788,6 +1831,10 @@ __global__ __launch_bounds__(WG, FR_OCC) void chunk_kernel(ScanArgs args) {
     }
 #if defined(FR_STAMPS) && FR_STAMPS == 1
     FR_STAMP_FLUSH(k0_);
+#endif
+#if defined(FR_STAMPS) && FR_STAMPS == 4
+    if ((threadIdx.x & 63) == 0)
+        atomicAdd((unsigned long long*)&a.st->stamp[5], (unsigned long long)(__builtin_amdgcn_s_memtime() - k0_));
 #endif
 #if defined(FR_STAMPS) && FR_STAMPS == 3
     if (tid == 0 && blockIdx.x < TRACE_WGS) g_wg_trace[(a.par * TRACE_WGS + blockIdx.x) * 2 + 1] = __builtin_amdgcn_s_memrealtime();

@@ -548,7 +548,10 @@ inline size_t find_start(const uint8_t* s, size_t n, size_t from, size_t to) {
 // reused for the chunks' output (their capacity; the caller's recycled pieces).  On success `pieces` holds the decoded
 // bytes in order (each piece one chunk's output), dend = the deflate data's byte length (the trailer
 // follows), crc / total = the output's CRC-32 and length.  False on any failure (the caller decodes the
-// file with zlib from its start).
+// file with zlib from its start), and when the chunks' output passes max_out bytes (the caller's memory
+// budget: its estimate of the decoded size was low).  member_tail: the member's 8-byte trailer must
+// follow the deflate data and nothing but NUL bytes after it (a gzip file of one member), checked right
+// after the stitch, before the window, resolve and CRC phases.
 struct Result {
     size_t dend = 0;
     uint32_t crc = 0;
@@ -557,7 +560,7 @@ struct Result {
 };
 template <class Buf>
 inline bool inflate_parallel(const uint8_t* s, size_t n, int threads, size_t chunk_bytes, std::vector<Buf>& pieces,
-                             Result& r) {
+                             Result& r, size_t max_out = SIZE_MAX, bool member_tail = false) {
     const size_t K = std::max<size_t>(1, (n + chunk_bytes - 1) / chunk_bytes);
     std::vector<Chunk<Buf>> ch(K);
     for (size_t k = 0; k < K; ++k) {
@@ -578,6 +581,8 @@ inline bool inflate_parallel(const uint8_t* s, size_t n, int threads, size_t chu
     };
     // 1. every chunk in parallel: its start, then blocks up to the next chunk's nominal start
     std::atomic<size_t> next{0};
+    std::atomic<size_t> produced{0};  // phase 1's output so far (bytes): past max_out the decode stops
+    std::atomic<bool> over{false};
 #ifdef FRPZ_TIMING
     auto T0 = std::chrono::steady_clock::now();
     auto lap = [&](const char* what) {
@@ -590,7 +595,7 @@ inline bool inflate_parallel(const uint8_t* s, size_t n, int threads, size_t chu
 #endif
     pool(
         [&]() {
-            for (size_t k; (k = next.fetch_add(1)) < K;) {
+            for (size_t k; !over.load(std::memory_order_relaxed) && (k = next.fetch_add(1)) < K;) {
                 auto& c = ch[k];
                 const size_t stop = (k + 1) * chunk_bytes * 8;
                 try {
@@ -602,6 +607,11 @@ inline bool inflate_parallel(const uint8_t* s, size_t n, int threads, size_t chu
                     auto a1 = std::chrono::steady_clock::now();
 #endif
                     if (c.start != SIZE_MAX && !c.run(c.start, stop)) c.bad = true;
+                    // (phase 1's chunks overlap by up to a block each, and a chunk's output can carry a window
+                    // prefix: a quarter and 64 MiB of slack)
+                    if (max_out != SIZE_MAX &&
+                        produced.fetch_add(c.out_len()) + c.out_len() > max_out + max_out / 4 + (64u << 20))
+                        over = true;
 #ifdef FRPZ_TIMING
                     auto a2 = std::chrono::steady_clock::now();
                     fprintf(stderr, "chunk %zu find %.1f ms (%zu bits) run %.1f ms out %zu bytes-mode %d\n", k,
@@ -615,6 +625,10 @@ inline bool inflate_parallel(const uint8_t* s, size_t n, int threads, size_t chu
         },
         K);
     lap("phase 1");
+    if (over) {
+        r.why = "the output outgrows the budget";
+        return false;
+    }
     if (ch[0].bad) {
         r.why = "the first chunk does not decode";
         return false;
@@ -648,6 +662,22 @@ inline bool inflate_parallel(const uint8_t* s, size_t n, int threads, size_t chu
     if (dend > n) {
         r.why = "the data ends inside the final block";
         return false;
+    }
+    if (member_tail) {  // one member: its trailer, then only NUL padding (else another member follows)
+        bool tail = dend + 8 <= n;
+        for (size_t q = dend + 8; tail && q < n; ++q) tail = s[q] == 0;
+        if (!tail) {
+            r.why = "not a single member";
+            return false;
+        }
+    }
+    if (max_out != SIZE_MAX) {  // the stitch decodes on past phase 1: the same bound on the kept chunks
+        size_t tot = 0;
+        for (size_t j : keep) tot += ch[j].out_len();
+        if (tot > max_out + max_out / 4 + (64u << 20)) {
+            r.why = "the output outgrows the budget";
+            return false;
+        }
     }
     // 3. windows in order: the resolved last WSIZE bytes before each kept chunk
     auto resolve = [](uint32_t v, const std::vector<uint8_t>& wv, bool& ok) -> uint8_t {

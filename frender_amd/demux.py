@@ -413,6 +413,9 @@ def frender_demux(args, dev=None) -> None:
     samples = not args.no_samples
     level = getattr(args, "gz_level", None) or 9  # gzip.open's default, as the reference writes
     kind = writer_kind(getattr(args, "gz_writer", None) or "gpu")
+    if kind is _GzDevice and getattr(args, "gz_level", None) not in (None, 9):
+        print(f"Warning: --gz-level {args.gz_level} has no effect with --gz-writer gpu (the GPU writer's streams "
+              "are no larger than level 9's); use --gz-writer libdeflate or zlib for another level", file=sys.stderr)
     infix = args.o
     undeter_name = f"Undetermined{'-ambiguous' if ambiguous else ''}{'-index-hop' if index_hop else ''}"
 

@@ -366,6 +366,9 @@ int fr_defl_run_host(fr_defl* z, const uint8_t* data, uint64_t len, const uint64
                      uint64_t* comp_bytes, uint32_t* crc32);
 /* the last run's streams, concatenated in stream order */
 uint64_t fr_defl_out_bytes(const fr_defl* z);
+/* blocks this context stored because their dynamic encoding's bit accounting did not add up (the stored
+ * form is always a valid encoding of the block; a nonzero count is a diagnostic, not an error) */
+uint64_t fr_defl_stored_fallbacks(const fr_defl* z);
 int fr_defl_fetch(fr_defl* z, uint8_t* out, uint64_t len);
 
 #ifdef __cplusplus

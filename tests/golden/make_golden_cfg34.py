@@ -12,7 +12,8 @@ file resident in HBM.  This script writes the same records (host SYN-v1 generato
 frender_amd/synth.py, byte-identical to the device one) as `--workers` consecutive level-1
 .fastq.gz files, imports /root/reference/frender.py (spec_from_file_location; the CLI sits
 behind `__main__`, frender.py:817) and runs the reference's own frender_scan sequence
-(frender.py:606-630):
+(frender.py:606-630).  In the config-3 shape the reads of synth.CFG3_RC_NAMES carry rc(idx2), so the
+reference's call flips those 8 names and pass B classifies against the rewritten idx2 list:
 
     counter = tally_barcodes(W, files)                                       (:183-207)
     results = process(W, counter["total"], indexes, n, rc)                   (:391-426)
@@ -57,10 +58,11 @@ REF_PATH = "/root/reference/frender.py"
 BLOCK = 1 << 20
 
 SHAPES = {
-    3: {"samples": 384, "L": 10, "combinatorial": None, "n": 1, "rc": True,
+    3: {"samples": 384, "L": 10, "combinatorial": None, "n": 1, "rc": True, "rc_names": synth.CFG3_RC_NAMES,
         "workload": "BASELINE config 3 shape: SYN-v1 records [0, reads), 384 samples (synth.make_sheet(384, 10, 10), "
-                    "seed 42), 10+10 bp, R=8, seed 1, n=1, -rc (pass A, per-name call, pass B)"},
-    4: {"samples": 96, "L": 8, "combinatorial": (12, 8), "n": 2, "rc": False,
+                    "seed 42), 10+10 bp, R=8, seed 1, n=1, -rc (pass A, per-name call, pass B); the reads of the "
+                    "8 samples synth.CFG3_RC_NAMES carry rc(idx2), so the per-name call flips them"},
+    4: {"samples": 96, "L": 8, "combinatorial": (12, 8), "n": 2, "rc": False, "rc_names": None,
         "workload": "BASELINE config 4 shape: SYN-v1 records [0, reads), 96 combinatorial dual indexes "
                     "(synth.make_sheet(96, 8, 8, combinatorial=(12, 8)), seed 42), 8+8 bp, R=8, seed 1, n=2, no -rc"},
 }
@@ -78,7 +80,8 @@ def _write_part(job):
     with open(path, "wb") as f:
         for a in range(r0, r0 + n, BLOCK):
             b = min(BLOCK, r0 + n - a)
-            f.write(co.compress(synth.generate_records(sheet, a, b, R=8, seed=1).tobytes()))
+            f.write(co.compress(synth.generate_records(sheet, a, b, R=8, seed=1,
+                                                       rc_names=SHAPES[cfg]["rc_names"]).tobytes()))
         f.write(co.flush())
     return path
 

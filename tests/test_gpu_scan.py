@@ -1040,7 +1040,9 @@ def test_bench_geometry_pinned_cfg34(lib, cfg):
     c = lib.Context(device=0, chunk_bytes=(16 << 30) - (1 << 20), table_slots=1 << 22)
     buf = c.device_alloc(n * reclen + 64)
     try:
-        c.synth_device(buf, 0, n, 8, 1, sheet.idx1, sheet.idx2)
+        # config 3: the reads of synth.CFG3_RC_NAMES carry rc(idx2), so the per-name call flips them
+        c.synth_device(buf, 0, n, 8, 1, sheet.idx1,
+                       synth.read_idx2(sheet, synth.CFG3_RC_NAMES if cfg == 3 else None))
         for step in range(2):
             c.reset()
             c.begin_file(None, file_index=0, byte_base=0)
@@ -1051,6 +1053,8 @@ def test_bench_geometry_pinned_cfg34(lib, cfg):
             c.finalize()
             got = synth.pin_rows(c, sheet, 1 if cfg == 3 else 2, cfg == 3)
             assert synth.pin_differences(got, pin) == [], (cfg, step)
+            if cfg == 3:  # pass B ran on the rewritten idx2 list
+                assert sorted(r[0] for r in got["rc_calls"] if r[3]) == sorted(synth.CFG3_RC_NAMES)
         # the second feed: config 4 (no commit logs) one launch; config 3's commits log, so its ranges stay
         # <= 4 GiB (one launch-log aggregation per range: its LDS fold holds that many distinct codes)
         assert launches == (2 if cfg == 3 else 1), launches

@@ -50,7 +50,9 @@ def test_oracle_cfg2_prefix_pinned():
     with open(os.path.join(os.path.dirname(__file__), "golden", "cfg2_pin_1m.json")) as f:
         pin = json.load(f)
     sheet = synth.make_sheet(96, 8, 8)
-    counts, records = O.tally_text(synth.generate_bytes(sheet, 0, pin["reads"], R=8, seed=1).decode())
+    rc_names = synth.CFG3_RC_NAMES if cfg == 3 else None  # their reads carry rc(idx2): the call flips them
+    counts, records = O.tally_text(synth.generate_bytes(sheet, 0, pin["reads"], R=8, seed=1,
+                                                        rc_names=rc_names).decode())
     assert records == pin["total_reads"] and len(counts) == pin["unique_codes"]
     codes = list(counts)
     with Pool(4) as pool:
@@ -97,7 +99,9 @@ def test_oracle_cfg34_prefix_pinned(cfg):
     nsubs = 1 if cfg == 3 else 2
     L, S = (10, 384) if cfg == 3 else (8, 96)
     sheet = synth.make_sheet(S, L, L, combinatorial=(12, 8) if cfg == 4 else None)
-    counts, records = O.tally_text(synth.generate_bytes(sheet, 0, pin["reads"], R=8, seed=1).decode())
+    rc_names = synth.CFG3_RC_NAMES if cfg == 3 else None  # their reads carry rc(idx2): the call flips them
+    counts, records = O.tally_text(synth.generate_bytes(sheet, 0, pin["reads"], R=8, seed=1,
+                                                        rc_names=rc_names).decode())
     assert records == pin["total_reads"] and len(counts) == pin["unique_codes"]
     codes = list(counts)
     keep = len(pin["first_rows"])
@@ -116,6 +120,7 @@ def test_oracle_cfg34_prefix_pinned(cfg):
                     sums[r["rc_sample_name"]][1] += r["reads"]
             calls = [[n, f, b, f < b] for n, (f, b) in sums.items()]
             assert calls == pin["rc_calls"]
+            assert sorted(n for n, _, _, c in calls if c) == sorted(synth.CFG3_RC_NAMES)
             use = {n: c for n, _, _, c in calls}
             idx2 = [reverse_complement(x) if use[i] else x for i, x in zip(sheet.ids, idx2)]
             res = pool.starmap(O.classify_code, [(c, counts[c], sheet.idx1, idx2, sheet.ids, nsubs, False)

@@ -50,9 +50,7 @@ def test_oracle_cfg2_prefix_pinned():
     with open(os.path.join(os.path.dirname(__file__), "golden", "cfg2_pin_1m.json")) as f:
         pin = json.load(f)
     sheet = synth.make_sheet(96, 8, 8)
-    rc_names = synth.CFG3_RC_NAMES if cfg == 3 else None  # their reads carry rc(idx2): the call flips them
-    counts, records = O.tally_text(synth.generate_bytes(sheet, 0, pin["reads"], R=8, seed=1,
-                                                        rc_names=rc_names).decode())
+    counts, records = O.tally_text(synth.generate_bytes(sheet, 0, pin["reads"], R=8, seed=1).decode())
     assert records == pin["total_reads"] and len(counts) == pin["unique_codes"]
     codes = list(counts)
     with Pool(4) as pool:

@@ -610,6 +610,7 @@ def main():
     traffic, traffic_note, valu = load_traffic(args.traffic_json, _lib.source_tree_hash(), per_launch_bytes,
                                          args.samples, args.index_len, args.combinatorial)
 
+    dg = ctx.diag()  # the last feed's launch-log folds (fullest sub-region of 4096 slots, overflowed entries)
     csum = table_checksum(ctx, U) if (world == 1 or args.merge == "a2a" or rank == 0) else 0
     if world > 1 and args.merge == "a2a":  # report the merged table's size (sum of the partitions)
         U, csum = (int(x) for x in reduce_sum(dist, wire, [U, csum]))
@@ -648,6 +649,7 @@ def main():
                          "kernel": "fr::chunk_kernel", "bytes_per_launch": int(per_launch_bytes),
                          "avg_launch_ms": round(per_launch_ms, 4), "launches_per_step": int(launches),
                          "log_aggregation_ms_per_launch": round(t_after.log_ms / max(launches, 1), 4),
+                         "log_fold": {"max": dg["fold_max"], "over": dg["fold_over"], "slots": 4096},
                          "valu_issue": valu_roofline(valu, per_launch_ms)},
             "cpu_baseline": cpu,
             "e2e": _E2E,

@@ -835,8 +835,8 @@ class Context:
         return t
 
     def diag(self) -> dict:
-        v = np.zeros(21, dtype=np.uint64)
-        self._ck(lib.fr_get_diag(self.h, _ptr(v), 21), "fr_get_diag")
+        v = np.zeros(24, dtype=np.uint64)
+        self._ck(lib.fr_get_diag(self.h, _ptr(v), 24), "fr_get_diag")
         d = dict(zip(("spin_max", "spin_total", "keys", "overflow", "presence", "exotic", "grid", "slots"),
                      v[:8].tolist()))
         d["spec_replays"] = int(v[16])
@@ -844,6 +844,9 @@ class Context:
         d["chunk_tiles"] = int(v[18])  # full-chunk size of the next ramped launch (larger once commits log)
         d["heavy_launches"] = int(v[19])  # ramped launches since the reset that walked the heavy chunk size
         d["big_rollbacks"] = int(v[20])  # big feeds replayed in logged ranges (the table ran out of room)
+        d["fold_max"] = int(v[21])  # the last device feed's fullest launch-log fold (of AGG_LNS = 4096 slots)
+        d["fold_over"] = int(v[22])  # its entries that found their fold full
+        d["feed_step"] = int(v[23])  # its range size (bytes per launch)
         if v[8:16].any():  # FR_TIMING build / FR_ABLATE=64: per-phase cycles or commit counts
             names = ("guess", "walk0", "wait0", "resolve", "walk1", "commit", "kernel", "chunks")
             d["stamps"] = dict(zip(names, v[8:].tolist()))

@@ -59,9 +59,10 @@ struct fr_ctx {
     u32 log_scap = 0;
     void* log_temp = nullptr;
     size_t log_temp_bytes = 0;
-    u32 log_min = 2600;            // pairs from which a commit logs (SYN-v1 config 2's full chunks commit ~1740 pairs
-                                   // and are faster inserted directly; config 3's ~2680 are faster logged)
-    u32 log_hot = 4;               // a logged commit's LDS entries of >= log_hot records insert directly (FR_LOG_HOT)
+    u32 log_min = 0;               // pairs from which a commit logs (round 6: every commit.  Direct commits are bound by
+                                   // the memory-side atomics, ~23.7 G/s chip-wide whatever their scope or footprint:
+                                   // scripts/ubench_l2atomic.hip; config 2's ~12M per 100M reads cost 0.4 ms)
+    u32 log_hot = 0xFFFFFFFFu;     // a logged commit's LDS entries of >= log_hot records insert directly (round 6: none)
     uint4* rare = nullptr;
 
     DevState* st = nullptr;
@@ -101,9 +102,12 @@ struct fr_ctx {
     u64 ring_bytes = 0;
     u64 feed_keys = ~0ull;    // codes the last device feed created (a range over RANGE_FIRST_MAX needs table room for them)
     bool feed_logged = true;  // the last device feed's commits went to the launch log: its ranges stay <= RANGE_FIRST_MAX
-                              // (one aggregation over a bigger range has more distinct codes per sub-region than
-                              // log_reduce_kernel's LDS fold holds: measured 15 ms instead of 0.28 per launch at the
-                              // config-3 shape)
+                              // unless its folds had room (one aggregation over a bigger range has more distinct codes
+                              // per sub-region than log_reduce_kernel's LDS fold holds: measured 15 ms instead of 0.28
+                              // per launch at the config-3 shape)
+    u32 feed_fold_max = 0;    // the last device feed's fullest sub-region fold, its fold overflows and range size:
+    u32 feed_fold_over = 0;   // a logged feed's next ranges may exceed RANGE_FIRST_MAX when the folds, scaled by the
+    u64 feed_step = 0;        // range size, stay at most 0.85 full
     u32 chunk_tiles = 320;  // wave-tiles (4 KiB) per full chunk of a ramped launch (FR_CHUNK_TILES; round 2's
                             // 80 workgroup tiles of 16 KiB: 64-96 measured within 2 %, 80 best)
     // Ramped launches after one in which at least a quarter of the chunks since the reset logged their
@@ -599,10 +603,9 @@ static int launch_range(fr_ctx* ctx, const u8* dptr, u64 len, u64 avail, int own
     }
     a.cold_cap = ctx->cold_cap;
     a.cold = ctx->cold;
-    // launch-log offsets fold as u32 in log_reduce_kernel, and one aggregation's distinct codes must fit its
-    // LDS fold: a range over RANGE_FIRST_MAX runs without the log (fr_feed_device takes one only after a feed
-    // that did not log)
-    a.log = (exo_only || len > RANGE_FIRST_MAX) ? nullptr : ctx->log;
+    // launch-log first occurrences fold in 32 bits (4-B ordinals: ranges up to RANGE_MAX); one aggregation's
+    // distinct codes must fit its LDS fold, which fr_feed_device's range size sees to
+    a.log = exo_only ? nullptr : ctx->log;
     a.log_cap = ctx->log_cap;
     a.log_rcap = ctx->log_rcap;
     a.log_min = ctx->log_min;
@@ -706,8 +709,7 @@ fr_ctx* fr_create_tuned(int device, uint64_t chunk_bytes, uint64_t table_slots, 
     if (t.log) {
         // entries: 1 per 256 B of a launch (SYN-v1 config 3 logs ~1 per 700 B), in LOG_NR equal regions;
         // a run past its region's end inserts directly
-        const u64 want = std::min<u64>(std::max<u64>(std::min<u64>(ctx->chunk_bytes, RANGE_FIRST_MAX) / 256, 1ull << 16),
-                                       1ull << 26);  // logged ranges are <= RANGE_FIRST_MAX
+        const u64 want = std::min<u64>(std::max<u64>(ctx->chunk_bytes / 256, 1ull << 16), 1ull << 26);
         ctx->log_rcap = (u32)(want / LOG_NR);
         ctx->log_cap = (u64)ctx->log_rcap * LOG_NR;
         ctx->log_scap = (u32)std::max<u64>(2ull * ctx->log_rcap / LOG_SUBS, 64);  // 2x the mean share
@@ -813,7 +815,7 @@ int fr_get_diag(fr_ctx* ctx, uint64_t* out, int n) {
                           (uint64_t)ctx->grid, ctx->nslots, s.stamp[0], s.stamp[1], s.stamp[2], s.stamp[3],
                           s.stamp[4],  s.stamp[5],  s.stamp[6], s.stamp[7], ctx->spec_replays, ctx->exo_replays,
                           s.heavy[ctx->par] ? ctx->chunk_tiles_heavy : ctx->chunk_tiles,  // the next ramped launch's
-                          s.heavy_launches, ctx->big_rollbacks};
+                          s.heavy_launches, ctx->big_rollbacks, ctx->feed_fold_max, ctx->feed_fold_over, ctx->feed_step};
     for (int i = 0; i < n && i < (int)(sizeof(v) / sizeof(v[0])); ++i) out[i] = v[i];
     return FR_OK;
 }
@@ -1108,11 +1110,19 @@ int fr_feed_device(fr_ctx* ctx, const uint8_t* dev_data, uint64_t len) {
     // slots and the overflow list -- is rolled back like a wrong speculation and replayed in ranges of an
     // eighth of the size, with the table grown between them (each launch's state read before the next),
     // down to RANGE_ROOM_MIN (speculative feeds: the rollback needs the snapshot).
-    bool big = spec && !ctx->feed_logged && ctx->feed_keys != ~0ull &&
+    // a logged feed's folds, scaled to this feed's big range, at most 0.85 full (distinct codes grow slower than the
+    // bytes: config 2's 3.7-GB halves fill at most 1 626 of 4 096 slots, projected 3 252 for 7.4 GB; config 3's 3.9-GB
+    // halves 2 424 (projected 4 848), scripts/fold_probe.py)
+    const double big_range = (double)std::min<u64>(ctx->chunk_bytes, len);
+    const bool fold_room = ctx->feed_fold_over == 0 && ctx->feed_step > 0 &&
+                           (double)ctx->feed_fold_max * big_range <= 0.85 * AGG_LNS * (double)ctx->feed_step;
+    bool big = spec && (!ctx->feed_logged || fold_room) && ctx->feed_keys != ~0ull &&
                (saved.n_keys + ctx->feed_keys) * 2 <= ctx->nslots;
     bool spec_now = spec;
     u64 step = 0, lim_room = ~0ull;
     for (int attempt = 0; attempt < 12; ++attempt) {
+        // the attempt's fold statistics start at zero (a rollback restores the state before the feed)
+        CK(hipMemsetAsync(&ctx->st->log_fold_max, 0, 2 * sizeof(u32), ctx->stream));
         const u64 lim = std::min<u64>(big ? ctx->chunk_bytes : std::min<u64>(ctx->chunk_bytes, RANGE_FIRST_MAX),
                                       lim_room);
         const u64 nr = (len + lim - 1) / lim;
@@ -1166,6 +1176,9 @@ int fr_feed_device(fr_ctx* ctx, const uint8_t* dev_data, uint64_t len) {
     if (rc) return rc;
     ctx->feed_keys = ctx->h_st->n_keys - saved.n_keys;
     ctx->feed_logged = ctx->h_st->log_commits != saved.log_commits;  // read_state above: exact
+    ctx->feed_fold_max = ctx->h_st->log_fold_max;
+    ctx->feed_fold_over = ctx->h_st->log_fold_over;
+    ctx->feed_step = step;
     // exotic records overflowed the list: grow it to the counted totals and run the feed's launches
     // again capturing exotic records only (the table is already complete), then drain
     rc = read_state(ctx);

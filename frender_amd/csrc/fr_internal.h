@@ -108,6 +108,7 @@ constexpr int LOG_NR = 1 << LOG_REGION_BITS;  // launch-log regions (parts of th
 constexpr int LOG_SUB_BITS = FR_LOG_SUB_BITS;
 constexpr int LOG_SUBS = 1 << LOG_SUB_BITS;   // sub-regions per region (aggregation workgroups)
 constexpr int LOG_NSUB = LOG_NR * LOG_SUBS;    // sub-regions in all
+constexpr int AGG_LNS = 4096;  // LDS slots of one sub-region's fold in log_reduce_kernel (64 KB: 2 workgroups per CU)
 
 struct DevState {
     // per-file block (contiguous: fr_begin_file resets it with one copy from the reset image)
@@ -144,6 +145,8 @@ struct DevState {
     u32 log_rcur[LOG_NR];  // per launch-log region: entries claimed this launch (the aggregation zeroes them)
     u32 log_scur[LOG_NSUB];  // per sub-region: entries the split pass placed (the aggregation zeroes them)
     u32 log_red_done;    // aggregation workgroups finished (the last zeroes it)
+    u32 log_fold_max;    // the fullest sub-region fold (distinct codes) of the current device feed's aggregations
+    u32 log_fold_over;   // entries that found their sub-region's fold full (inserted on their own)
 };
 
 struct Table {

@@ -277,9 +277,14 @@ typedef u32 u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) u32 lds_u32;
 typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
 typedef __attribute__((address_space(3))) u64 lds_u64;
+typedef __attribute__((address_space(3))) u8 lds_u8;
 
+// Ordinal of a record: file tag << 44 | its header's file offset rounded down to a multiple of 4.  Record
+// starts are >= 4 bytes apart (four lines of >= 1 byte), so the rounding keeps every comparison of two
+// records' ordinals, i.e. the first-occurrence order; it lets the launch log's fold keep a first
+// occurrence in 32 bits for launches up to 16 GiB (log_reduce_kernel).  Every path rounds alike.
 __device__ __forceinline__ u64 make_ord(const ScanArgs& a, u64 off_in_range) {
-    return ((u64)a.file_tag << ORD_SHIFT) | (a.file_offset + off_in_range);
+    return ((u64)a.file_tag << ORD_SHIFT) | ((a.file_offset + off_in_range) & ~3ull);
 }
 
 __device__ __forceinline__ u32 wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
@@ -1098,7 +1103,7 @@ __device__ __attribute__((noinline)) void commit_buffers(ScanShared& sh, const S
                 const bool v1[1] = {true};
                 Resolved r1[1];
                 made += resolve_batch<1>(a, k1, v1, r1);
-                apply_entry(a, r1[0], k, cnt, ord0 + off);
+                apply_entry(a, r1[0], k, cnt, make_ord(a, off));  // (off: a launch offset, or a multiple of 4 past ord0)
             }
         };
         u64 hk[CL];
@@ -1398,11 +1403,44 @@ __device__ __forceinline__ bool encode_uniform(const ScanShared& sh, u32 wid, u3
     return bad == 0;
 }
 
+// R2 from the line start p in ONE window of the ' ' | line-end bitmap and one of the ':' bitmap (round 6):
+// f1 = the first ' ' or line end, the token end = the next one (the window's second set bit), the code
+// start = one past the last ':' before the token end, or the token start when the token has none.  The
+// byte at f1 tells a ' ' from a line end (IndexError), read from the wave's tile copy with the code.
+// Branch-free: 0 code at [start, start + n) (tile offsets); 2 word-scan fallback (the line starts past the
+// staged bytes, or no ' ' / line end within 64 bytes); 3 the token ends past the window (a first token of
+// 40-odd bytes: Illumina instrument headers), which locate_code finishes from the token start.
+__device__ __forceinline__ int locate_near(const ScanShared& sh, u32 wid, u32 p, u32 bl, u32& start, u32& n, u32& f1) {
+    const u32 w = min(p >> 6, (u32)SEGS - 1u), b = p & 63u;
+    const lds_u64* S = (const lds_u64*)&sh.bsp[wid][w];
+    const lds_u64* C = (const lds_u64*)&sh.bcol[wid][w];
+    u64 s0 = S[0], s1 = S[1], c0 = C[0], c1 = C[1];
+    asm volatile("" : "+v"(s0), "+v"(s1), "+v"(c0), "+v"(c1));  // one LDS round, before any use
+    const u64 se = window64(s0, s1, b);
+    const u64 co = window64(c0, c1, b);
+    const u64 se1 = se & (se - 1ull);
+    f1 = ctz64x(se);
+    const u32 f2 = ctz64x(se1);
+    const int hc = hsb64x(co & ((1ull << (f2 & 63u)) - 1ull));  // the last ':' before the token end (< 0: none)
+    const u32 cs = (u32)max(hc, (int)f1) + 1u;                  // a ':' of the first token does not count
+    start = p + cs;
+    n = f2 - cs;
+    return (p >= bl || se == 0ull) ? 2 : (se1 == 0ull ? 3 : 0);
+}
+
 __device__ __forceinline__ void parse_header(ScanShared& sh, const ScanArgs& a, u32 wid, u32 tile0, u32 p, u32 bl) {
-    u32 start = 0, n = 0;
-    const int r = locate_code(sh, wid, p, bl, start, n);
+    u32 start = 0, n = 0, f1 = 0;
+    int r = locate_near(sh, wid, p, bl, start, n, f1);
+    if (__ballot(r == 3) != 0) {  // uniform: some lane's token ends past its first window
+        if (r == 3) {
+            r = locate_code(sh, wid, p, bl, start, n);  // decides "no ' '" itself
+            f1 = 0xFFFFFFFFu;
+        }
+    }
+    // the first delimiter's byte (in the staged bytes whenever r == 0 and f1 < 64): not a ' ' -> a line end
+    const u32 dch = *((const lds_u8*)&sh.raw[wid][0] + min(p + f1, (u32)TILE - 1u));
     if (ABLATE & 2u) {
-        asm volatile("" ::"v"(start), "v"(n), "v"(r));
+        asm volatile("" ::"v"(start), "v"(n), "v"(r), "v"(dch));
         return;
     }
     u64 key = 0;
@@ -1417,6 +1455,10 @@ __device__ __forceinline__ void parse_header(ScanShared& sh, const ScanArgs& a, 
             fast = encode_pack(w, start, n, key);
         }
     }
+    if (r == 0 && f1 < 64u && dch != (u32)' ') {  // the line ends before any ' ': IndexError (:169)
+        r = 1;
+        fast = false;
+    }
     if (fast) count_code(sh, a, tile0 + p, key);
     else rare_push(sh, a, tile0 + p, (u32)r, tile0 + start, n);
 }
@@ -1425,6 +1467,7 @@ __device__ __forceinline__ void parse_header(ScanShared& sh, const ScanArgs& a, 
 // where they lie.  L0 = lines before the wave-tile (absolute with -s, else mod 4 suffices).  The
 // first header needs the skip-th set bit of the terminator mask; a second one in the same segment
 // (records shorter than 64 B) takes the loop at the end.
+template <bool LIM>
 __device__ __forceinline__ void parse_own_headers(ScanShared& sh, const ScanArgs& a, u32 t, u32 ct,
                                                   const SegClass& sc, u64 L0, int lane, u32 wid) {
     const u64 tile0 = (u64)t * TSTEP;
@@ -1441,15 +1484,13 @@ __device__ __forceinline__ void parse_own_headers(ScanShared& sh, const ScanArgs
         const u64 d = m & (m - 1ull);
         m = q < skip ? d : m;
     }
-#ifdef FR_NOLIMIT
-    const bool limited = false;
-#else
-    const bool limited = a.max_records > 0;  // -s: uniform
-#endif
+    constexpr bool limited = LIM;  // -s (a.max_records > 0): the kernel instance's, so the common one has no record limit
     u64 rec = 0;
     if (limited) rec = (L0 + (sc.x - sc.c) + skip + 1u) >> 2;
-    const bool own0 = t == 0 && lane == 0 && a.own_start && (L0 & 3ull) == 0 && a.avail > 0 &&
-                      (!limited || (i64)(L0 >> 2) < a.max_records);
+    // the range's own first line start (position 0): lane 0 of the range's first tile; the rest is wave-uniform
+    const bool own0s = t == 0 && a.own_start && (L0 & 3ull) == 0 && a.avail > 0 &&
+                       (!limited || (i64)(L0 >> 2) < a.max_records);
+    const bool own0 = own0s && lane == 0;
     // m's lowest set bit: the first header terminator.  own0's header at position 0 comes first.
     const u32 p = own0 ? 0u : s0 + ctz64x(m) + 1u;
     const bool ok = own0 || (m != 0 && p < pend && (!limited || (i64)rec < a.max_records));
@@ -1485,6 +1526,7 @@ __device__ __forceinline__ void parse_own_headers(ScanShared& sh, const ScanArgs
 // (in registers since the previous step) go to the wave's LDS copy first, so the registers take the
 // next tile's loads at once and those stay in flight through this tile's classify AND its parse;
 // the classify reads the lane's segment back from LDS.
+template <bool LIM>
 __device__ __forceinline__ u64 walk_wave(ScanShared& sh, const ScanArgs& a0, u32 ct, u32 tb, u32 te, u64 L0,
                                          bool parse, int lane, u32 wid) {
     const ScanArgs& a = a0;
@@ -1529,7 +1571,7 @@ __device__ __forceinline__ u64 walk_wave(ScanShared& sh, const ScanArgs& a0, u32
         // redone exactly and everything its walk buffered is discarded, so parsing on is harmless; the check
         // was an LDS round trip per tile)
         FR_WSTAMP(2);
-        if (parse && !(ABLATE & 1u)) parse_own_headers(sh, a, t, ct, sc, L0 + lines, lane, wid);
+        if (parse && !(ABLATE & 1u)) parse_own_headers<LIM>(sh, a, t, ct, sc, L0 + lines, lane, wid);
         lines += sc.wtot;
         FR_WSTAMP(3);
     }
@@ -1639,6 +1681,9 @@ extern "C" int fr_trace_clear() {
 #define FR_OCC 4  // workgroups (= waves per SIMD) per CU: ~39 KB of LDS per workgroup (the wave-tile copies
                   // and the LDS table) fit 4 in a CU's 160 KB; fr_api sizes the grid with chunk_occupancy()
 #endif
+// LIM: -s (a.max_records > 0), the launch's instance (launch_chunk_scan): the record limit's checks are not in the
+// common instance's tile loop
+template <bool LIM>
 __global__ __launch_bounds__(WG, FR_OCC) void chunk_kernel(ScanArgs args) {
     // every helper reads the arguments where they lie (the kernarg segment): the out-of-line
     // helpers take them by reference without a scratch copy of the struct
@@ -1676,7 +1721,7 @@ __global__ __launch_bounds__(WG, FR_OCC) void chunk_kernel(ScanArgs args) {
                                                                      __HIP_MEMORY_SCOPE_AGENT)) != 0;
     const Geom g = hv ? Geom{a.chunk_tiles_h, a.mid_chunks_h, a.num_chunks_h, a.ramp_down_g_h}
                       : Geom{a.chunk_tiles, a.mid_chunks, a.num_chunks, a.ramp_down_g};
-    const bool limited = a.max_records > 0;
+    constexpr bool limited = LIM;
 #if defined(FR_STAMPS) && (FR_STAMPS == 1 || FR_STAMPS == 4)
     const u64 k0_ = __builtin_amdgcn_s_memtime();
 #endif
@@ -1737,7 +1782,7 @@ __global__ __launch_bounds__(WG, FR_OCC) void chunk_kernel(ScanArgs args) {
         u64 base = base_lines;
         for (int pass = 0;; ++pass) {
             FR_TRACE("w%d pass %d run %d [%u,%u) parse %d\n", (int)wid, pass, (int)run, wb, we, (int)parse);
-            const u64 n = run ? walk_wave(sh, a, tb, wb, we, L0, parse, lane, wid) : 0ull;
+            const u64 n = run ? walk_wave<LIM>(sh, a, tb, wb, we, L0, parse, lane, wid) : 0ull;
             FR_TRACE("w%d walked %llu\n", (int)wid, (unsigned long long)n);
             FR_STAMP(pass == 0 ? 1 : 4);
             if (pass == 0) {
@@ -1857,7 +1902,8 @@ __global__ __launch_bounds__(WG, FR_OCC) void chunk_kernel(ScanArgs args) {
 int chunk_occupancy() { return FR_OCC; }
 
 hipError_t launch_chunk_scan(const ScanArgs& a, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(chunk_kernel, dim3(grid), dim3(WG), 0, s, a);
+    if (a.max_records > 0) hipLaunchKernelGGL(chunk_kernel<true>, dim3(grid), dim3(WG), 0, s, a);
+    else hipLaunchKernelGGL(chunk_kernel<false>, dim3(grid), dim3(WG), 0, s, a);
     return hipGetLastError();
 }
 
@@ -1951,7 +1997,6 @@ __device__ __forceinline__ bool last_block(u32* ctr) {
     return last != 0;
 }
 
-constexpr int AGG_LNS = 4096;  // LDS slots of one sub-region's aggregation (64 KB: 2 workgroups per CU)
 constexpr int AGG_PROBE = 64;
 constexpr int CLAIM_WORDS = 1024;  // a reduce workgroup's claim bitmap: sub-regions of up to 32K slots (4 KB; tables of up to 16 Mi slots)
 struct alignas(16) AggSlot {
@@ -2156,7 +2201,7 @@ __global__ __launch_bounds__(256) void log_split_kernel(Table t, DevState* st, c
             } else {
                 const u64 key1[1] = {e[q].key};
                 const u32 cnt1[1] = {log_cnt(e[q].oc)};
-                const u64 ord1[1] = {ord0 + log_off(e[q].oc)};
+                const u64 ord1[1] = {(ord0 + log_off(e[q].oc)) & ~3ull};  // make_ord's rounding
                 const u32 tag1[1] = {file_tag};
                 const bool v1[1] = {true};
                 made += insert_rows<1>(t, st, key1, cnt1, ord1, tag1, v1);
@@ -2171,7 +2216,15 @@ __global__ __launch_bounds__(256) void log_split_kernel(Table t, DevState* st, c
 // folded in LDS (records summed, min offset), then its distinct codes inserted into the HBM table with
 // the launch's ordinal base and file tag.  The sub-regions partition the codes, so found and claimed
 // slots take plain stores (insert_rows EXCL).  The last workgroup empties the log for the next launch.
-__global__ __launch_bounds__(256) void log_reduce_kernel(Table t, DevState* st, const LogEntry* sub, u32 scap,
+// RED_WG threads (round 6: 512, was 256): the fold's LDS table (64 KB) allows two workgroups per CU, and
+// with 256 threads that left 2 waves per SIMD to cover the entry loads' and the inserts' round trips (1 024
+// threads need 114 VGPRs: one workgroup per CU, and the 512 sub-regions would run in two rounds).
+#ifndef FR_RED_WG
+#define FR_RED_WG 512
+#endif
+constexpr int RED_WG = FR_RED_WG;
+constexpr int RED_FB = RED_WG >= 512 ? 4 : 8;  // distinct codes per thread per insert batch (4: <= 128 VGPRs, two workgroups per CU)
+__global__ __launch_bounds__(RED_WG) void log_reduce_kernel(Table t, DevState* st, const LogEntry* sub, u32 scap,
                                                          u32 file_tag, u64 ord0) {
     if (st->log_n == 0) return;
     __shared__ AggSlot ls[AGG_LNS];
@@ -2179,30 +2232,33 @@ __global__ __launch_bounds__(256) void log_reduce_kernel(Table t, DevState* st, 
     __shared__ u16 occ[AGG_LNS];  // the occupied slots of ls, listed for the inserts
     __shared__ u32 occ_n;
     u32 made = 0;
-    for (int i = threadIdx.x; i < AGG_LNS; i += 256) ls[i] = AggSlot{0, 0xFFFFFFFFu, 0};
+    for (int i = threadIdx.x; i < AGG_LNS; i += RED_WG) ls[i] = AggSlot{0, 0xFFFFFFFFu, 0};
     // this sub-region's home range: slots [blockIdx.x n, (blockIdx.x + 1) n) of the table (table_home's top
     // bits are the region and sub-region bits); its claim zone skips the first GPROBE slots
     const u64 nslots = t.mask + 1ull, rn = nslots >= (u64)LOG_NSUB ? nslots / LOG_NSUB : 0ull;
     ClaimZone cz{nullptr, 0, 0, 0};
     if (rn > 2ull * GPROBE && rn <= 32ull * CLAIM_WORDS && !(ABLATE & 2048u)) {
         cz = ClaimZone{zone_bits, (u64)blockIdx.x * rn, (u64)blockIdx.x * rn + GPROBE, (u64)(blockIdx.x + 1) * rn};
-        for (u32 i = threadIdx.x; i < (u32)(rn / 32); i += 256) zone_bits[i] = 0;
+        for (u32 i = threadIdx.x; i < (u32)(rn / 32); i += RED_WG) zone_bits[i] = 0;
     }
     __syncthreads();
     const u32 n = min(st->log_scur[blockIdx.x], scap);
     const LogEntry* part = sub + (u64)blockIdx.x * scap;
+    // a first occurrence folds as v = its ordinal's offset / 4 - the launch base's (make_ord's rounding): 32 bits
+    // for launches up to 16 GiB; the ordinal is tag | (base4 + v) << 2
+    const u64 base4 = (ord0 & ((1ull << ORD_SHIFT) - 1ull)) >> 2, tagpart = ord0 & ~((1ull << ORD_SHIFT) - 1ull);
     u64 sink = 0;
     constexpr int LB = 8;  // entries per thread per batch; the next batch's loads fly during this one's fold
     const u32 nn = (ABLATE & 512u) ? 0u : n;  // 512: timing ablation
     LogEntry nx[LB];
 #pragma unroll
-    for (int q = 0; q < LB; ++q) nx[q] = threadIdx.x + q * 256 < nn ? part[threadIdx.x + q * 256] : LogEntry{0, 0};
-    for (u32 i0 = threadIdx.x; i0 < nn; i0 += LB * 256) {
+    for (int q = 0; q < LB; ++q) nx[q] = threadIdx.x + q * RED_WG < nn ? part[threadIdx.x + q * RED_WG] : LogEntry{0, 0};
+    for (u32 i0 = threadIdx.x; i0 < nn; i0 += LB * RED_WG) {
         LogEntry ev[LB];
 #pragma unroll
         for (int q = 0; q < LB; ++q) {
             ev[q] = nx[q];
-            const u32 j = i0 + LB * 256 + q * 256;
+            const u32 j = i0 + LB * RED_WG + q * RED_WG;
             nx[q] = j < nn ? part[j] : LogEntry{0, 0};
         }
 #pragma unroll
@@ -2213,7 +2269,7 @@ __global__ __launch_bounds__(256) void log_reduce_kernel(Table t, DevState* st, 
                 sink ^= e.key;
                 continue;
             }
-            const u32 eoff = (u32)log_off(e.oc);  // (a logged launch is < 4 GiB)
+            const u32 eoff = (u32)((((ord0 & ((1ull << ORD_SHIFT) - 1ull)) + log_off(e.oc)) >> 2) - base4);
             const u32 ecnt = log_cnt(e.oc);
             u32 h = (u32)mix64(e.key) & (AGG_LNS - 1);
             bool done = false;
@@ -2234,37 +2290,39 @@ __global__ __launch_bounds__(256) void log_reduce_kernel(Table t, DevState* st, 
             if (!done) {  // a full LDS table: this row goes in on its own
                 const u64 key1[1] = {e.key};
                 const u32 cnt1[1] = {ecnt};
-                const u64 ord1[1] = {ord0 + eoff};
+                const u64 ord1[1] = {tagpart | ((base4 + eoff) << 2)};
                 const u32 tag1[1] = {file_tag};
                 const bool v1[1] = {true};
                 made += insert_rows<1>(t, st, key1, cnt1, ord1, tag1, v1, cz);
+                atomicAdd(&st->log_fold_over, 1u);  // the fold was full: the next feeds keep smaller logged launches
             }
         }
     }
     if (sink == 1) atomicAdd((unsigned long long*)&st->stamp[7], 1ull);  // keeps the ablation's loads
     __syncthreads();
     // the distinct codes into the table: the occupied slots listed first (LDS), then FB of them per thread in
-    // flight -- one batch of probe loads covers 256 * FB codes, instead of one batch per FB slots scanned
+    // flight -- one batch of probe loads covers RED_WG * FB codes, instead of one batch per FB slots scanned
     // (half of them empty at the fold's usual load)
     if (threadIdx.x == 0) occ_n = 0;
     __syncthreads();
-    for (int i = threadIdx.x; i < AGG_LNS; i += 256)
+    for (int i = threadIdx.x; i < AGG_LNS; i += RED_WG)
         if (ls[i].key) occ[atomicAdd(&occ_n, 1u)] = (u16)i;
     __syncthreads();
-    constexpr int FB = 8;
+    if (threadIdx.x == 0) atomicMax(&st->log_fold_max, occ_n);  // the feed's fullest fold (fr_feed_device's launch size)
+    constexpr int FB = RED_FB;
     const u32 nocc = (ABLATE & 256u) ? 0u : occ_n;  // 256: timing ablation
-    for (u32 i0 = threadIdx.x; i0 < nocc; i0 += FB * 256) {
+    for (u32 i0 = threadIdx.x; i0 < nocc; i0 += FB * RED_WG) {
         u64 key[FB], ord[FB];
         u32 cnt[FB], tag[FB];
         bool v[FB];
 #pragma unroll
         for (int b = 0; b < FB; ++b) {
-            const u32 j = i0 + b * 256;
+            const u32 j = i0 + b * RED_WG;
             v[b] = j < nocc;
             const AggSlot e = v[b] ? ls[occ[j]] : AggSlot{0, 0, 0};
             key[b] = e.key;
             cnt[b] = e.cnt;
-            ord[b] = ord0 + e.mino;
+            ord[b] = tagpart | ((base4 + e.mino) << 2);
             tag[b] = file_tag;
         }
         made += insert_rows<FB, true>(t, st, key, cnt, ord, tag, v, cz);
@@ -2273,9 +2331,9 @@ __global__ __launch_bounds__(256) void log_reduce_kernel(Table t, DevState* st, 
     // every workgroup has read log_n and its cursor (the split pass read the region cursors before
     // this launch): the last one empties the log
     if (last_block(&st->log_red_done)) {
-        for (int i = threadIdx.x; i < LOG_NR; i += 256)
+        for (int i = threadIdx.x; i < LOG_NR; i += RED_WG)
             __hip_atomic_store(&st->log_rcur[i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (int i = threadIdx.x; i < LOG_NSUB; i += 256)
+        for (int i = threadIdx.x; i < LOG_NSUB; i += RED_WG)
             __hip_atomic_store(&st->log_scur[i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (threadIdx.x == 0) __hip_atomic_store(&st->log_n, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -2290,7 +2348,7 @@ hipError_t launch_log_aggregate(Table t, DevState* st, const LogEntry* log, u32 
     const u64 ord0 = ((u64)file_tag << ORD_SHIFT) | file_offset;
     hipLaunchKernelGGL(log_split_kernel, dim3(LOG_NR * SPLIT_WGS), dim3(256), 0, s, t, st, log, rcap, sub, scap, file_tag,
                        ord0);
-    hipLaunchKernelGGL(log_reduce_kernel, dim3(LOG_NSUB), dim3(256), 0, s, t, st, sub, scap, file_tag, ord0);
+    hipLaunchKernelGGL(log_reduce_kernel, dim3(LOG_NSUB), dim3(RED_WG), 0, s, t, st, sub, scap, file_tag, ord0);
     return hipGetLastError();  // log_reduce_kernel's last block emptied the log
 }
 

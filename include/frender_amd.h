@@ -110,7 +110,7 @@ int fr_set_timing(fr_ctx* ctx, int on);
 int fr_sync(fr_ctx* ctx);
 /* diagnostics: {look-back max polls, total polls, keys, overflow, presence, exotic, grid, slots,
  * 8 phase stamps, speculation replays, exotic-only replays, next full-chunk size, heavy launches,
- * big-feed rollbacks} */
+ * big-feed rollbacks, the last device feed's fullest launch-log fold, its fold overflows, its range bytes} */
 int fr_get_diag(fr_ctx* ctx, uint64_t* out, int n);
 
 /* ---- sample sheet (the idx1/idx2/id lists of get_indexes, frender.py:90-116) -------

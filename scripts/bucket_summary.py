@@ -21,7 +21,7 @@ def load(d):
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             for r in csv.DictReader(fh):
-                if not r["Kernel_Name"].startswith(KERNEL):
+                if KERNEL not in r["Kernel_Name"]:
                     continue
                 key = (os.path.dirname(f), int(r["Dispatch_Id"]))
                 per.setdefault(r["Counter_Name"], {}).setdefault(key, 0.0)

@@ -17,9 +17,9 @@ with tempfile.TemporaryDirectory() as d:
                     "--cuda-device-only", "-S", "-o", os.path.join(d, "k.s"), *sys.argv[1:], src], check=True,
                    stderr=subprocess.DEVNULL)
     asm = open(os.path.join(d, "k.s")).read()
-m = re.search(r"^_ZN2fr12chunk_kernelENS_8ScanArgsE:[^\n]*\n(.*?)s_endpgm", asm, re.S | re.M)
+m = re.search(r"^_ZN2fr12chunk_kernelILb0EEEvNS_8ScanArgsE:[^\n]*\n(.*?)s_endpgm", asm, re.S | re.M)
 body = m.group(1).splitlines()
-npos = asm.find(".name:           _ZN2fr12chunk_kernelENS_8ScanArgsE")
+npos = asm.find(".name:           _ZN2fr12chunk_kernelILb0EEEvNS_8ScanArgsE")
 lo = asm.rfind("\n  - .", 0, npos)
 hi = asm.find("\n  - .", npos)
 md = asm[lo:hi if hi > 0 else None]

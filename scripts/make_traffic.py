@@ -40,13 +40,13 @@ def per_dispatch(rs, counter):
     feeds are one launch), so dispatches under 70 % of the largest FETCH/WRITE/VALU value are dropped."""
     acc = {}
     for r in rs:
-        if r["Counter_Name"] == counter and r["Kernel_Name"].startswith(KERNEL):
+        if r["Counter_Name"] == counter and KERNEL in r["Kernel_Name"]:
             acc[int(r["Dispatch_Id"])] = acc.get(int(r["Dispatch_Id"]), 0.0) + float(r["Counter_Value"])
     if acc:
         top = max(acc.values())
         acc = {d: v for d, v in acc.items() if v >= 0.7 * top}
     keep = set(acc)
-    return acc, [r for r in rs if r["Counter_Name"] == counter and r["Kernel_Name"].startswith(KERNEL)
+    return acc, [r for r in rs if r["Counter_Name"] == counter and KERNEL in r["Kernel_Name"]
                  and int(r["Dispatch_Id"]) in keep]
 
 
@@ -103,7 +103,7 @@ def main():
     # the full-size launches' rocprof duration (the kernel trace of the same command): the --stats average
     # also counts the first feed's smaller launches
     durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
-            for r in rows(src + "/prof_trace/**/*kernel_trace.csv") if r["Kernel_Name"].startswith(KERNEL)]
+            for r in rows(src + "/prof_trace/**/*kernel_trace.csv") if KERNEL in r["Kernel_Name"]]
     full = [d for d in durs if durs and d >= 0.7 * max(durs)]
     out = {
         "round": int(os.environ.get("ROUND", "5")),

@@ -101,6 +101,76 @@ __global__ void valu_kernel(u32* out, u64* cyc, int iters, u32 a, u32 b) {  // c
     }
 }
 
+// Steady state (round 6): every wave spins until the common start time t0 (s_memrealtime, 100 MHz, read
+// on the device by a one-lane kernel just before the launch, plus a lead for the dispatch), then runs
+// blocks of 16 chain steps and checks the time after each, until t0 + window; only the instructions
+// issued inside [t0, t0 + window) are counted, so launch ramps and tails are outside the measurement.
+__global__ void now_kernel(u64* t) { t[0] = __builtin_amdgcn_s_memrealtime(); }
+
+template <int K>
+__global__ void valu_deadline_kernel(u32* out, u64* cnt, const u64* t0p, u64 lead, u64 window, u32 a, u32 b) {
+    u32 x[8];
+    u64 y[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        x[i] = threadIdx.x * 7u + i;
+        y[i] = ((u64)x[i] << 32) | x[i];
+    }
+    const u64 t0 = t0p[0] + lead, t1 = t0 + window;
+    while (__builtin_amdgcn_s_memrealtime() < t0) __builtin_amdgcn_s_sleep(1);
+    const u64 c0 = __builtin_amdgcn_s_memtime();
+    u64 blocks = 0;
+    for (;;) {
+#pragma unroll 1
+        for (int it = 0; it < 16; ++it) step<K>(x, y, a, b);
+        ++blocks;
+        if (__builtin_amdgcn_s_memrealtime() >= t1) break;
+    }
+    const u64 c1 = __builtin_amdgcn_s_memtime();
+    u32 acc = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc ^= x[i] ^ (u32)y[i] ^ (u32)(y[i] >> 32);
+    out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+    if ((threadIdx.x & 63) == 0) {
+        u64* c = cnt + 2 * ((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+        c[0] = blocks;
+        c[1] = c1 - c0;
+    }
+}
+
+template <int K>
+static void run_steady(int wps, int ncu) {
+    const int per_wg = wps >= 8 ? 1024 : 256 * wps;
+    const int grid = wps >= 8 ? 2 * ncu : ncu;
+    const int threads = grid * per_wg, waves = threads / 64;
+    u32* out;
+    u64 *cnt, *t0;
+    CK(hipMalloc(&out, threads * 4));
+    CK(hipMalloc(&cnt, waves * 16));
+    CK(hipMalloc(&t0, 8));
+    const u64 lead = 200000, window = 500000;  // 2 ms to dispatch every wave, then a 5-ms window
+    for (int r = 0; r < 3; ++r) {  // the first runs warm the clock; the last is reported
+        hipLaunchKernelGGL(now_kernel, dim3(1), dim3(1), 0, 0, t0);
+        hipLaunchKernelGGL(valu_deadline_kernel<K>, dim3(grid), dim3(per_wg), 0, 0, out, cnt, t0, lead, window,
+                           0x08040201u, 0x80402010u);
+        CK(hipDeviceSynchronize());
+    }
+    std::vector<u64> c(2 * (size_t)waves);
+    CK(hipMemcpy(c.data(), cnt, waves * 16, hipMemcpyDeviceToHost));
+    double inst = 0, cyc = 0;
+    for (int w = 0; w < waves; ++w) {
+        inst += (double)c[2 * w] * 16 * 8 * INSTS[K];
+        cyc += (double)c[2 * w + 1];
+    }
+    const double ghz = cyc / waves / (window * 10.0);  // shader cycles per ns of the window
+    const double per_simd_cyc = inst / (4.0 * ncu) / (cyc / waves);
+    printf("steady %-24s waves/SIMD %d  SIMD issue %5.3f inst/cyc  clock %.2f GHz  chip %7.1f G inst/s\n", NAMES[K], wps,
+           per_simd_cyc, ghz, inst / (window * 1e-8) / 1e9);
+    CK(hipFree(out));
+    CK(hipFree(cnt));
+    CK(hipFree(t0));
+}
+
 template <int K>
 static void run(int wps, int ncu, int iters) {
     const int per_wg = wps >= 8 ? 1024 : 256 * wps;
@@ -165,6 +235,7 @@ static void run(int wps, int ncu, int iters) {
 template <int K>
 static void sweep(int ncu, int iters) {
     for (int w : {1, 2, 4, 8}) run<K>(w, ncu, iters);
+    for (int w : {1, 2, 4, 8}) run_steady<K>(w, ncu);
 }
 
 int main(int argc, char** argv) {

@@ -4,7 +4,7 @@ exotic_table), merge (export_rows / merge_rows) and classify (set_sheet / classi
 rc_counts) restated in Python over the oracle's rules, so the multi-rank host logic
 (frender_amd/dist.py, frender_amd/scan.py on key partitions) runs under gloo on CPU.  Keys follow
 include/frender_amd.h (fast 3-bit keys, wide base-5 keys, exotic codes by bytes); ordinals are
-(file index + 1) << 44 | byte offset of the record's header.  Record parts are cut by the library's
+(file index + 1) << 44 | byte offset of the record's header rounded down to a multiple of 4.  Record parts are cut by the library's
 own host cutter (fr_gz_part_bounds), so that code is what these tests run."""
 from __future__ import annotations
 
@@ -98,7 +98,7 @@ class FakeContext:
             key = fast_key(code)
             if key is None:
                 key = _lib.encode_wide(code)
-            ordv = tag | (self.base + s)
+            ordv = tag | ((self.base + s) & ~3)  # the library's ordinals: offsets rounded down to 4 B
             if key is None:
                 tab, key = self.exo, code.encode()
                 st.exotic += 1

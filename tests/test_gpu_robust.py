@@ -157,4 +157,4 @@ def test_range_over_4gib_rare_paths(lib):
     assert a[1] == 1 and a[2] == at[3] * reclen  # FR_SCAN_NO_SPACE at the patched header (past 4 GiB)
     assert a[3] == 1 and a[4] == 1
     assert a[8] == [hostrec[at[0]].split(b"\n")[0].split(b" ")[1].split(b":")[-1].decode()]
-    assert a[10] == [(1 << 44) | (at[0] * reclen)]  # the exotic record's ordinal: file tag 1, byte offset
+    assert a[10] == [(1 << 44) | (at[0] * reclen & ~3)]  # the exotic record's ordinal: file tag 1, byte offset (4-B floor)

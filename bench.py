@@ -59,6 +59,11 @@ def parse():
     ap.add_argument("--merge", choices=["a2a", "tree"], default="a2a",
                     help="N>1 table merge: hash-partitioned all-to-all (every rank merges and classifies its "
                          "partition) or a binary tree into rank 0")
+    ap.add_argument("--merge-leg", action="store_true",
+                    help="N=1 only, not the headline: a one-rank nccl (RCCL) process group, and every step also runs "
+                         "the N>1 merge leg on the full table (partition_merge_device's all-to-all and rebuild, then "
+                         "classify, then gather_rows of the rows to rank 0, as the product's writer does); reports "
+                         "merge_leg with the phases' ms per step")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, one GPU per rank); gloo only to rehearse N ranks on one GPU")
     ap.add_argument("--rank-check", action="store_true",
@@ -487,7 +492,18 @@ def main():
         return rank_check(world) if world > 1 else (print(json.dumps({"rank_check": True, "world": 1,
                                                                       "ranks_joined": 1})) or 0)
     dist = None
-    if world > 1:
+    if args.merge_leg and world == 1:  # a one-rank RCCL group: the merge leg's collectives on device tensors
+        import socket
+
+        import torch
+        import torch.distributed as dist
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            port = so.getsockname()[1]
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    elif world > 1:
         import torch
         import torch.distributed as dist
         if args.dist_backend == "gloo":  # rehearsal: every rank on this box's GPU(s)
@@ -499,7 +515,7 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from frender_amd import _lib, synth
-    from frender_amd.dist import device_callbacks, partition_merge_device, reduce_sum, tree_merge
+    from frender_amd.dist import device_callbacks, gather_rows, partition_merge_device, reduce_sum, tree_merge
     from frender_amd.host import reverse_complement
     from frender_amd.scan import _sheet_names
 
@@ -549,8 +565,10 @@ def main():
         if world > 1 and args.merge == "tree":  # one exchange: binary tree into rank 0 (dist.py)
             U = tree_merge(dist, "cuda", U, *merge_cbs)
             classify_here = rank == 0
-        elif world > 1:  # one exchange: all-to-all into hash partitions (dist.py)
+        elif world > 1 or args.merge_leg:  # one exchange: all-to-all into hash partitions (dist.py)
+            phase("tally")
             U = partition_merge_device(dist, "cuda", ctx)
+            phase("merge")
         if classify_here:
             ctx.set_sheet(sheet.idx1, sheet.idx2, idx2rc, nid, len(names))
             ctx.classify(args.nsubs, args.rc, to_host=False)
@@ -568,9 +586,25 @@ def main():
                     idx2b, idx2brc = sheet.idx2, idx2rc
                 ctx.set_sheet(sheet.idx1, idx2b, idx2brc, nid, len(names))
                 ctx.classify(args.nsubs, False, to_host=False)
+            if args.merge_leg:  # the product's writer: every partition's rows to rank 0
+                phase("classify")
+                gather_rows(dist, "cuda", ctx.export_rows("cuda"))
+                phase("gather")
         # (no stream sync here: fr_classify already waited for its error flags, and the timed loop is
         # bracketed by ctx.sync() + barrier on both sides)
         return U
+
+    phase_ms = {}  # --merge-leg: per-phase ms of the extra steps after the timed ones (synchronised at each phase)
+    phase_on = [False]
+    phase_t = [0.0]
+
+    def phase(name):
+        if not phase_on[0]:
+            return
+        ctx.sync()
+        now = time.perf_counter()
+        phase_ms.setdefault(name, []).append((now - phase_t[0]) * 1e3)
+        phase_t[0] = now
 
     def barrier():
         if world > 1:
@@ -594,6 +628,21 @@ def main():
     dt = time.perf_counter() - t0
     t_after = tally_timing[0]
     ms = dt / args.steps * 1e3
+    merge_leg = None
+    if args.merge_leg:  # three more steps, each phase synchronised and timed on the host
+        for _ in range(3):
+            ctx.sync()
+            phase_t[0] = time.perf_counter()
+            phase_on[0] = True
+            step()
+            phase_on[0] = False
+        ctx.sync()
+        med = {k: round(sorted(v)[len(v) // 2], 3) for k, v in phase_ms.items()}
+        merge_leg = {"rows": int(U), "row_bytes": 24, "world": 1, "backend": "nccl (RCCL), one rank",
+                     "ms_per_step_with_leg": round(ms, 4), "phase_ms": med,
+                     "note": "phases timed with a device sync at each boundary; 'tally' = reset, tally and finalize, 'merge' = export, all-to-all, "
+                             "rebuild and finalize of the partition (partition_merge_device), 'classify' = "
+                             "set_sheet + classify, 'gather' = export + gather_rows to rank 0 (host copy)"}
     if world > 1:
         import torch
         x = torch.tensor([ms], dtype=torch.float64, device="cpu" if args.dist_backend == "gloo" else "cuda")
@@ -654,6 +703,8 @@ def main():
             "cpu_baseline": cpu,
             "e2e": _E2E,
         }
+        if merge_leg:
+            out["merge_leg"] = merge_leg
         print(json.dumps(out), flush=True)
     ctx.device_free(buf)
     ctx.close()

@@ -2250,38 +2250,46 @@ __global__ __launch_bounds__(RED_WG) void log_reduce_kernel(Table t, DevState* s
     u64 sink = 0;
     constexpr int LB = 8;  // entries per thread per batch; the next batch's loads fly during this one's fold
     const u32 nn = (ABLATE & 512u) ? 0u : n;  // 512: timing ablation
+    // unconditional loads (a clamped index, the key zeroed past the end): exec-masked loads made the compiler wait
+    // for every outstanding load (vmcnt(0)) right after issuing the next batch, so no batch flew during a fold
     LogEntry nx[LB];
+    if (nn) {
 #pragma unroll
-    for (int q = 0; q < LB; ++q) nx[q] = threadIdx.x + q * RED_WG < nn ? part[threadIdx.x + q * RED_WG] : LogEntry{0, 0};
+        for (int q = 0; q < LB; ++q) nx[q] = part[min(threadIdx.x + q * RED_WG, nn - 1u)];
+    }
     for (u32 i0 = threadIdx.x; i0 < nn; i0 += LB * RED_WG) {
         LogEntry ev[LB];
 #pragma unroll
         for (int q = 0; q < LB; ++q) {
             ev[q] = nx[q];
-            const u32 j = i0 + LB * RED_WG + q * RED_WG;
-            nx[q] = j < nn ? part[j] : LogEntry{0, 0};
+            nx[q] = part[min(i0 + (LB + q) * RED_WG, nn - 1u)];  // (past the end: the last entry again, skipped)
         }
 #pragma unroll
         for (int q = 0; q < LB; ++q) {
             const LogEntry e = ev[q];
-            if (!e.key) continue;
+            if (i0 + q * RED_WG >= nn || !e.key) continue;
             if (ABLATE & 1024u) {  // timing ablation: loads only
                 sink ^= e.key;
                 continue;
             }
             const u32 eoff = (u32)((((ord0 & ((1ull << ORD_SHIFT) - 1ull)) + log_off(e.oc)) >> 2) - base4);
             const u32 ecnt = log_cnt(e.oc);
-            u32 h = (u32)mix64(e.key) & (AGG_LNS - 1);
+            // the fold's slot: two 32-bit multiplies (a sub-region's keys share mix64's top bits, not these)
+            u32 h = (u32)e.key * 0x9E3779B1u ^ (u32)(e.key >> 32) * 0x85EBCA6Bu;
+            h = (h ^ (h >> 15)) & (AGG_LNS - 1);
             bool done = false;
             for (int pr = 0; pr < AGG_PROBE && !done; ++pr) {
-                u64 k = ls[h].key;
+                const AggSlot sl = ls[h];  // key, first and count in one LDS read
+                u64 k = sl.key;
+                u32 mino = sl.mino;
                 if (k == 0) {
                     const u64 old = atomicCAS((unsigned long long*)&ls[h].key, 0ull, (unsigned long long)e.key);
                     k = old == 0 ? e.key : old;
+                    mino = old == 0 ? 0xFFFFFFFFu : ls[h].mino;
                 }
                 if (k == e.key) {
                     atomicAdd(&ls[h].cnt, ecnt);  // (fire-and-forget LDS atomics: no wait in the fold's chain)
-                    if (eoff < ls[h].mino) atomicMin(&ls[h].mino, eoff);
+                    if (eoff < mino) atomicMin(&ls[h].mino, eoff);
                     done = true;
                     break;
                 }

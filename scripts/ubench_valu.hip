@@ -30,10 +30,14 @@ typedef uint64_t u64;
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
 
-enum { K_AND, K_PERM, K_DOT4, K_DPP, K_FFBL, K_SHR64, K_ALIGN, K_MIX, K_N };
+enum { K_AND, K_PERM, K_DOT4, K_DPP, K_FFBL, K_SHR64, K_ALIGN, K_MIX, K_BITOP3, K_OR3, K_LSHLOR, K_LSHR, K_CND, K_ADD,
+       K_BCNT, K_MIN, K_MULLO, K_MUL24, K_ADD64, K_ALIGNB, K_N };
 static const char* NAMES[K_N] = {"v_and_b32", "v_perm_b32", "v_dot4_u32_u8", "v_add_u32 dpp row_shr", "v_ffbl_b32",
-                                  "v_lshrrev_b64", "v_alignbit_b32", "classify mix (11 VALU)"};
-static const int INSTS[K_N] = {1, 1, 1, 1, 1, 1, 1, 11};  // VALU instructions per chain step
+                                  "v_lshrrev_b64", "v_alignbit_b32", "classify mix (11 VALU)", "v_bitop3_b32",
+                                  "v_or3_b32", "v_lshl_or_b32", "v_lshrrev_b32", "v_cndmask_b32", "v_add_u32",
+                                  "v_bcnt_u32_b32", "v_min_u32", "v_mul_lo_u32", "v_mul_u32_u24", "v_lshl_add_u64",
+                                  "v_alignbyte_b32"};
+static const int INSTS[K_N] = {1, 1, 1, 1, 1, 1, 1, 11, 1, 1, 1, 1, 2, 1, 1, 1, 1, 1, 1, 1};  // VALU instructions per chain step
 
 template <int K>
 __device__ __forceinline__ void step(u32 (&x)[8], u64 (&y)[8], u32 a, u32 b) {
@@ -53,6 +57,30 @@ __device__ __forceinline__ void step(u32 (&x)[8], u64 (&y)[8], u32 a, u32 b) {
             asm volatile("v_lshrrev_b64 %0, 1, %0" : "+v"(y[i]));
         } else if constexpr (K == K_ALIGN) {
             asm volatile("v_alignbit_b32 %0, %0, %1, 7" : "+v"(x[i]) : "v"(a));
+        } else if constexpr (K == K_BITOP3) {
+            asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(x[i]) : "v"(a), "v"(b));
+        } else if constexpr (K == K_OR3) {
+            asm volatile("v_or3_b32 %0, %0, %1, %2" : "+v"(x[i]) : "v"(a), "v"(b));
+        } else if constexpr (K == K_LSHLOR) {
+            asm volatile("v_lshl_or_b32 %0, %0, 3, %1" : "+v"(x[i]) : "v"(a));
+        } else if constexpr (K == K_LSHR) {
+            asm volatile("v_lshrrev_b32 %0, 3, %0" : "+v"(x[i]));
+        } else if constexpr (K == K_CND) {
+            asm volatile("v_cmp_gt_u32 vcc, %1, %0\n\tv_cndmask_b32 %0, %0, %1, vcc" : "+v"(x[i]) : "v"(a) : "vcc");
+        } else if constexpr (K == K_ADD) {
+            asm volatile("v_add_u32 %0, %0, %1" : "+v"(x[i]) : "v"(a));
+        } else if constexpr (K == K_BCNT) {
+            asm volatile("v_bcnt_u32_b32 %0, %0, %1" : "+v"(x[i]) : "v"(a));
+        } else if constexpr (K == K_MIN) {
+            asm volatile("v_min_u32 %0, %0, %1" : "+v"(x[i]) : "v"(a));
+        } else if constexpr (K == K_MULLO) {
+            asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(x[i]) : "v"(a));
+        } else if constexpr (K == K_MUL24) {
+            asm volatile("v_mul_u32_u24 %0, %0, %1" : "+v"(x[i]) : "v"(a));
+        } else if constexpr (K == K_ADD64) {
+            asm volatile("v_lshl_add_u64 %0, %0, 0, -1" : "+v"(y[i]));
+        } else if constexpr (K == K_ALIGNB) {
+            asm volatile("v_alignbyte_b32 %0, %0, %1, 3" : "+v"(x[i]) : "v"(a));
         } else {  // the classify of one dword: masks, three 8-entry lookups, two ANDs, three gathers
             u32 m0, m1, m2, l0, l1, l2;
             asm volatile(
@@ -238,8 +266,21 @@ static void sweep(int ncu, int iters) {
     for (int w : {1, 2, 4, 8}) run_steady<K>(w, ncu);
 }
 
+template <int K>
+static void quick(int ncu) { run_steady<K>(8, ncu); }
+
 int main(int argc, char** argv) {
     const int iters = argc > 1 ? atoi(argv[1]) : 20000;
+    if (argc > 2 && argv[2][0] == 'q') {  // steady state at 8 waves/SIMD only, every kind
+        hipDeviceProp_t p;
+        CK(hipGetDeviceProperties(&p, 0));
+        const int ncu = p.multiProcessorCount;
+        quick<K_AND>(ncu); quick<K_PERM>(ncu); quick<K_DOT4>(ncu); quick<K_DPP>(ncu); quick<K_FFBL>(ncu);
+        quick<K_SHR64>(ncu); quick<K_ALIGN>(ncu); quick<K_MIX>(ncu); quick<K_BITOP3>(ncu); quick<K_OR3>(ncu);
+        quick<K_LSHLOR>(ncu); quick<K_LSHR>(ncu); quick<K_CND>(ncu); quick<K_ADD>(ncu); quick<K_BCNT>(ncu);
+        quick<K_MIN>(ncu); quick<K_MULLO>(ncu); quick<K_MUL24>(ncu); quick<K_ADD64>(ncu); quick<K_ALIGNB>(ncu);
+        return 0;
+    }
     hipDeviceProp_t p;
     CK(hipGetDeviceProperties(&p, 0));
     printf("%s: %d CUs, clock %d kHz; s_memtime counts shader cycles\n", p.gcnArchName, p.multiProcessorCount,

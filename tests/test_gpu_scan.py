@@ -657,7 +657,9 @@ def test_scan_then_demux_96_samples(tmp_path, monkeypatch):
                                   "demux_ok_samples", "same_file_twice", "wide_codes_12", "no_space_header",
                                   # one file: every rank tallies a record-aligned part of it
                                   "comb96_n1_rc", "cfg1_10k_s4_n0", "cr_only", "mixed_newlines", "multi_member_gz",
-                                  "bad_utf8", "gz_truncated", "s96_r150_n1"])
+                                  "bad_utf8", "gz_truncated", "s96_r150_n1",
+                                  # the config-3 shape (384 samples, 10+10, -rc) and n=2 sharded over two ranks
+                                  "s384_l10_n1_rc_dup", "s96_n2"])
 def test_cli_two_ranks_match_golden(name, tmp_path):
     """`python -m frender_amd scan --gpus 2` (files sharded over two ranks, or one file's record-aligned
     parts, tables key-partitioned over the ranks) writes the reference's CSV bytes and per-file lines

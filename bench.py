@@ -82,7 +82,7 @@ def parse():
     ap.add_argument("--tuning", default="",
                     help="A/B runs only: fr_tuning fields for the bench's context, e.g. 'log_min=0,chunk_tiles=400' "
                          "(results never change; a tuned run reports them in config.tuning)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r05.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r06.json"),
                     help="per-launch HBM bytes of the tally kernel from rocprofv3 PMC (scripts/make_traffic.py); "
                          "used only when taken on this source tree and this launch shape, else traffic is null")
     return ap.parse_args()
@@ -142,26 +142,37 @@ def load_traffic(path, tree, per_launch_bytes, samples, index_len, combinatorial
                                             f"{tj.get('traffic_over_algorithmic')}x algorithmic"), tj.get("valu")
 
 
-# The chip's wave64 VALU issue ceiling, measured (scripts/ubench_valu.hip, profiles/r04c_ubench_valu.txt: wall-clock
-# chip rate, in-kernel clock 2.35-2.39 GHz by s_memtime/s_memrealtime): independent v_and_b32 chains top out at
-# 640-647 G inst/s at 2, 4 and 8 waves per SIMD, one wave64 instruction per SIMD every ~3.7 cycles.  The guide's
-# "2 cycles per wave64 instruction" (MI355X_MICROARCH.md:54, 1229 G/s) is the SIMD-32's two passes, not an issue
-# rate this chip sustains for these instructions.
-VALU_PEAK_G = 646.9   # v_and_b32, 4 waves/SIMD (the kernel's occupancy)
-VALU_MIX_G = 626.9    # the tally's classify mix (v_perm, v_dot4, masks), 4 waves/SIMD
+# The chip's wave64 VALU issue rates, measured in steady state (round 6: scripts/ubench_valu.hip's deadline mode --
+# every wave runs until a common s_memrealtime deadline and only instructions inside the window count, so the
+# launch ramp and tail are outside; profiles/r06_ubench_valu.txt).  At 4 waves/SIMD (the tally's occupancy) and
+# 2.35-2.38 GHz: VOP2-class v_and / v_add / v_lshrrev 0.42-0.49 inst/cycle/SIMD (~2 cycles each), v_bitop3 and
+# v_cndmask ~3 cycles, and v_perm, v_dot4, DPP, v_ffbl, 64-bit shifts and adds, v_alignbit/byte, v_or3, v_lshl_or,
+# v_bcnt, v_min and the multiplies 0.246-0.248 (4 cycles each: 600 G/s chip-wide); the tally's classify mix 0.275.
+# (The round-4 figure of 647 G/s for v_and was a wall-clock rate over a launch whose waves overlapped 2.5 of 4.)
+# The bound the kernel meets is the SIMDs' VALU-busy share: SQ_ACTIVE_INST_VALU (quad-cycles, summed over waves)
+# over the SIMD quad-cycles of the launch.
+VALU_PEAK_G = 600.0   # 4-cycle class (v_perm, v_dot4, ... : most of the tally's VALU), 4 waves/SIMD, steady state
+VALU_MIX_G = 666.2    # the tally's classify mix (v_perm, v_dot4, masks), 4 waves/SIMD, steady state
+SIMD_CLOCK_GHZ = 2.35  # in-kernel shader clock under load (s_memtime / s_memrealtime, profiles/r06_ubench_valu.txt)
+NUM_SIMDS = 1024
 
 
 def valu_roofline(valu, per_launch_ms):
     """The kernel's second bound: VALU issue.  SQ_INSTS_VALU per launch (the same PMC file, same tree)
-    over this run's measured launch time, against the measured chip issue ceiling (647 G/s) and the
-    measured ceiling of the kernel's own instruction mix at its occupancy (627 G/s at 4 waves per SIMD,
-    scripts/ubench_valu.hip).  None without a VALU pass for this tree."""
+    over this run's measured launch time against the 4-cycle class's steady-state rate (600 G/s) and the
+    classify mix's (666 G/s); simd_valu_busy = SQ_ACTIVE_INST_VALU quad-cycles over the launch's SIMD
+    quad-cycles.  None without a VALU pass for this tree."""
     if not valu or not valu.get("insts_per_launch") or per_launch_ms <= 0:
         return None
     g = valu["insts_per_launch"] / (per_launch_ms / 1e3) / 1e9
+    busy = None
+    if valu.get("active_quad_cycles_per_launch"):  # the SIMDs' VALU-busy share of the launch
+        busy = round(4.0 * valu["active_quad_cycles_per_launch"] /
+                     (NUM_SIMDS * per_launch_ms * 1e-3 * SIMD_CLOCK_GHZ * 1e9), 4)
     return {"achieved": round(g, 1), "peak": VALU_PEAK_G, "unit": "G wave64 VALU inst/s",
             "frac": round(g / VALU_PEAK_G, 4), "mix_ceiling_4waves": VALU_MIX_G,
-            "frac_of_mix_ceiling": round(g / VALU_MIX_G, 4), "insts_per_record": valu.get("insts_per_record")}
+            "frac_of_mix_ceiling": round(g / VALU_MIX_G, 4), "insts_per_record": valu.get("insts_per_record"),
+            "simd_valu_busy": busy}
 
 
 def _gz(chunk: bytes) -> bytes:

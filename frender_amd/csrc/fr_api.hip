@@ -1114,7 +1114,8 @@ int fr_feed_device(fr_ctx* ctx, const uint8_t* dev_data, uint64_t len) {
     // bytes: config 2's 3.7-GB halves fill at most 1 626 of 4 096 slots, projected 3 252 for 7.4 GB; config 3's 3.9-GB
     // halves 2 424 (projected 4 848), scripts/fold_probe.py)
     const double big_range = (double)std::min<u64>(ctx->chunk_bytes, len);
-    const bool fold_room = ctx->feed_fold_over == 0 && ctx->feed_step > 0 &&
+    const bool fold_room = (u64)ctx->feed_fold_over * 64 <= ctx->feed_fold_max && ctx->feed_step > 0 &&  // (a few
+                           // entries past a fold's probe bound insert on their own: harmless)
                            (double)ctx->feed_fold_max * big_range <= 0.85 * AGG_LNS * (double)ctx->feed_step;
     bool big = spec && (!ctx->feed_logged || fold_room) && ctx->feed_keys != ~0ull &&
                (saved.n_keys + ctx->feed_keys) * 2 <= ctx->nslots;

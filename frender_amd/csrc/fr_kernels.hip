@@ -1997,7 +1997,7 @@ __device__ __forceinline__ bool last_block(u32* ctr) {
     return last != 0;
 }
 
-constexpr int AGG_PROBE = 64;
+constexpr int AGG_PROBE = 256;  // (64 let ~20 of a 7.4-GB launch's 11M entries overflow a fold at load 0.69)
 constexpr int CLAIM_WORDS = 1024;  // a reduce workgroup's claim bitmap: sub-regions of up to 32K slots (4 KB; tables of up to 16 Mi slots)
 struct alignas(16) AggSlot {
     u64 key;
@@ -2274,8 +2274,11 @@ __global__ __launch_bounds__(RED_WG) void log_reduce_kernel(Table t, DevState* s
             }
             const u32 eoff = (u32)((((ord0 & ((1ull << ORD_SHIFT) - 1ull)) + log_off(e.oc)) >> 2) - base4);
             const u32 ecnt = log_cnt(e.oc);
-            // the fold's slot: two 32-bit multiplies (a sub-region's keys share mix64's top bits, not these)
+            // the fold's slot and probe step (double hashing: a wave waits for its lanes' longest probe chain,
+            // and linear probing's clusters at the fold's ~0.7 load made that chain long); two 32-bit
+            // multiplies (a sub-region's keys share mix64's top bits, not these)
             u32 h = (u32)e.key * 0x9E3779B1u ^ (u32)(e.key >> 32) * 0x85EBCA6Bu;
+            const u32 hstep = ((h >> 7) & (AGG_LNS - 1)) | 1u;
             h = (h ^ (h >> 15)) & (AGG_LNS - 1);
             bool done = false;
             for (int pr = 0; pr < AGG_PROBE && !done; ++pr) {
@@ -2293,7 +2296,7 @@ __global__ __launch_bounds__(RED_WG) void log_reduce_kernel(Table t, DevState* s
                     done = true;
                     break;
                 }
-                h = (h + 1) & (AGG_LNS - 1);
+                h = (h + hstep) & (AGG_LNS - 1);
             }
             if (!done) {  // a full LDS table: this row goes in on its own
                 const u64 key1[1] = {e.key};

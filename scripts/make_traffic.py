@@ -23,7 +23,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNEL = "fr::chunk_kernel"
-VALU_PEAK_G = 646.9  # measured chip issue ceiling (profiles/r04c_ubench_valu.txt: v_and_b32, 4 waves/SIMD, wall clock)
+VALU_PEAK_G = 600.0  # 4-cycle VALU class at 4 waves/SIMD, steady state (profiles/r06_ubench_valu.txt, scripts/ubench_valu.hip)
 
 
 def rows(pattern):
@@ -86,10 +86,10 @@ def main():
         valu_d = {"insts_per_launch": int(vi), "insts_per_record": round(vi / (reads / launches), 3),
                   "active_quad_cycles_per_launch": int(sum(vact.values()) / len(vact)) if vact else None,
                   "peak_g_insts_per_s": VALU_PEAK_G,
-                  "peak_note": "measured chip issue ceiling: independent v_and_b32 chains at 4 waves/SIMD, wall clock, "
-                                "in-kernel clock 2.37 GHz (profiles/r04c_ubench_valu.txt, scripts/ubench_valu.hip); the "
-                                "guide's 2-cycle figure (1229 G/s) is not sustained",
-                  "mix_ceiling_g_insts_per_s": 626.9}
+                  "peak_note": "steady state (deadline mode) at 4 waves/SIMD, 2.35-2.38 GHz: v_perm, v_dot4, DPP, v_ffbl, "
+                                "64-bit shifts, v_alignbit, v_or3, v_lshl_or, v_bcnt, v_min issue every 4 cycles "
+                                "(600 G/s); v_and, v_add, v_lshrrev every ~2 (profiles/r06_ubench_valu.txt)",
+                  "mix_ceiling_g_insts_per_s": 666.2}
     # A lower reading of the same counters: the table probes beyond the stream (random 32-B slot reads)
     # are one 64-B FETCH unit each (profiles/r04h_table_pmc/summary.json); x2 assumes each is a 128-B
     # line tallied at 64 B like the streaming loads, x1 that it is a 64-B fill.  Needs the stream-only pass.
@@ -106,7 +106,7 @@ def main():
             for r in rows(src + "/prof_trace/**/*kernel_trace.csv") if KERNEL in r["Kernel_Name"]]
     full = [d for d in durs if durs and d >= 0.7 * max(durs)]
     out = {
-        "round": int(os.environ.get("ROUND", "5")),
+        "round": int(os.environ.get("ROUND", "6")),
         "rocprof_full_launch_ms": round(sum(full) / len(full), 4) if full else None,
         "rocprof_full_launches": len(full),
         "tree_hash": source_tree_hash(),
@@ -131,7 +131,7 @@ def main():
         "source": f"profiles/{tag}_pmc_chunk_kernel.csv (rocprofv3 --pmc FETCH_SIZE, then --pmc WRITE_SIZE, "
                   f"separate runs of bench.py {os.environ.get('PROF_ARGS', '--steps 5 --warmup 1 --no-cpu')})",
     }
-    with open(os.path.join(prof, os.environ.get("TRAFFIC_JSON", "traffic_r05.json")), "w") as fh:
+    with open(os.path.join(prof, os.environ.get("TRAFFIC_JSON", "traffic_r06.json")), "w") as fh:
         json.dump(out, fh, indent=1)
     print(json.dumps(out, indent=1))
 

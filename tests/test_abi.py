@@ -75,5 +75,9 @@ def test_bench_refuses_traffic_of_another_tree(tmp_path):
     g = 6.82e8 / 1.45e-3 / 1e9
     assert r["unit"] == "G wave64 VALU inst/s" and abs(r["frac"] - g / bench.VALU_PEAK_G) < 1e-3
     assert abs(r["frac_of_mix_ceiling"] - g / bench.VALU_MIX_G) < 1e-3
+    assert r["simd_valu_busy"] is None  # no active-cycle counter in this record
+    r2 = bench.valu_roofline(dict(valu, active_quad_cycles_per_launch=250_000_000), 1.45)
+    busy = 4 * 2.5e8 / (bench.NUM_SIMDS * 1.45e-3 * bench.SIMD_CLOCK_GHZ * 1e9)  # VALU share of the SIMD cycles
+    assert abs(r2["simd_valu_busy"] - busy) < 1e-3
     assert bench.valu_roofline(None, 1.45) is None
     assert bench.load_traffic(str(tmp_path / "absent.json"), tree, 3.7e9, 96, 8, False)[0] is None

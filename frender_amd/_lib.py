@@ -112,6 +112,8 @@ _SIGS = {
     "fr_classify_cp": (C.c_int, [P, C.c_int, P, P, P, P, C.c_int, C.c_int, C.c_int, P, P, P, P, P, P, P, P]),
     "fr_export_unique_device": (C.c_int, [P, P, P, P, C.c_uint64]),
     "fr_merge_unique_device": (C.c_int, [P, P, P, P, C.c_uint64]),
+    "fr_export_partitioned_device": (C.c_int, [P, C.c_int, P, P, C.c_uint64]),
+    "fr_merge_rows_device": (C.c_int, [P, P, C.c_uint64]),
     "fr_device_alloc": (P, [P, C.c_uint64]),
     "fr_device_free": (C.c_int, [P, P]),
     "fr_copy_to_host": (C.c_int, [P, P, P, C.c_uint64]),
@@ -872,6 +874,30 @@ class Context:
     def merge_unique_device(self, keys_ptr: int, counts_ptr: int, first_ptr: int, n: int):
         self._ck(lib.fr_merge_unique_device(self.h, P(keys_ptr), P(counts_ptr), P(first_ptr), n),
                  "fr_merge_unique_device")
+
+    def export_partitioned(self, world: int):
+        """The finalized rows as an int64 tensor [U, 3] on this GPU, partitioned by owner rank (blocks of
+        owners 0..world-1 in order; fr_export_partitioned_device), and the rows per owner (int64 [world], same
+        device).  Same stream contract as export_unique_device."""
+        U = int(self.U)
+        dev = torch.device("cuda", self.device)
+        rows = torch.empty((max(U, 1), 3), dtype=torch.int64, device=dev)
+        cnt = torch.empty(2 * world, dtype=torch.int64, device=dev)
+        _torch_stream_done(self.device)
+        self._ck(lib.fr_export_partitioned_device(self.h, int(world), P(rows.data_ptr()), P(cnt.data_ptr()),
+                                                  max(U, 1)), "fr_export_partitioned_device")
+        return rows[:U], cnt[:world]
+
+    def merge_rows_rowmajor(self, rows):
+        """Merge (key, count, first) rows [n, 3] (int64, on this GPU, row-major) into the table
+        (fr_merge_rows_device); torch's stream is drained first (the rows may come from an RCCL receive)."""
+        n = int(rows.shape[0])
+        if not n:
+            return
+        rows = rows.contiguous()
+        torch.cuda.current_stream(rows.device).synchronize()
+        self._ck(lib.fr_merge_rows_device(self.h, P(rows.data_ptr()), n), "fr_merge_rows_device")
+        self.sync()  # rows goes back to torch's allocator after this
 
     # ---- tensor views for the multi-GPU merge (frender_amd/dist.py) ----------------------
     def export_rows(self, device):

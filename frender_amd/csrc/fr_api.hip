@@ -1681,6 +1681,33 @@ int fr_export_unique_device(fr_ctx* ctx, void* dev_keys, void* dev_counts, void*
     return FR_OK;
 }
 
+int fr_export_partitioned_device(fr_ctx* ctx, int world, void* dev_rows, void* dev_counts, uint64_t cap) {
+    if (int src = settle_finalize(ctx)) return src;
+    if (world < 1 || world > 1024) return fail(ctx, FR_ERR_INVALID, "fr_export_partitioned_device: world out of range");
+    if (ctx->U > cap) return fail(ctx, FR_ERR_CAPACITY, "export buffer too small");
+    CK(launch_partition_rows(ctx->d_keys_s, ctx->d_counts_s, ctx->d_first_s, ctx->U, (u32)world, (u64*)dev_counts,
+                             (u64*)dev_counts + world, (u64*)dev_rows, ctx->stream));
+    CK(hipStreamSynchronize(ctx->stream));
+    return FR_OK;
+}
+
+int fr_merge_rows_device(fr_ctx* ctx, const void* dev_rows, uint64_t n) {
+    if (int src = settle_finalize(ctx)) return src;
+    if (ctx->file_open) return fail(ctx, FR_ERR_INVALID, "fr_merge_rows_device: a file is open");
+    int rc = flush_presence(ctx);
+    if (rc) return rc;
+    ctx->merged = true;
+    rc = read_state(ctx);
+    if (rc) return rc;
+    if ((ctx->h_st->n_keys + n) * 2 > ctx->nslots) {
+        rc = grow_table(ctx, true);
+        if (rc) return rc;
+    }
+    ctx->st_fresh = false;
+    CK(launch_merge_rows(ctx->tab, ctx->st, (const u64*)dev_rows, n, ctx->stream));
+    return grow_table(ctx, false);
+}
+
 int fr_merge_unique_device(fr_ctx* ctx, const void* dev_keys, const void* dev_counts, const void* dev_first,
                            uint64_t n) {
     if (int src = settle_finalize(ctx)) return src;

@@ -334,6 +334,11 @@ hipError_t launch_presence_scan(const GSlot* slots, u64 n, u32 tag, Presence* pr
                                 hipStream_t s);
 hipError_t launch_merge(Table t, DevState* st, const u64* keys, const u64* counts, const u64* first, u64 n,
                         hipStream_t s);
+// the multi-GPU merge's rows by owner rank (counts: world counters then world cursors, adjacent) and the
+// row-major merge of received rows
+hipError_t launch_partition_rows(const u64* keys, const u64* counts_in, const u64* first, u64 n, u32 world,
+                                 u64* counts, u64* cursor, u64* rows, hipStream_t s);
+hipError_t launch_merge_rows(Table t, DevState* st, const u64* rows, u64 n, hipStream_t s);
 // aggregate the launch log into the table and empty it (stream-ordered; reads log_n and the region
 // cursors on the device)
 hipError_t launch_log_aggregate(Table t, DevState* st, const LogEntry* log, u32 rcap, LogEntry* sub, u32 scap,

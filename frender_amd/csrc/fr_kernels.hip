@@ -2627,6 +2627,76 @@ __global__ void merge_kernel(Table t, DevState* st, const u64* keys, const u64* 
     add_created(st, made);
 }
 
+// the multi-GPU merge's send side: the finalized rows (key, count, first) partitioned by owner rank
+// (owner = the top 24 bits of key * 0x9E3779B97F4A7C15 mod world, frender_amd/dist.py owner_of), row-major,
+// owner blocks contiguous.  Pass 1 counts per owner (an LDS histogram per workgroup, one atomic per
+// (workgroup, owner)); pass 2 gives each workgroup's rows of an owner a run claimed from that owner's cursor
+// (cursors start at the owners' exclusive prefix).  Order inside a block is not fixed: the merge is commutative.
+constexpr int PART_MAX = 1024;  // ranks
+__device__ __forceinline__ u32 owner_rank(u64 key, u32 world) {
+    return (u32)(((key * 0x9E3779B97F4A7C15ull) >> 40) & 0xFFFFFFull) % world;
+}
+__global__ __launch_bounds__(256) void part_count_kernel(const u64* keys, u64 n, u32 world, u64* counts) {
+    __shared__ u32 h[PART_MAX];
+    for (u32 i = threadIdx.x; i < world; i += 256) h[i] = 0;
+    __syncthreads();
+    for (u64 i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (u64)gridDim.x * 256ull) atomicAdd(&h[owner_rank(keys[i], world)], 1u);
+    __syncthreads();
+    for (u32 i = threadIdx.x; i < world; i += 256)
+        if (h[i]) atomicAdd((unsigned long long*)&counts[i], (unsigned long long)h[i]);
+}
+__global__ __launch_bounds__(256) void part_scatter_kernel(const u64* keys, const u64* counts_in, const u64* first,
+                                                          u64 n, u32 world, const u64* counts, u64* cursor, u64* rows) {
+    __shared__ u32 h[PART_MAX];
+    __shared__ u64 base[PART_MAX];
+    for (u32 i = threadIdx.x; i < world; i += 256) h[i] = 0;
+    __syncthreads();
+    const u64 stride = (u64)gridDim.x * 256ull;
+    for (u64 i = blockIdx.x * 256ull + threadIdx.x; i < n; i += stride) atomicAdd(&h[owner_rank(keys[i], world)], 1u);
+    __syncthreads();
+    if (threadIdx.x == 0) {  // cursors start at the exclusive prefix of the counts (the first claim of each sets it)
+        u64 pre = 0;
+        for (u32 r = 0; r < world; ++r) {
+            base[r] = h[r] ? pre + atomicAdd((unsigned long long*)&cursor[r], (unsigned long long)h[r]) : 0ull;
+            pre += counts[r];
+            h[r] = 0;
+        }
+    }
+    __syncthreads();
+    for (u64 i = blockIdx.x * 256ull + threadIdx.x; i < n; i += stride) {
+        const u64 k = keys[i];
+        const u32 r = owner_rank(k, world);
+        const u64 at = base[r] + atomicAdd(&h[r], 1u);
+        rows[3 * at] = k;
+        rows[3 * at + 1] = counts_in[i];
+        rows[3 * at + 2] = first[i];
+    }
+}
+// merge rows (key, count, first), row-major, into the table (count +, first min)
+__global__ void merge_rows_kernel(Table t, DevState* st, const u64* rows, u64 n) {
+    u32 made = 0;
+    for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x)
+        made += global_insert(t, st, rows[3 * i], rows[3 * i + 1], rows[3 * i + 2], 0u) ? 1u : 0u;
+    add_created(st, made);
+}
+hipError_t launch_partition_rows(const u64* keys, const u64* counts_in, const u64* first, u64 n, u32 world,
+                                 u64* counts, u64* cursor, u64* rows, hipStream_t s) {
+    if (world < 1 || world > (u32)PART_MAX) return hipErrorInvalidValue;
+    hipError_t e = hipMemsetAsync(counts, 0, 2ull * world * sizeof(u64), s);  // counts and cursors (adjacent)
+    if (e != hipSuccess || !n) return e;
+    const int grid = (int)std::min<u64>((n + 255) / 256, 2048);
+    hipLaunchKernelGGL(part_count_kernel, dim3(grid), dim3(256), 0, s, keys, n, world, counts);
+    hipLaunchKernelGGL(part_scatter_kernel, dim3(grid), dim3(256), 0, s, keys, counts_in, first, n, world, counts,
+                       cursor, rows);
+    return hipGetLastError();
+}
+hipError_t launch_merge_rows(Table t, DevState* st, const u64* rows, u64 n, hipStream_t s) {
+    if (!n) return hipSuccess;
+    const int grid = (int)std::min<u64>((n + 255) / 256, 8192);
+    hipLaunchKernelGGL(merge_rows_kernel, dim3(grid), dim3(256), 0, s, t, st, rows, n);
+    return hipGetLastError();
+}
+
 // per-file presence (R10) and the per-file distinct-code count (frender.py:175): after a
 // file, exactly the slots whose last_tag is that file's tag hold a code seen in it.  Each pair keeps
 // the code's running count (its per-file count is the difference to the code's previous pair).  A workgroup

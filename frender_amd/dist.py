@@ -157,6 +157,23 @@ def exchange(dist, wire, rows, dest):
     return recv
 
 
+def exchange_partitioned(dist, wire, send, scount):
+    """All-to-all of int64 rows [n, k] already in owner blocks (ranks 0..world-1 in order, scount[r] rows for
+    rank r: the library's partitioned export).  Returns the received rows [m, k], by source rank."""
+    import torch
+
+    t0 = time.perf_counter()
+    k = int(send.shape[1]) if send.dim() == 2 else 3
+    scount = scount.to(wire).to(torch.int64)
+    rcount = torch.empty_like(scount)
+    dist.all_to_all_single(rcount, scount)
+    sc, rc = scount.tolist(), rcount.tolist()
+    recv = torch.empty((sum(rc), k), dtype=torch.int64, device=wire)
+    dist.all_to_all_single(recv.view(-1), send.contiguous().view(-1), [k * c for c in rc], [k * c for c in sc])
+    _census("exchange", t0, 8 * k * sum(sc))
+    return recv
+
+
 def _reduce(dist, wire, values, op):
     import torch
 
@@ -232,6 +249,14 @@ def partition_merge_device(dist, device, ctx):
     import torch
 
     wire = "cpu" if dist.get_backend() == "gloo" else device
+    if wire != "cpu":  # RCCL: rows partitioned by owner on the device (one library call), merged row-major
+        rows, scount = ctx.export_partitioned(dist.get_world_size())
+        mine = exchange_partitioned(dist, rows.device, rows, scount)
+        ctx.reset()
+        ctx.merge_rows_rowmajor(mine)
+        n, _, _ = ctx.finalize()
+        ctx.sync()
+        return int(n)
     rows = ctx.export_rows(wire)
     mine = exchange(dist, wire, rows, owner_of(rows[:, 0], dist.get_world_size()) if rows.shape[0]
                     else torch.zeros(0, dtype=torch.int64, device=rows.device))

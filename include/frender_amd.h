@@ -291,6 +291,14 @@ int fr_classify_cp(fr_ctx* ctx, int n, const uint32_t* q1, const int32_t* q1len,
 
 /* ---- multi-GPU merge: export / import the compacted table ----------- */
 int fr_export_unique_device(fr_ctx* ctx, void* dev_keys, void* dev_counts, void* dev_first, uint64_t cap);
+/* The same rows as one int64 array [U][3] of (key, count, first), partitioned by owner rank: owner = the top 24
+ * bits of key * 0x9E3779B97F4A7C15 (mod 2^64) mod world (frender_amd/dist.py owner_of), the blocks of owners
+ * 0..world-1 contiguous in that order (order inside a block not fixed); dev_counts receives 2 x world int64:
+ * the rows per owner, then scratch.  Synchronises the library's stream.  1 <= world <= 1024. */
+int fr_export_partitioned_device(fr_ctx* ctx, int world, void* dev_rows, void* dev_counts, uint64_t cap);
+/* Merge n int64 rows [n][3] (key, count, first) from device memory into the table (count = sum, first = min);
+ * the row-major form of fr_merge_unique_device (the rows an all-to-all delivered). */
+int fr_merge_rows_device(fr_ctx* ctx, const void* dev_rows, uint64_t n);
 int fr_merge_unique_device(fr_ctx* ctx, const void* dev_keys, const void* dev_counts, const void* dev_first,
                            uint64_t n);
 

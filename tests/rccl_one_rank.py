@@ -71,6 +71,15 @@ def main():
     assert D.reduce_min(dist, wire, v).tolist() == v
     blobs = D.gather_bytes(dist, wire, b"exotic\x00bytes")
     assert blobs == [b"exotic\x00bytes"]
+    # the library's partitioned export (the RCCL merge's send side) at world 4 on this one GPU: owner blocks in
+    # rank order, each row in the block of owner_of(key), the same rows as the table
+    prow, pcnt = ctx.export_partitioned(4)
+    pc = pcnt.cpu().tolist()
+    assert sum(pc) == U and prow.shape == (U, 3)
+    own = D.owner_of(prow[:, 0], 4).cpu().numpy()
+    assert np.array_equal(own, np.repeat(np.arange(4), pc))
+    pr = prow.cpu().numpy()
+    assert np.array_equal(pr[np.lexsort(pr.T[::-1])], ref_rows[np.lexsort(ref_rows.T[::-1])])
     U2 = D.partition_merge_device(dist, wire, ctx)
     k2, c2, f2 = ctx.unique()
     assert U2 == U and np.array_equal(k2, keys) and np.array_equal(c2, counts) and np.array_equal(f2, first)

@@ -123,6 +123,57 @@ def test_partition_exchange_gloo(world, seed):  # dist.exchange, as partition_me
     assert all(t == len(want) for _, _, t in got)
 
 
+def _worker_a2a_partitioned(rank, world, port, seed, out):
+    """exchange_partitioned's side of the RCCL merge: rows already in owner blocks (what
+    fr_export_partitioned_device writes; here sorted by owner_of on the host) with per-owner counts."""
+    from frender_amd.dist import exchange_partitioned, owner_of, reduce_sum
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    table = _table(rank, seed)
+    rows = torch.tensor([[k, c, f] for k, (c, f) in sorted(table.items())], dtype=torch.int64).reshape(-1, 3)
+    own = owner_of(rows[:, 0], world)
+    order = torch.argsort(own, stable=True)
+    mine = exchange_partitioned(dist, "cpu", rows[order], torch.bincount(own, minlength=world))
+    part = {}
+    for k, c, f in mine.tolist():
+        assert int(owner_of(torch.tensor([k]), world)[0]) == rank
+        c0, f0 = part.get(k, (0, 1 << 62))
+        part[k] = (c0 + c, min(f0, f))
+    total = int(reduce_sum(dist, "cpu", [len(part)])[0])
+    out.put((rank, sorted(part.items()), total))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,seed", [(2, 8), (4, 9)])
+def test_partitioned_exchange_gloo(world, seed):
+    """dist.exchange_partitioned (the RCCL merge's all-to-all of rows in owner blocks): every code lands on
+    its owner and the union of the partitions equals the merged table."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_a2a_partitioned, args=(r, world, port, seed, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    union = {}
+    for _, items, _ in got:
+        for k, v in items:
+            assert k not in union
+            union[k] = v
+    want = {}
+    for r in range(world):
+        for k, (c, f) in _table(r, seed).items():
+            c0, f0 = want.get(k, (0, 1 << 62))
+            want[k] = (c0 + c, min(f0, f))
+    assert union == want
+    assert all(t == len(want) for _, _, t in got)
+
+
 def _worker_census(rank, world, port, out):
     from frender_amd import dist as D
     os.environ["MASTER_ADDR"] = "127.0.0.1"

@@ -605,9 +605,10 @@ static int launch_range(fr_ctx* ctx, const u8* dptr, u64 len, u64 avail, int own
     a.cold = ctx->cold;
     // launch-log first occurrences fold in 32 bits (4-B ordinals: ranges up to RANGE_MAX); one aggregation's
     // distinct codes must fit its LDS fold, which fr_feed_device's range size sees to
-    a.log = exo_only ? nullptr : ctx->log;
-    a.log_cap = ctx->log_cap;
-    a.log_rcap = ctx->log_rcap;
+    // (direct logging: the commits append to the sub-region parts, log_scap entries each)
+    a.log = exo_only ? nullptr : LOG_DIRECT ? ctx->log_sub : ctx->log;
+    a.log_cap = LOG_DIRECT ? (u64)ctx->log_scap * LOG_NSUB : ctx->log_cap;
+    a.log_rcap = LOG_DIRECT ? ctx->log_scap : ctx->log_rcap;
     a.log_min = ctx->log_min;
     a.log_hot = ctx->log_hot;
     a.rare = ctx->rare;
@@ -713,7 +714,8 @@ fr_ctx* fr_create_tuned(int device, uint64_t chunk_bytes, uint64_t table_slots, 
         ctx->log_rcap = (u32)(want / LOG_NR);
         ctx->log_cap = (u64)ctx->log_rcap * LOG_NR;
         ctx->log_scap = (u32)std::max<u64>(2ull * ctx->log_rcap / LOG_SUBS, 64);  // 2x the mean share
-        if ((e = dalloc(&ctx->log, ctx->log_cap)) != hipSuccess) return bad("launch log", e);
+        // (direct logging: the commits fill the sub-region parts, no region parts)
+        if (!LOG_DIRECT && (e = dalloc(&ctx->log, ctx->log_cap)) != hipSuccess) return bad("launch log", e);
         if ((e = dalloc(&ctx->log_sub, (u64)ctx->log_scap * LOG_NSUB)) != hipSuccess) return bad("launch log parts", e);
     }
     ctx->tiles_cap = RANGE_MAX / TSTEP + 2;

@@ -24,7 +24,7 @@ constexpr int TSTEP = TILE - SEG;    // tile stride: tiles overlap by one segmen
 constexpr int LOG_NS = FR_LOG_NS;
 constexpr int NS = 1 << LOG_NS;      // LDS hash slots per workgroup
 #ifndef FR_LPROBE
-#define FR_LPROBE 4
+#define FR_LPROBE 2
 #endif
 constexpr int LPROBE = FR_LPROBE;          // LDS probe bound before going to HBM directly
 constexpr int GPROBE = 256;          // HBM probe bound before the overflow list
@@ -108,6 +108,13 @@ constexpr int LOG_NR = 1 << LOG_REGION_BITS;  // launch-log regions (parts of th
 constexpr int LOG_SUB_BITS = FR_LOG_SUB_BITS;
 constexpr int LOG_SUBS = 1 << LOG_SUB_BITS;   // sub-regions per region (aggregation workgroups)
 constexpr int LOG_NSUB = LOG_NR * LOG_SUBS;    // sub-regions in all
+#ifndef FR_LOG_DIRECT
+#define FR_LOG_DIRECT 1
+#endif
+// round 6: commits append straight to the sub-region parts (LOG_NSUB runs per commit, no split pass);
+// 0 = the region runs + split pass of rounds 4-5 (A/B builds)
+constexpr bool LOG_DIRECT = FR_LOG_DIRECT != 0;
+constexpr int LOG_NB = LOG_DIRECT ? LOG_NSUB : LOG_NR;  // a commit's log buckets
 constexpr int AGG_LNS = 4096;  // LDS slots of one sub-region's fold in log_reduce_kernel (64 KB: 2 workgroups per CU)
 
 struct DevState {
@@ -196,8 +203,8 @@ struct ScanArgs {
     uint4* rare;         // chunk kernel: rare-event rings, [grid][RARE_RING] (fr_kernels.hip)
     u64* chunk_info;     // chunk kernel: per chunk {line count, spec flag + guessed phase << 1 in the high word}
     LogEntry* log;       // the launch log (nullptr: commits insert into the HBM table directly)
-    u64 log_cap;         // LOG_NR x log_rcap
-    u32 log_rcap;        // entries per region (a run past it inserts directly)
+    u64 log_cap;         // LOG_NB x log_rcap
+    u32 log_rcap;        // entries per log bucket (a run past it inserts directly)
     u32 log_min;         // a commit of at least log_min pairs goes to the log, smaller ones straight into the table
     u32 log_hot;         // ... except its LDS entries of at least log_hot records, which insert directly
     u32 exo_only;        // replay of a launch whose exotic list overflowed: capture exotic records only (no
@@ -279,6 +286,10 @@ __host__ __device__ inline u64 mix64(u64 x) {
 // launch-log region of a code: the top bits of mix64, as the table's home slot, so a region's codes
 // live in one contiguous part of a table of at least LOG_NR slots
 __host__ __device__ inline u32 log_region(u64 key) { return (u32)(mix64(key) >> (64 - LOG_REGION_BITS)); }
+// a commit's log bucket: the region, or with LOG_DIRECT the region and sub-region (region * LOG_SUBS + sub)
+__host__ __device__ inline u32 log_bucket(u64 key) {
+    return (u32)(mix64(key) >> (64 - LOG_REGION_BITS - (LOG_DIRECT ? LOG_SUB_BITS : 0)));
+}
 __host__ __device__ inline u32 log_subregion(u64 key) {
     return (u32)(mix64(key) >> (64 - LOG_REGION_BITS - LOG_SUB_BITS)) & (LOG_SUBS - 1);
 }

@@ -1036,18 +1036,19 @@ __device__ __attribute__((noinline)) void commit_buffers(ScanShared& sh, const S
     const u64* cl = a.cold + 2ull * (u64)blockIdx.x * a.cold_cap;
     // LDS scratch of the logged commit (the walks are done): per-region run counters
     u32* rcnt = &sh.raw[0][0];
-    u32* rcur = rcnt + LOG_NR;
-    u32* rbase = rcur + LOG_NR;  // each region's run start in its part of the log
-    static_assert(3 * LOG_NR * 4 <= sizeof(sh.raw), "log region scratch");
+    u32* rcur = rcnt + LOG_NB;
+    u32* rbase = rcur + LOG_NB;  // each bucket's run start in its part of the log
+    static_assert(3 * LOG_NB * 4 <= sizeof(sh.raw), "log bucket scratch");
+    u32* bcur = LOG_DIRECT ? a.st->log_scur : a.st->log_rcur;  // the buckets' cursors (sub-regions or regions)
     constexpr int CB = 8;  // cold entries per lane with their loads in flight together
     // a logged commit sends its hot codes (chunk count >= log_hot: few per chunk, their slots L2-warm)
     // straight to the table; the tail goes to the log, one run per region appended to the region's part
     if (a.log && nl + nc && nl + nc >= a.log_min) {
-        for (int i = tid; i < LOG_NR; i += WG) rcnt[i] = rcur[i] = 0;
+        for (int i = tid; i < LOG_NB; i += WG) rcnt[i] = rcur[i] = 0;
         __syncthreads();
         for (int i = tid; i < NS; i += WG) {
             const LSlot e = sh.ls[i];
-            if (e.key && e.cnt < a.log_hot) atomicAdd(&rcnt[log_region(e.key)], 1u);
+            if (e.key && e.cnt < a.log_hot) atomicAdd(&rcnt[log_bucket(e.key)], 1u);
         }
         for (u32 i0 = tid; i0 < nc; i0 += CB * WG) {
             u64 k[CB];
@@ -1055,25 +1056,25 @@ __device__ __attribute__((noinline)) void commit_buffers(ScanShared& sh, const S
             for (int q = 0; q < CB; ++q) k[q] = i0 + q * WG < nc ? cl[2 * (i0 + q * WG)] : 0ull;
 #pragma unroll
             for (int q = 0; q < CB; ++q)
-                if (i0 + q * WG < nc) atomicAdd(&rcnt[log_region(k[q])], 1u);
+                if (i0 + q * WG < nc) atomicAdd(&rcnt[log_bucket(k[q])], 1u);
         }
         if (tid == 0) sh.log_on = 0;
         __syncthreads();
         FR_CSTAMP(1);
         {  // one claim per region with a run, all in flight together
-            constexpr int PR = (LOG_NR + WG - 1) / WG;
+            constexpr int PR = (LOG_NB + WG - 1) / WG;
             u32 n[PR], base[PR], tot = 0;
 #pragma unroll
             for (int j = 0; j < PR; ++j) {
                 const int r = tid + j * WG;
-                n[j] = r < LOG_NR ? rcnt[r] : 0u;
+                n[j] = r < LOG_NB ? rcnt[r] : 0u;
                 tot += n[j];
             }
 #pragma unroll
-            for (int j = 0; j < PR; ++j) base[j] = n[j] ? atomicAdd(&a.st->log_rcur[tid + j * WG], n[j]) : 0u;
+            for (int j = 0; j < PR; ++j) base[j] = n[j] ? atomicAdd(&bcur[tid + j * WG], n[j]) : 0u;
 #pragma unroll
             for (int j = 0; j < PR; ++j)
-                if (tid + j * WG < LOG_NR) rbase[tid + j * WG] = base[j];
+                if (tid + j * WG < LOG_NB) rbase[tid + j * WG] = base[j];
             if (tot) atomicAdd(&sh.log_on, tot);
         }
         __syncthreads();
@@ -1094,7 +1095,7 @@ __device__ __attribute__((noinline)) void commit_buffers(ScanShared& sh, const S
         // a pair past its region's end inserts directly (the region's claimed range up to its end is
         // always written: the aggregation reads min(cursor, log_rcap) entries)
         auto put = [&](u64 k, u64 off, u32 cnt) {
-            const u32 r = log_region(k);
+            const u32 r = log_bucket(k);
             const u64 pos = (u64)rbase[r] + atomicAdd(&rcur[r], 1u);
             const bool fits = cnt <= LOG_CNT_MAX;  // (a chunk holds fewer records unless its geometry is extreme)
             if (pos < a.log_rcap) a.log[(u64)r * a.log_rcap + pos] = fits ? LogEntry{k, log_pack(off, cnt)} : LogEntry{0, 0};
@@ -2357,8 +2358,9 @@ hipError_t launch_log_aggregate(Table t, DevState* st, const LogEntry* log, u32 
     // reads log_n on the device and returns at once when no commit logged (the usual case for
     // low-cardinality runs: only commits of at least ScanArgs::log_min pairs log)
     const u64 ord0 = ((u64)file_tag << ORD_SHIFT) | file_offset;
-    hipLaunchKernelGGL(log_split_kernel, dim3(LOG_NR * SPLIT_WGS), dim3(256), 0, s, t, st, log, rcap, sub, scap, file_tag,
-                       ord0);
+    if (!LOG_DIRECT)  // (direct logging: the commits wrote the sub-region parts)
+        hipLaunchKernelGGL(log_split_kernel, dim3(LOG_NR * SPLIT_WGS), dim3(256), 0, s, t, st, log, rcap, sub, scap,
+                           file_tag, ord0);
     hipLaunchKernelGGL(log_reduce_kernel, dim3(LOG_NSUB), dim3(RED_WG), 0, s, t, st, sub, scap, file_tag, ord0);
     return hipGetLastError();  // log_reduce_kernel's last block emptied the log
 }

@@ -68,7 +68,8 @@ struct fr_ctx {
     DevState* st = nullptr;
     DevState* h_st = nullptr;      // pinned snapshot
     DevState* h_zero = nullptr;    // pinned reset image (zero counters, no error), never modified
-    u8* h_byte = nullptr;          // pinned: a device feed's last byte, copied with the feed's state read
+    u8* h_byte = nullptr;          // pinned: a device feed's last byte (copied with the feed's state read), and at
+                                   // bytes 8-15 fr_classify's error flag
     // fr_finalize returns without a host round trip; its live-count check and timing settle at the
     // next call that synchronises (settle_finalize)
     u64* h_fin = nullptr;          // pinned: the finalize's live-slot count
@@ -1580,9 +1581,11 @@ int fr_classify(fr_ctx* ctx, int num_subs, int rc_mode, int16_t* m1, int16_t* m2
     if (timed) CK(hipEventRecord(e0, ctx->stream));
     CK(launch_classify(ctx->d_keys_s, ctx->d_counts_s, n, sh, num_subs, rc_mode ? 1 : 0, o, ctx->nbr, ctx->stream));
     if (timed) CK(hipEventRecord(e1, ctx->stream));
-    u64 ef = ~0ull;
-    CK(hipMemcpyAsync(&ef, ctx->d_errf, 8, hipMemcpyDeviceToHost, ctx->stream));  // ~index, 0 none
+    // (into pinned memory: a pageable destination makes the copy a staged, synchronous one)
+    CK(hipMemcpyAsync(ctx->h_byte + 8, ctx->d_errf, 8, hipMemcpyDeviceToHost, ctx->stream));  // ~index, 0 none
     CK(hipStreamSynchronize(ctx->stream));
+    u64 ef;
+    std::memcpy(&ef, ctx->h_byte + 8, 8);
     ef = ~ef;  // the kernel kept ~(first error index): 0 -> ~0, none
     if (int src = settle_finalize(ctx)) return src;  // landed with the classify: no extra round trip
     float ms = 0;

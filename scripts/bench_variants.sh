@@ -1,6 +1,6 @@
 #!/bin/bash
 # On-box A/B of bench.py variants, interleaved rounds (box-to-box and run-to-run drift hits every variant alike).
-#   VARIANTS: newline-separated "label|bench.py arguments[|library suffix]" (e.g. "logall|--tuning log_min=0",
+#   VARIANTS: newline-separated "label|bench.py arguments[|library suffix[|environment assignments]]" (e.g. "logall|--tuning log_min=0",
 #             "noins|--tuning log_min=0|noins" runs frender_amd/libfrender_hip_exp_noins.so: scripts/build_exp.sh)
 #   ROUNDS (default 2), STEPS (10), OUT (gpurun_out/variants.jsonl), TIMEOUT per run (240 s)
 # Every run: --no-cpu; a run that fails or times out ends the script (nothing more runs on the GPU).
@@ -9,11 +9,11 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out
 OUT=${OUT:-gpurun_out/variants.jsonl}
 : > "$OUT"
 for r in $(seq 1 "${ROUNDS:-2}"); do
-  while IFS='|' read -r label args libs; do
+  while IFS='|' read -r label args libs envs; do
     [[ -z "$label" ]] && continue
     lib=frender_amd/libfrender_hip.so
     [[ -n "${libs:-}" ]] && lib=frender_amd/libfrender_hip_exp_${libs}.so
-    FRENDER_HIP_LIB=$(pwd)/$lib timeout -k 10 "${TIMEOUT:-240}" python bench.py --steps "${STEPS:-10}" --warmup 2 \
+    env ${envs:-} FRENDER_HIP_LIB=$(pwd)/$lib timeout -k 10 "${TIMEOUT:-240}" python bench.py --steps "${STEPS:-10}" --warmup 2 \
         --no-cpu $args > gpurun_out/variant_run.log 2>&1
     rc=$?
     if [[ $rc -ne 0 ]]; then echo "variant $label failed ($rc)"; tail -20 gpurun_out/variant_run.log; exit $rc; fi

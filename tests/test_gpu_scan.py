@@ -189,6 +189,28 @@ def test_launch_log_commits(lib, log_min, log_hot):
             c.close()
 
 
+def test_launch_log_parts_full(lib):
+    """A launch whose commits log more pairs than a sub-region part holds: with chunk_bytes 16 MiB the log
+    has its minimum of 65 536 entries, 256 per sub-region part (fr_api.hip), while one 16-MiB launch of
+    34-B records over 300 000 codes logs ~450 000 pairs, ~900 per part.  The pairs past a part's end insert
+    straight into the table (commit_buffers' put) during the tally, the rest through the aggregation's
+    plain-store inserts afterwards -- mixed on the same codes -- and the tally must equal the oracle's."""
+    rng = random.Random(11)
+    pool = ["".join(rng.choice("ACGT") for _ in range(8)) + "+" + "".join(rng.choice("ACGT") for _ in range(8))
+            for _ in range(300_000)]
+    files = []
+    for f in range(2):
+        recs = [f"@r{f} 1:N:0:{pool[rng.randrange(len(pool))]}\nA\n+\nI\n" for _ in range(480_000)]
+        files.append("".join(recs).encode())
+    assert all(len(d) < 16 << 20 for d in files)
+    exp = oracle_tally(files)
+    c = lib.Context(device=0, chunk_bytes=16 << 20, table_slots=1 << 21, tuning={"log_min": 0})
+    try:
+        assert_same(gpu_tally(c, lib, files, mode="device"), exp)
+    finally:
+        c.close()
+
+
 def test_heavy_chunk_switch(lib):
     """Ramped launches switch to the heavy chunk size once at least a quarter of the chunks since the
     reset logged their commits; the device decides at the end of each launch for the next one
